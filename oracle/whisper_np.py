@@ -1,0 +1,673 @@
+"""numpy restatement of the streaming-Whisper hot path (TEST INFRASTRUCTURE ONLY).
+
+See ``oracle/__init__.py`` for scope and pinning.  Every function cites what it
+restates.  Arithmetic is float32 (log-mel float64), i.e. the exact-math
+reference the bf16/fp16 HIP path is compared against.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+from scipy.special import erf
+
+SAMPLE_RATE = 16000
+N_FFT = 400
+HOP = 160
+N_SAMPLES = 480000          # 30 s window
+N_FRAMES = 3000             # mel frames per window
+N_AUDIO_CTX = 1500          # encoder positions
+N_TEXT_CTX = 448
+
+
+# ----------------------------------------------------------------------------------------------
+# model dimensions (openai-whisper ModelDimensions; CT2 converted models carry the same numbers)
+# ----------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class Dims:
+    n_mels: int
+    n_vocab: int
+    n_audio_state: int
+    n_audio_head: int
+    n_audio_layer: int
+    n_text_state: int
+    n_text_head: int
+    n_text_layer: int
+    n_audio_ctx: int = N_AUDIO_CTX
+    n_text_ctx: int = N_TEXT_CTX
+
+
+DIMS = {
+    "tiny": Dims(80, 51865, 384, 6, 4, 384, 6, 4),
+    "base": Dims(80, 51865, 512, 8, 6, 512, 8, 6),
+    "small": Dims(80, 51865, 768, 12, 12, 768, 12, 12),
+    "medium": Dims(80, 51865, 1024, 16, 24, 1024, 16, 24),
+    "large-v3": Dims(128, 51866, 1280, 20, 32, 1280, 20, 32),
+    "large-v3-turbo": Dims(128, 51866, 1280, 20, 32, 1280, 20, 4),
+    # a deliberately small configuration for fast parity tests (not a released model)
+    "micro": Dims(80, 51865, 128, 2, 2, 128, 2, 2),
+}
+
+
+# ----------------------------------------------------------------------------------------------
+# special tokens (openai-whisper tokenizer.py; faster-whisper Tokenizer wraps the same ids)
+# ----------------------------------------------------------------------------------------------
+LANGUAGES = [
+    "en", "zh", "de", "es", "ru", "ko", "fr", "ja", "pt", "tr", "pl", "ca", "nl", "ar", "sv", "it",
+    "id", "hi", "fi", "vi", "he", "uk", "el", "ms", "cs", "ro", "da", "hu", "ta", "no", "th", "ur",
+    "hr", "bg", "lt", "la", "mi", "ml", "cy", "sk", "te", "fa", "lv", "bn", "sr", "az", "sl", "kn",
+    "et", "mk", "br", "eu", "is", "hy", "ne", "mn", "bs", "kk", "sq", "sw", "gl", "mr", "pa", "si",
+    "km", "sn", "yo", "so", "af", "oc", "ka", "be", "tg", "sd", "gu", "am", "yi", "lo", "uz", "fo",
+    "ht", "ps", "tk", "nn", "mt", "sa", "lb", "my", "bo", "tl", "mg", "as", "tt", "haw", "ln", "ha",
+    "ba", "jw", "su", "yue",
+]
+
+
+@dataclass(frozen=True)
+class Special:
+    eot: int
+    sot: int
+    lang0: int
+    n_langs: int
+    translate: int
+    transcribe: int
+    sot_lm: int
+    sot_prev: int
+    no_speech: int
+    no_timestamps: int
+    timestamp_begin: int
+    blank: int = 220  # " " in the GPT-2 byte-level BPE
+
+
+def special_tokens(n_vocab: int) -> Special:
+    """openai-whisper tokenizer: large-v3 (51866) adds "yue" and shifts every id after the languages by one."""
+    n_langs = 100 if n_vocab >= 51866 else 99
+    base = 50258 + 1 + n_langs  # first id after the language tokens
+    return Special(eot=50257, sot=50258, lang0=50259, n_langs=n_langs, translate=base,
+                   transcribe=base + 1, sot_lm=base + 2, sot_prev=base + 3, no_speech=base + 4,
+                   no_timestamps=base + 5, timestamp_begin=base + 6)
+
+
+# ----------------------------------------------------------------------------------------------
+# build-owned deterministic weight PRNG (same algorithm as csrc/wmx_weights.hip)
+# ----------------------------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+_G1 = 0x9E3779B97F4A7C15
+_G2 = 0xBF58476D1CE4E5B9
+_G3 = 0x94D049BB133111EB
+
+
+def prng_uniform(seed: int, tid: int, n: int) -> np.ndarray:
+    """u in [-1, 1) for element indices 0..n-1 of tensor `tid`: splitmix64 of a counter, top 24 bits."""
+    key = np.uint64((seed * _G1 + tid * _G2) & _M64)
+    z = np.arange(n, dtype=np.uint64) + key
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(_G2)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(_G3)
+        z = z ^ (z >> np.uint64(31))
+    k = (z >> np.uint64(40)).astype(np.float32)  # < 2^24, exact
+    return k * np.float32(2.0 ** -23) - np.float32(1.0)  # exact in fp32
+
+
+def round_bf16(x: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + np.uint64(0x7FFF) + ((u >> np.uint64(16)) & np.uint64(1))) >> np.uint64(16)) << np.uint64(16)
+    return r.astype(np.uint32).view(np.float32)
+
+
+def round_dtype(x: np.ndarray, dtype: str) -> np.ndarray:
+    if dtype == "bf16":
+        return round_bf16(x)
+    if dtype == "f16":
+        return x.astype(np.float16).astype(np.float32)
+    return x.astype(np.float32)
+
+
+def tensor_specs(d: Dims):
+    """(name, logical shape, scale, offset) in generation order; tid = index in this list.
+
+    Names follow the HF/openai state-dict naming so a real checkpoint maps 1:1."""
+    specs = []
+    f32 = lambda v: float(np.float32(v))
+
+    def lin(p, n_out, n_in, bias=True):
+        specs.append((p + ".weight", (n_out, n_in), f32(1.0 / math.sqrt(n_in)), 0.0))
+        if bias:
+            specs.append((p + ".bias", (n_out,), 0.02, 0.0))
+
+    def ln(p, n):
+        specs.append((p + ".weight", (n,), 0.1, 1.0))
+        specs.append((p + ".bias", (n,), 0.02, 0.0))
+
+    def attn(p, n):
+        lin(p + ".q_proj", n, n)
+        lin(p + ".k_proj", n, n, bias=False)
+        lin(p + ".v_proj", n, n)
+        lin(p + ".out_proj", n, n)
+
+    da, dt = d.n_audio_state, d.n_text_state
+    specs.append(("encoder.conv1.weight", (da, d.n_mels, 3), f32(1.0 / math.sqrt(3 * d.n_mels)), 0.0))
+    specs.append(("encoder.conv1.bias", (da,), 0.02, 0.0))
+    specs.append(("encoder.conv2.weight", (da, da, 3), f32(1.0 / math.sqrt(3 * da)), 0.0))
+    specs.append(("encoder.conv2.bias", (da,), 0.02, 0.0))
+    for i in range(d.n_audio_layer):
+        p = f"encoder.layers.{i}"
+        ln(p + ".self_attn_layer_norm", da)
+        attn(p + ".self_attn", da)
+        ln(p + ".final_layer_norm", da)
+        lin(p + ".fc1", 4 * da, da)
+        lin(p + ".fc2", da, 4 * da)
+    ln("encoder.layer_norm", da)
+    specs.append(("decoder.embed_tokens.weight", (d.n_vocab, dt), f32(6.0 / math.sqrt(dt)), 0.0))
+    specs.append(("decoder.embed_positions.weight", (d.n_text_ctx, dt), 0.05, 0.0))
+    for i in range(d.n_text_layer):
+        p = f"decoder.layers.{i}"
+        ln(p + ".self_attn_layer_norm", dt)
+        attn(p + ".self_attn", dt)
+        ln(p + ".encoder_attn_layer_norm", dt)
+        attn(p + ".encoder_attn", dt)
+        ln(p + ".final_layer_norm", dt)
+        lin(p + ".fc1", 4 * dt, dt)
+        lin(p + ".fc2", dt, 4 * dt)
+    ln("decoder.layer_norm", dt)
+    return specs
+
+
+def make_weights(d: Dims, seed: int, dtype: str = "bf16") -> dict:
+    """Deterministic synthetic weights, value = u*scale + offset (separately rounded fp32 ops), then
+    rounded to the storage dtype.  Returns float32 arrays holding the stored values."""
+    W = {}
+    for tid, (name, shape, scale, offset) in enumerate(tensor_specs(d)):
+        n = int(np.prod(shape))
+        u = prng_uniform(seed, tid, n)
+        v = u * np.float32(scale)
+        if offset != 0.0:
+            v = v + np.float32(offset)
+        W[name] = round_dtype(v, dtype).reshape(shape)
+    W["encoder.embed_positions.weight"] = sinusoids(d.n_audio_ctx, d.n_audio_state)
+    return W
+
+
+def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> np.ndarray:
+    """openai-whisper model.sinusoids (transformers modeling_whisper.py:55), evaluated in float64."""
+    inc = math.log(max_timescale) / (channels // 2 - 1)
+    inv = np.exp(-inc * np.arange(channels // 2, dtype=np.float64))
+    t = np.arange(length, dtype=np.float64)[:, None] * inv[None, :]
+    return np.concatenate([np.sin(t), np.cos(t)], axis=1).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------------------------
+# log-mel (faster-whisper 1.2.1 feature_extractor.py FeatureExtractor.__call__, padding=160)
+# ----------------------------------------------------------------------------------------------
+def mel_filters(n_mels: int, sr: int = SAMPLE_RATE, n_fft: int = N_FFT) -> np.ndarray:
+    """faster-whisper FeatureExtractor.get_mel_filters: slaney-scale triangles, slaney norm."""
+    fftfreqs = np.fft.rfftfreq(n=n_fft, d=1.0 / sr)
+    mels = np.linspace(0.0, 45.245640471924965, n_mels + 2)
+    f_sp = 200.0 / 3
+    freqs = f_sp * mels
+    min_log_hz = 1000.0
+    min_log_mel = min_log_hz / f_sp
+    logstep = np.log(6.4) / 27.0
+    log_t = mels >= min_log_mel
+    freqs[log_t] = min_log_hz * np.exp(logstep * (mels[log_t] - min_log_mel))
+    fdiff = np.diff(freqs)
+    ramps = freqs.reshape(-1, 1) - fftfreqs.reshape(1, -1)
+    lower = -ramps[:-2] / fdiff[:-1].reshape(-1, 1)
+    upper = ramps[2:] / fdiff[1:].reshape(-1, 1)
+    weights = np.maximum(0.0, np.minimum(lower, upper))
+    enorm = 2.0 / (freqs[2: n_mels + 2] - freqs[:n_mels])
+    return weights * enorm[:, None]
+
+
+def reflect_index(idx: np.ndarray, n: int) -> np.ndarray:
+    """numpy 'reflect' padding index map (iterated reflection = periodic mirror, period 2(n-1))."""
+    if n == 1:
+        return np.zeros_like(idx)
+    p = 2 * (n - 1)
+    m = np.mod(idx, p)
+    return np.where(m < n, m, p - m)
+
+
+def logmel_frames(audio: np.ndarray, n_mels: int) -> np.ndarray:
+    """Un-normalised log10 mel for faster-whisper's framing: audio + 160 zeros, centre reflect pad,
+    periodic Hann 400, hop 160, |rfft|^2, drop last frame.  Returns [n_mels, F], F = N//160 + 1."""
+    x = np.concatenate([np.asarray(audio, dtype=np.float64), np.zeros(HOP)])
+    L = x.shape[0]
+    n_frames = 1 + L // HOP
+    idx = np.arange(n_frames)[:, None] * HOP + np.arange(N_FFT)[None, :] - N_FFT // 2
+    frames = x[reflect_index(idx, L)]
+    window = 0.5 - 0.5 * np.cos(2.0 * np.pi * np.arange(N_FFT) / N_FFT)
+    spec = np.fft.rfft(frames * window[None, :], axis=-1)
+    power = (spec.real ** 2 + spec.imag ** 2)[:-1]  # drop last frame -> [F, 201]
+    mel = power @ mel_filters(n_mels).T
+    return np.log10(np.maximum(mel, 1e-10)).T  # [M, F]
+
+
+def logmel(audio: np.ndarray, n_mels: int) -> np.ndarray:
+    """faster-whisper FeatureExtractor(...)(audio): normalised features [n_mels, N//160 + 1]."""
+    lm = logmel_frames(audio, n_mels)
+    lm = np.maximum(lm, lm.max() - 8.0)
+    return ((lm + 4.0) / 4.0).astype(np.float32)
+
+
+def logmel_segment(audio: np.ndarray, n_mels: int, seek: int = 0) -> np.ndarray:
+    """The encoder input of one window, faster-whisper generate_segments: content_frames = F - 1,
+    segment = features[:, seek : seek + min(3000, content_frames - seek)], pad_or_trim to 3000."""
+    feats = logmel(audio, n_mels)
+    content = feats.shape[1] - 1
+    size = max(0, min(N_FRAMES, content - seek))
+    seg = np.zeros((n_mels, N_FRAMES), dtype=np.float32)
+    seg[:, :size] = feats[:, seek: seek + size]
+    return seg
+
+
+# ----------------------------------------------------------------------------------------------
+# transformer blocks
+# ----------------------------------------------------------------------------------------------
+def gelu(x):
+    return (0.5 * x * (1.0 + erf(x / np.float32(math.sqrt(2.0))))).astype(np.float32)
+
+
+def layer_norm(x, g, b, eps=1e-5):
+    mu = x.mean(-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(-1, keepdims=True)
+    return ((x - mu) / np.sqrt(var + eps) * g + b).astype(np.float32)
+
+
+def linear(x, W, p, bias=True):
+    y = x @ W[p + ".weight"].T
+    if bias:
+        y = y + W[p + ".bias"]
+    return y.astype(np.float32)
+
+
+def softmax(x, axis=-1):
+    m = np.max(x, axis=axis, keepdims=True)
+    e = np.exp(x - m)
+    return e / e.sum(axis=axis, keepdims=True)
+
+
+def mha(q, k, v, n_head, mask=None, return_probs=False):
+    """q [Tq,d], k/v [Tk,d]; softmax(q k^T / sqrt(dh)) v per head."""
+    Tq, dm = q.shape
+    dh = dm // n_head
+    qh = q.reshape(Tq, n_head, dh).transpose(1, 0, 2)
+    kh = k.reshape(-1, n_head, dh).transpose(1, 0, 2)
+    vh = v.reshape(-1, n_head, dh).transpose(1, 0, 2)
+    s = (qh @ kh.transpose(0, 2, 1)) * np.float32(dh ** -0.5)
+    if mask is not None:
+        s = s + mask
+    p = softmax(s, -1).astype(np.float32)
+    o = (p @ vh).transpose(1, 0, 2).reshape(Tq, dm).astype(np.float32)
+    return (o, s) if return_probs else o
+
+
+def conv1d_k3(x, w, b, stride):
+    """x [C,T], w [O,C,3], padding 1."""
+    C, T = x.shape
+    xp = np.pad(x, ((0, 0), (1, 1)))
+    Tout = (T + 2 - 3) // stride + 1
+    cols = np.stack([xp[:, k: k + stride * (Tout - 1) + 1: stride] for k in range(3)], axis=0)  # [3,C,Tout]
+    y = np.einsum("ock,kct->ot", w, cols, optimize=True) + b[:, None]
+    return y.astype(np.float32)
+
+
+def encoder(W, d: Dims, mel: np.ndarray) -> np.ndarray:
+    """WhisperEncoder.forward (modeling_whisper.py:592): conv-GELU x2, + sinusoid, L pre-LN blocks, LN."""
+    x = gelu(conv1d_k3(mel.astype(np.float32), W["encoder.conv1.weight"], W["encoder.conv1.bias"], 1))
+    x = gelu(conv1d_k3(x, W["encoder.conv2.weight"], W["encoder.conv2.bias"], 2))
+    x = (x.T + W["encoder.embed_positions.weight"][: x.shape[1]]).astype(np.float32)
+    for i in range(d.n_audio_layer):
+        p = f"encoder.layers.{i}"
+        h = layer_norm(x, W[p + ".self_attn_layer_norm.weight"], W[p + ".self_attn_layer_norm.bias"])
+        q = linear(h, W, p + ".self_attn.q_proj")
+        k = linear(h, W, p + ".self_attn.k_proj", bias=False)
+        v = linear(h, W, p + ".self_attn.v_proj")
+        x = x + linear(mha(q, k, v, d.n_audio_head), W, p + ".self_attn.out_proj")
+        h = layer_norm(x, W[p + ".final_layer_norm.weight"], W[p + ".final_layer_norm.bias"])
+        x = x + linear(gelu(linear(h, W, p + ".fc1")), W, p + ".fc2")
+    return layer_norm(x, W["encoder.layer_norm.weight"], W["encoder.layer_norm.bias"])
+
+
+class DecoderCache:
+    """Per-sequence self-attention KV cache + the window's cross K/V (openai-whisper kv_cache)."""
+
+    def __init__(self, W, d: Dims, enc: np.ndarray):
+        self.d = d
+        self.k = [np.zeros((0, d.n_text_state), np.float32) for _ in range(d.n_text_layer)]
+        self.v = [np.zeros((0, d.n_text_state), np.float32) for _ in range(d.n_text_layer)]
+        self.ck, self.cv = [], []
+        for i in range(d.n_text_layer):
+            p = f"decoder.layers.{i}.encoder_attn"
+            self.ck.append(linear(enc, W, p + ".k_proj", bias=False))
+            self.cv.append(linear(enc, W, p + ".v_proj"))
+
+    @property
+    def length(self):
+        return self.k[0].shape[0]
+
+    def copy(self):
+        c = DecoderCache.__new__(DecoderCache)
+        c.d, c.ck, c.cv = self.d, self.ck, self.cv
+        c.k = [a.copy() for a in self.k]
+        c.v = [a.copy() for a in self.v]
+        return c
+
+
+def decoder_forward(W, d: Dims, tokens, cache: DecoderCache, align_heads=None):
+    """WhisperDecoder.forward (modeling_whisper.py:690) for new `tokens` appended after the cache.
+    Returns logits [T, V] (and cross-attention pre-softmax scores of `align_heads` as [n, T, 1500])."""
+    tokens = np.asarray(tokens, dtype=np.int64)
+    T = tokens.shape[0]
+    off = cache.length
+    x = (W["decoder.embed_tokens.weight"][tokens] + W["decoder.embed_positions.weight"][off: off + T]).astype(np.float32)
+    causal = np.triu(np.full((T, off + T), -np.inf, np.float32), k=off + 1)
+    qk_store = []
+    for i in range(d.n_text_layer):
+        p = f"decoder.layers.{i}"
+        h = layer_norm(x, W[p + ".self_attn_layer_norm.weight"], W[p + ".self_attn_layer_norm.bias"])
+        q = linear(h, W, p + ".self_attn.q_proj")
+        cache.k[i] = np.concatenate([cache.k[i], linear(h, W, p + ".self_attn.k_proj", bias=False)])
+        cache.v[i] = np.concatenate([cache.v[i], linear(h, W, p + ".self_attn.v_proj")])
+        x = x + linear(mha(q, cache.k[i], cache.v[i], d.n_text_head, causal), W, p + ".self_attn.out_proj")
+        h = layer_norm(x, W[p + ".encoder_attn_layer_norm.weight"], W[p + ".encoder_attn_layer_norm.bias"])
+        q = linear(h, W, p + ".encoder_attn.q_proj")
+        o, s = mha(q, cache.ck[i], cache.cv[i], d.n_text_head, return_probs=True)
+        if align_heads is not None:
+            for (l, hh) in align_heads:
+                if l == i:
+                    qk_store.append(s[hh])
+        x = x + linear(o, W, p + ".encoder_attn.out_proj")
+        h = layer_norm(x, W[p + ".final_layer_norm.weight"], W[p + ".final_layer_norm.bias"])
+        x = x + linear(gelu(linear(h, W, p + ".fc1")), W, p + ".fc2")
+    x = layer_norm(x, W["decoder.layer_norm.weight"], W["decoder.layer_norm.bias"])
+    logits = (x @ W["decoder.embed_tokens.weight"].T).astype(np.float32)
+    if align_heads is not None:
+        return logits, np.stack(qk_store) if qk_store else np.zeros((0, T, cache.ck[0].shape[0]), np.float32)
+    return logits
+
+
+# ----------------------------------------------------------------------------------------------
+# decoding rules (openai-whisper decoding.py LogitFilters; CT2 re-implements the same rules)
+# ----------------------------------------------------------------------------------------------
+@dataclass
+class DecodeOptions:
+    task: str = "transcribe"
+    language: int | None = None          # language token id, None = detect
+    beam_size: int = 1                    # 1 = greedy (temperature 0)
+    patience: float = 1.0
+    length_penalty: float | None = None   # None/1.0 -> logprob / len (CT2 length_penalty=1)
+    max_new_tokens: int = 224
+    suppress_blank: bool = True
+    suppress_tokens: tuple = ()
+    without_timestamps: bool = False
+    max_initial_timestamp_index: int | None = 50
+
+
+def apply_rules(logits: np.ndarray, sampled: list, sp: Special, opt: DecodeOptions) -> np.ndarray:
+    """SuppressBlank -> SuppressTokens -> ApplyTimestampRules for ONE row; `sampled` = tokens generated
+    after the SOT sequence.  Returns filtered float32 logits (-inf masked)."""
+    x = logits.astype(np.float32).copy()
+    V = x.shape[0]
+    if opt.suppress_blank and len(sampled) == 0:
+        x[[sp.blank, sp.eot]] = -np.inf
+    if opt.suppress_tokens:
+        x[list(opt.suppress_tokens)] = -np.inf
+    if opt.without_timestamps:
+        x[sp.no_timestamps] = -np.inf  # the SOT sequence carries <|notimestamps|>; rules below skipped
+        return x
+    tb = sp.timestamp_begin
+    x[sp.no_timestamps] = -np.inf
+    last_ts = len(sampled) >= 1 and sampled[-1] >= tb
+    pen_ts = len(sampled) < 2 or sampled[-2] >= tb
+    if last_ts:
+        if pen_ts:
+            x[tb:] = -np.inf
+        else:
+            x[: sp.eot] = -np.inf
+    ts = [t for t in sampled if t >= tb]
+    if ts:
+        ts_last = ts[-1] if (last_ts and not pen_ts) else ts[-1] + 1
+        x[tb: ts_last] = -np.inf
+    if len(sampled) == 0:
+        x[:tb] = -np.inf
+        if opt.max_initial_timestamp_index is not None:
+            x[tb + opt.max_initial_timestamp_index + 1:] = -np.inf
+    lp = log_softmax(x)
+    ts_lp = logsumexp(lp[tb:])
+    if ts_lp > np.max(lp[:tb]):
+        x[:tb] = -np.inf
+    return x
+
+
+def log_softmax(x):
+    x = x.astype(np.float64)
+    m = np.max(x)
+    if not np.isfinite(m):
+        return np.full_like(x, -np.inf)
+    return (x - m - np.log(np.sum(np.exp(x - m)))).astype(np.float64)
+
+
+def logsumexp(x):
+    x = np.asarray(x, np.float64)
+    m = np.max(x)
+    if not np.isfinite(m):
+        return -np.inf
+    return float(m + np.log(np.sum(np.exp(x - m))))
+
+
+def sot_sequence(sp: Special, language: int, task: str, without_timestamps=False):
+    seq = [sp.sot, language, sp.translate if task == "translate" else sp.transcribe]
+    if without_timestamps:
+        seq.append(sp.no_timestamps)
+    return seq
+
+
+def build_prompt(sp: Special, prompt_ids, language, task, without_timestamps=False, max_prompt=223):
+    """faster-whisper get_prompt: [<|startofprev|>] + last (448//2 - 1) prompt ids + SOT sequence."""
+    pre = []
+    if prompt_ids:
+        pre = [sp.sot_prev] + list(prompt_ids)[-max_prompt:]
+    return pre + sot_sequence(sp, language, task, without_timestamps)
+
+
+def detect_language(W, d: Dims, enc: np.ndarray):
+    """openai-whisper detect_language / CT2 Whisper.detect_language: logits at <|startoftranscript|>,
+    restricted to language tokens.  Returns (lang_token, prob)."""
+    sp = special_tokens(d.n_vocab)
+    cache = DecoderCache(W, d, enc)
+    logits = decoder_forward(W, d, [sp.sot], cache)[0]
+    lang = logits[sp.lang0: sp.lang0 + sp.n_langs].astype(np.float64)
+    p = np.exp(lang - lang.max())
+    p /= p.sum()
+    i = int(np.argmax(lang))
+    return sp.lang0 + i, float(p[i])
+
+
+@dataclass
+class DecodeResult:
+    tokens: list          # sampled tokens (without the trailing EOT)
+    sum_logprob: float
+    avg_logprob: float    # sum_logprob / (len(tokens) + 1)  (faster-whisper generate_with_fallback)
+    no_speech_prob: float
+    language: int
+
+
+def decode(W, d: Dims, enc: np.ndarray, opt: DecodeOptions, prompt_ids=(), forced=None):
+    """Greedy (beam_size == 1) or beam search over one window.  `forced` = teacher-forced token list
+    (greedy only): the argmax/margin per step is recorded instead of being fed back."""
+    sp = special_tokens(d.n_vocab)
+    lang = opt.language
+    if lang is None:
+        lang, _ = detect_language(W, d, enc)
+    prefix = build_prompt(sp, list(prompt_ids), lang, opt.task, opt.without_timestamps)
+    sot_index = prefix.index(sp.sot)
+    base = DecoderCache(W, d, enc)
+    logits = decoder_forward(W, d, prefix, base)
+    no_speech = float(softmax(logits[sot_index].astype(np.float64))[sp.no_speech])
+    max_new = min(opt.max_new_tokens, d.n_text_ctx - len(prefix))
+    if opt.beam_size <= 1:
+        return _greedy(W, d, sp, opt, base, logits[-1], no_speech, lang, max_new, forced)
+    return _beam(W, d, sp, opt, base, logits[-1], no_speech, lang, max_new)
+
+
+def _greedy(W, d, sp, opt, cache, last_logits, no_speech, lang, max_new, forced):
+    sampled, total, trace = [], 0.0, []
+    cur = last_logits
+    for step in range(max_new):
+        x = apply_rules(cur, sampled, sp, opt)
+        lp = log_softmax(x)
+        order = np.argsort(-x, kind="stable")
+        tok = int(order[0])
+        margin = float(x[order[0]] - x[order[1]]) if np.isfinite(x[order[1]]) else np.inf
+        trace.append((tok, margin))
+        if forced is not None:
+            if step >= len(forced):
+                break
+            tok = int(forced[step])
+        total += float(lp[tok])
+        if tok == sp.eot:
+            break
+        sampled.append(tok)
+        cur = decoder_forward(W, d, [tok], cache)[0]
+    res = DecodeResult(sampled, total, total / (len(sampled) + 1), no_speech, lang)
+    res.trace = trace
+    return res
+
+
+def _beam(W, d, sp, opt, cache0, last_logits, no_speech, lang, max_new):
+    """openai-whisper BeamSearchDecoder (patience) + MaximumLikelihoodRanker; ties broken by
+    (score desc, source beam asc, token asc) — deterministic, mirrored by the HIP kernel."""
+    K = opt.beam_size
+    max_cand = int(round(K * opt.patience))
+    beams = [([], 0.0, cache0.copy(), last_logits) for _ in range(K)]
+    finished = {}
+    for step in range(max_new):
+        cands = []
+        seen = set()
+        for j, (seq, score, cache, lg) in enumerate(beams):
+            x = apply_rules(lg, seq, sp, opt)
+            lp = log_softmax(x)
+            top = np.lexsort((np.arange(lp.shape[0]), -lp))[: K + 1]
+            for t in top:
+                s = tuple(seq + [int(t)])
+                if s in seen:
+                    continue
+                seen.add(s)
+                cands.append((score + float(lp[t]), j, int(t), s))
+        cands.sort(key=lambda c: (-c[0], c[1], c[2]))
+        new_beams, new_fin = [], []
+        for sc, j, t, s in cands:
+            if t == sp.eot:
+                new_fin.append((s, sc))
+            else:
+                new_beams.append((list(s), sc, j))
+                if len(new_beams) == K:
+                    break
+        for s, sc in new_fin:
+            if len(finished) >= max_cand:
+                break
+            if s not in finished:
+                finished[s] = sc
+        if len(finished) >= max_cand or step == max_new - 1:
+            beams = [(s, sc, beams[j][2], None) for (s, sc, j) in new_beams]
+            break
+        nb = []
+        for s, sc, j in new_beams:
+            c = beams[j][2].copy()
+            lg = decoder_forward(W, d, [s[-1]], c)[0]
+            nb.append((s, sc, c, lg))
+        beams = nb
+    if len(finished) < K:
+        for s, sc, _, _ in sorted(beams, key=lambda b: -b[1]):
+            key = tuple(s) + (sp.eot,)
+            if key not in finished:
+                finished[key] = sc
+            if len(finished) >= K:
+                break
+    best, best_score, best_sum = None, -np.inf, 0.0
+    for s, sc in finished.items():
+        toks = [t for t in s if t != sp.eot]
+        L = max(len(toks), 1)  # openai ranks the sequence trimmed at EOT (decoding.py DecodingTask.run)
+        pen = L if opt.length_penalty is None else ((5 + L) / 6) ** opt.length_penalty
+        norm = sc / pen
+        if norm > best_score:
+            best, best_score, best_sum = toks, norm, sc
+    return DecodeResult(best, best_sum, best_sum / (len(best) + 1), no_speech, lang)
+
+
+# ----------------------------------------------------------------------------------------------
+# word-level alignment (openai-whisper timing.py find_alignment / faster-whisper find_alignment)
+# ----------------------------------------------------------------------------------------------
+def median_filter(x: np.ndarray, width: int) -> np.ndarray:
+    """openai timing.median_filter: reflect-pad the last axis by width//2, sliding median."""
+    pad = width // 2
+    if x.shape[-1] <= pad:
+        return x
+    xp = np.pad(x, [(0, 0)] * (x.ndim - 1) + [(pad, pad)], mode="reflect")
+    win = np.lib.stride_tricks.sliding_window_view(xp, width, axis=-1)
+    return np.sort(win, axis=-1)[..., pad]
+
+
+def dtw(cost: np.ndarray):
+    """openai timing.dtw_cpu + backtrace: returns (text_indices, time_indices)."""
+    N, M = cost.shape
+    c = np.full((N + 1, M + 1), np.inf, np.float32)
+    tr = -np.ones((N + 1, M + 1), np.float32)
+    c[0, 0] = 0
+    for j in range(1, M + 1):
+        for i in range(1, N + 1):
+            c0, c1, c2 = c[i - 1, j - 1], c[i - 1, j], c[i, j - 1]
+            if c0 < c1 and c0 < c2:
+                v, t = c0, 0
+            elif c1 < c0 and c1 < c2:
+                v, t = c1, 1
+            else:
+                v, t = c2, 2
+            c[i, j] = cost[i - 1, j - 1] + v
+            tr[i, j] = t
+    i, j = N, M
+    tr[0, :] = 2
+    tr[:, 0] = 1
+    ti, tj = [], []
+    while i > 0 or j > 0:
+        ti.append(i - 1)
+        tj.append(j - 1)
+        t = tr[i, j]
+        if t == 0:
+            i -= 1
+            j -= 1
+        elif t == 1:
+            i -= 1
+        else:
+            j -= 1
+    return np.array(ti[::-1]), np.array(tj[::-1])
+
+
+def alignment_heads_default(d: Dims):
+    """openai Whisper.alignment_heads default: every head of the second half of the decoder."""
+    return [(l, h) for l in range(d.n_text_layer // 2, d.n_text_layer) for h in range(d.n_text_head)]
+
+
+def find_alignment(W, d: Dims, enc: np.ndarray, language: int, task: str, text_tokens, num_frames: int,
+                   align_heads=None, medfilt_width: int = 7):
+    """Returns (text_indices, time_indices, text_token_probs) for sot_sequence + text + [eot]."""
+    sp = special_tokens(d.n_vocab)
+    heads = align_heads if align_heads is not None else alignment_heads_default(d)
+    sot = sot_sequence(sp, language, task)
+    tokens = sot + list(text_tokens) + [sp.eot]
+    cache = DecoderCache(W, d, enc)
+    logits, qk = decoder_forward(W, d, tokens, cache, align_heads=heads)
+    sampled = logits[len(sot) - 1: -1, : sp.eot].astype(np.float64)
+    probs = softmax(sampled, -1)
+    text_token_probs = probs[np.arange(len(text_tokens)), list(text_tokens)] if text_tokens else np.zeros(0)
+    w = qk[:, :, : num_frames // 2].astype(np.float64)
+    w = softmax(w, -1)
+    std = w.std(axis=-2, keepdims=True)
+    mean = w.mean(axis=-2, keepdims=True)
+    w = (w - mean) / std
+    w = median_filter(w, medfilt_width)
+    matrix = w.mean(axis=0)[len(sot): -1]
+    ti, tj = dtw(-matrix.astype(np.float32))
+    return ti, tj, text_token_probs
