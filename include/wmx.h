@@ -1,0 +1,170 @@
+/*
+ * wmx.h — C ABI of libwmx.so, the MI355X-native streaming-Whisper hot path.
+ *
+ * This is the drop-in boundary that replaces the faster-whisper 1.2.1 / CTranslate2 4.6.1 engine behind
+ * the reference's ASR plugin surface.  The reference binds that engine from Python:
+ *
+ *   asr_components.py:247-264  load_model()  -> faster_whisper.WhisperModel(name, device, compute_type,
+ *                                                download_root, num_workers, device_index)
+ *   asr_components.py:267-289  transcribe()  -> model.transcribe(audio, language, initial_prompt,
+ *                                                beam_size, temperature, word_timestamps=True,
+ *                                                condition_on_previous_text=True, task=...)
+ *
+ * The Python adapter wmx.asr.MI355XWhisperASR keeps that exact Python surface and calls the entry points
+ * below through ctypes.  Plain pointers and sizes only; no torch types.
+ *
+ * Conventions
+ *   - every call returns wmx_status (0 = ok); on error wmx_last_error() returns a thread-local message.
+ *   - input buffers are owned by the caller; wmx_result is owned by the library until wmx_result_free().
+ *   - one wmx_ctx per host thread / stream group; a wmx_model is read-only after init and shareable.
+ *   - "host" pointers are ordinary CPU memory; "_device" entry points take device pointers on the
+ *     context's device and do not synchronise.
+ */
+#ifndef WMX_H
+#define WMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int wmx_status;
+enum {
+  WMX_OK = 0,
+  WMX_ERR_ARG = 1,      /* bad argument / shape */
+  WMX_ERR_HIP = 2,      /* HIP runtime error */
+  WMX_ERR_STATE = 3,    /* call in the wrong state (e.g. decode before encode) */
+  WMX_ERR_NOMEM = 4,
+};
+
+enum { WMX_DTYPE_BF16 = 0, WMX_DTYPE_F16 = 1 };
+enum { WMX_TASK_TRANSCRIBE = 0, WMX_TASK_TRANSLATE = 1 };
+
+typedef struct wmx_model wmx_model;
+typedef struct wmx_ctx wmx_ctx;
+
+/* openai-whisper ModelDimensions (what a CT2 / HF checkpoint's config.json carries). */
+typedef struct {
+  int32_t n_mels;
+  int32_t n_vocab;
+  int32_t n_audio_ctx;   /* 1500 */
+  int32_t n_audio_state;
+  int32_t n_audio_head;
+  int32_t n_audio_layer;
+  int32_t n_text_ctx;    /* 448 */
+  int32_t n_text_state;
+  int32_t n_text_head;
+  int32_t n_text_layer;
+} wmx_dims;
+
+/* decoding options — faster-whisper TranscriptionOptions fields that reach CT2 generate()
+ * (asr_components.py:279-288 passes beam_size, temperature=0.0, task, word_timestamps). */
+typedef struct {
+  int32_t max_batch;                 /* windows per call (streams sharing one launch) */
+  int32_t beam_size;                 /* 1 = greedy (temperature 0), else beam search */
+  float patience;                    /* faster-whisper default 1.0 */
+  float length_penalty;              /* 1.0 -> score / len (CT2 default used by faster-whisper) */
+  int32_t max_new_tokens;            /* <= n_text_ctx - prompt; faster-whisper: 448 - prompt */
+  int32_t task;                      /* WMX_TASK_* */
+  int32_t language;                  /* language token id, or -1 = detect per window */
+  int32_t without_timestamps;        /* 0 (faster-whisper default) */
+  int32_t max_initial_timestamp_index; /* 50 = 1.0 s; -1 = none */
+  int32_t suppress_blank;            /* 1 */
+  const int32_t* suppress_tokens;    /* ids to suppress every step (faster-whisper suppress_tokens=[-1] expanded) */
+  int32_t n_suppress_tokens;
+  int32_t word_timestamps;           /* run the alignment forward + DTW */
+  const int32_t* alignment_heads;    /* [n][2] (layer, head); NULL = every head of the second half */
+  int32_t n_alignment_heads;
+  int32_t median_filter_width;       /* 7 */
+  int32_t use_graph;                 /* capture the decode step in a hipGraph */
+  int32_t max_audio_samples;         /* longest pcm per window accepted (default 480000) */
+} wmx_opts;
+
+/* per-window result of wmx_transcribe */
+typedef struct {
+  int32_t language;                  /* language token used (detected or given) */
+  float language_prob;               /* probability of that language (1.0 if given) */
+  int32_t n_tokens;                  /* sampled tokens, EOT excluded (text + timestamp tokens) */
+  const int32_t* tokens;
+  float sum_logprob;
+  float avg_logprob;                 /* sum_logprob / (n_tokens + 1) (faster-whisper) */
+  float no_speech_prob;
+  int32_t seek_frames;               /* content frames of this window (segment_size) */
+  /* word_timestamps: one entry per TEXT token (tokens < eot, in order) + 1 for the trailing eot */
+  int32_t n_text_tokens;
+  const float* jump_times;           /* [n_text_tokens + 1] seconds, faster-whisper find_alignment jump_times */
+  const float* text_token_probs;     /* [n_text_tokens] */
+} wmx_window_result;
+
+typedef struct {
+  int32_t n_windows;
+  const wmx_window_result* windows;
+} wmx_result;
+
+const char* wmx_last_error(void);
+const char* wmx_version(void);
+int wmx_device_count(void);
+
+/* ---- model ---- */
+wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_model** out);
+void wmx_model_free(wmx_model* m);
+/* build-owned deterministic synthetic weights (oracle/whisper_np.py make_weights, same PRNG) */
+wmx_status wmx_model_init_synthetic(wmx_model* m, uint64_t seed);
+/* load one tensor by its HF/openai state-dict name from host fp32 (logical HF layout) */
+wmx_status wmx_model_set_tensor(wmx_model* m, const char* name, const float* data, int64_t n);
+/* read back one tensor (logical HF layout, values as stored) — tests / checkpoint export */
+wmx_status wmx_model_get_tensor(wmx_model* m, const char* name, float* out, int64_t n);
+int64_t wmx_model_n_params(const wmx_model* m);
+/* the weight arena: one device allocation holding every parameter (for RCCL broadcast of weights) */
+wmx_status wmx_model_arena(wmx_model* m, void** device_ptr, size_t* bytes);
+/* after the arena was overwritten externally (e.g. ncclBroadcast), mark weights as initialised */
+wmx_status wmx_model_arena_loaded(wmx_model* m);
+
+/* ---- context ---- */
+void wmx_opts_default(wmx_opts* o);
+wmx_status wmx_ctx_create(wmx_model* m, const wmx_opts* o, wmx_ctx** out);
+void wmx_ctx_destroy(wmx_ctx* c);
+/* the HIP stream the context launches on (hipStream_t as void*) */
+void* wmx_ctx_stream(wmx_ctx* c);
+
+/* log-mel of B windows (faster-whisper FeatureExtractor, padding=160, pad_or_trim to 3000 frames).
+ * pcm: B rows of `stride` floats, row b holds lens[b] samples; seek: first frame per window (NULL = 0).
+ * mel_out: host [B][n_mels][3000]. */
+wmx_status wmx_logmel(wmx_ctx* c, const float* pcm, int64_t stride, const int64_t* lens, const int32_t* seek,
+                      int B, float* mel_out);
+wmx_status wmx_logmel_device(wmx_ctx* c, const float* pcm_dev, int64_t stride, const int64_t* lens,
+                             const int32_t* seek, int B, float* mel_out_dev);
+
+/* encoder on B normalised mel windows (host [B][n_mels][3000]); keeps encoder output + cross K/V in the
+ * context.  enc_out (nullable): host [B][1500][n_audio_state] f32 copy of the (rounded) encoder output. */
+wmx_status wmx_encode(wmx_ctx* c, const float* mel, int B, float* enc_out);
+wmx_status wmx_encode_device(wmx_ctx* c, const float* mel_dev, int B);
+
+/* teacher-forced decoder forward over the encoded windows: tokens [B][T] (pad with any id beyond
+ * lens[b]); logits_out host [B][T][n_vocab] f32 (rows beyond lens[b] undefined). */
+wmx_status wmx_decoder_logits(wmx_ctx* c, const int32_t* tokens, const int32_t* lens, int B, int T,
+                              float* logits_out);
+
+/* the hot path: pcm -> log-mel -> encoder -> [language detect] -> prompt prefill -> greedy/beam decode
+ * (hipGraph) -> [alignment forward + DTW].  prompt_ids: concatenated previous-text token ids per window
+ * (prompt_lens[b] each; faster-whisper keeps the last 223); NULL = no prompt. */
+wmx_status wmx_transcribe(wmx_ctx* c, const float* pcm, int64_t stride, const int64_t* lens, const int32_t* seek,
+                          int B, const int32_t* prompt_ids, const int32_t* prompt_lens, wmx_result** out);
+/* same with the pcm already resident in device memory (bench: inputs in HBM before the timed region) */
+wmx_status wmx_transcribe_device(wmx_ctx* c, const float* pcm_dev, int64_t stride, const int64_t* lens,
+                                 const int32_t* seek, int B, const int32_t* prompt_ids,
+                                 const int32_t* prompt_lens, wmx_result** out);
+void wmx_result_free(wmx_result* r);
+
+/* profiling hooks: per-stage device time of the last wmx_transcribe (ms), HIP events on the ctx stream.
+ * stages: 0 logmel, 1 encoder, 2 cross-kv, 3 lang-detect, 4 prefill, 5 decode loop, 6 alignment. */
+wmx_status wmx_ctx_stage_ms(wmx_ctx* c, float* out7);
+/* total decode steps executed by the last wmx_transcribe */
+int wmx_ctx_last_steps(wmx_ctx* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WMX_H */

@@ -652,14 +652,15 @@ def alignment_heads_default(d: Dims):
 
 def find_alignment(W, d: Dims, enc: np.ndarray, language: int, task: str, text_tokens, num_frames: int,
                    align_heads=None, medfilt_width: int = 7):
-    """Returns (text_indices, time_indices, text_token_probs) for sot_sequence + text + [eot]."""
+    """Returns (text_indices, time_indices, text_token_probs, jump_times) for the token sequence
+    sot_sequence + [<|notimestamps|>] + text + [eot] (openai timing.find_alignment)."""
     sp = special_tokens(d.n_vocab)
     heads = align_heads if align_heads is not None else alignment_heads_default(d)
     sot = sot_sequence(sp, language, task)
-    tokens = sot + list(text_tokens) + [sp.eot]
+    tokens = sot + [sp.no_timestamps] + list(text_tokens) + [sp.eot]
     cache = DecoderCache(W, d, enc)
     logits, qk = decoder_forward(W, d, tokens, cache, align_heads=heads)
-    sampled = logits[len(sot) - 1: -1, : sp.eot].astype(np.float64)
+    sampled = logits[len(sot):, : sp.eot].astype(np.float64)
     probs = softmax(sampled, -1)
     text_token_probs = probs[np.arange(len(text_tokens)), list(text_tokens)] if text_tokens else np.zeros(0)
     w = qk[:, :, : num_frames // 2].astype(np.float64)
@@ -670,4 +671,6 @@ def find_alignment(W, d: Dims, enc: np.ndarray, language: int, task: str, text_t
     w = median_filter(w, medfilt_width)
     matrix = w.mean(axis=0)[len(sot): -1]
     ti, tj = dtw(-matrix.astype(np.float32))
-    return ti, tj, text_token_probs
+    jumps = np.pad(np.diff(ti), (1, 0), constant_values=1).astype(bool)
+    jump_times = tj[jumps] / 50.0
+    return ti, tj, text_token_probs, jump_times

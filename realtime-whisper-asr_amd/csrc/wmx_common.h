@@ -1,0 +1,94 @@
+// Shared device helpers for libwmx (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+
+namespace wmx {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define WMX_HIP(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      throw ::wmx::Error(2, std::string(#expr) + ": " + hipGetErrorString(e_) + " @" __FILE__); \
+  } while (0)
+
+#define WMX_CHECK(cond, msg)                                 \
+  do {                                                       \
+    if (!(cond)) throw ::wmx::Error(1, std::string(msg));    \
+  } while (0)
+
+// ---- 16-bit storage types: bf16 and f16 share uint16_t storage; conversions are explicit ----
+enum class DT { BF16 = 0, F16 = 1 };
+
+__device__ __host__ inline float bf16_to_f32(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+// round-to-nearest-even (same formula as oracle.round_bf16; inputs are never NaN here)
+__device__ __host__ inline uint16_t f32_to_bf16(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ inline float f16_to_f32(uint16_t h) {
+  _Float16 v;
+  __builtin_memcpy(&v, &h, 2);
+  return (float)v;
+}
+__device__ inline uint16_t f32_to_f16(float f) {
+  _Float16 v = (_Float16)f;
+  uint16_t h;
+  __builtin_memcpy(&h, &v, 2);
+  return h;
+}
+
+template <DT T> __device__ inline float to_f32(uint16_t h);
+template <> __device__ inline float to_f32<DT::BF16>(uint16_t h) { return bf16_to_f32(h); }
+template <> __device__ inline float to_f32<DT::F16>(uint16_t h) { return f16_to_f32(h); }
+template <DT T> __device__ inline uint16_t from_f32(float f);
+template <> __device__ inline uint16_t from_f32<DT::BF16>(float f) { return f32_to_bf16(f); }
+template <> __device__ inline uint16_t from_f32<DT::F16>(float f) { return f32_to_f16(f); }
+
+// MFMA 16x16x32 on 8 x 16-bit operands held as u16x8
+template <DT T> __device__ inline f32x4 mfma16(const u16x8& a, const u16x8& b, f32x4 c);
+template <> __device__ inline f32x4 mfma16<DT::BF16>(const u16x8& a, const u16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <> __device__ inline f32x4 mfma16<DT::F16>(const u16x8& a, const u16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+__device__ inline float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ inline float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace wmx

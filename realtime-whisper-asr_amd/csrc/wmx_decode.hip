@@ -1,0 +1,582 @@
+// Decode-loop kernels: logit rules, log-softmax, greedy argmax / beam top-k and
+// beam bookkeeping, language detection, no-speech probability, alignment-matrix post-processing.
+//
+// Rules restated from openai-whisper decoding.py (CTranslate2 re-implements the same): SuppressBlank (step 0:
+// " " and <|endoftext|>), SuppressTokens (bitmask), ApplyTimestampRules (no <|notimestamps|>, timestamps in pairs,
+// monotonic, initial timestamp <= max_initial_timestamp_index, force a timestamp when
+// logsumexp(timestamps) > max(text)).  The masks are evaluated on the fly from a 5-int per-row state, so the
+// logits are read once for statistics and once for the argmax / top-k (never rewritten).
+// Beam search: openai BeamSearchDecoder with patience; candidates ranked by (score desc, beam asc, token asc).
+// Beams are reordered by copying token history + ancestry rows (ints), never the KV cache.
+#include "wmx_common.h"
+#include "wmx_decode.h"
+
+namespace wmx {
+
+struct RowState {  // SoA pointers, one entry per row
+  int* ns;         // sampled tokens so far
+  int* last;
+  int* pen;
+  int* last_ts;    // last timestamp token or -1
+  int* done;
+  float* sum_lp;
+};
+
+__device__ inline bool allowed(const RuleOpts& o, int t, int ns, bool last_ts, bool pen_ts, int lts) {
+  if (t == o.no_ts) return false;
+  if (o.suppress_blank && ns == 0 && (t == o.blank || t == o.eot)) return false;
+  if ((o.mask[t >> 5] >> (t & 31)) & 1u) return false;
+  if (!o.without_ts) {
+    if (last_ts) {
+      if (pen_ts) {
+        if (t >= o.tb) return false;
+      } else if (t < o.eot) {
+        return false;
+      }
+    }
+    if (lts >= 0) {
+      const int ts_last = (last_ts && !pen_ts) ? lts : lts + 1;
+      if (t >= o.tb && t < ts_last) return false;
+    }
+    if (ns == 0) {
+      if (t < o.tb) return false;
+      if (o.max_init >= 0 && t > o.tb + o.max_init) return false;
+    }
+  }
+  return true;
+}
+
+struct MS {  // online max/sum
+  float m, s;
+};
+__device__ inline MS ms_add(MS a, float v) {
+  if (v == -INFINITY) return a;
+  if (v > a.m) {
+    a.s = a.s * __expf(a.m - v) + 1.f;
+    a.m = v;
+  } else {
+    a.s += __expf(v - a.m);
+  }
+  return a;
+}
+__device__ inline MS ms_merge(MS a, MS b) {
+  if (b.m == -INFINITY) return a;
+  if (a.m == -INFINITY) return b;
+  const float m = fmaxf(a.m, b.m);
+  return MS{m, a.s * __expf(a.m - m) + b.s * __expf(b.m - m)};
+}
+__device__ inline float ms_lse(MS a) { return a.m == -INFINITY ? -INFINITY : a.m + __logf(a.s); }
+
+constexpr int kSelThreads = 512;
+constexpr int kMaxKP = 9;
+
+// better(a, b): value desc, index asc
+__device__ inline bool better(float va, int ia, float vb, int ib) { return va > vb || (va == vb && ia < ib); }
+
+__global__ __launch_bounds__(kSelThreads) void logits_select_kernel(const float* __restrict__ logits, int ldl, RuleOpts o,
+                                                                    RowState rs, int KP, int* __restrict__ out_tok,
+                                                                    float* __restrict__ out_lp, const int* row_map) {
+  const int r = blockIdx.x;
+  const int lrow = row_map ? row_map[r] : r;  // logits row
+  const float* x = logits + (long)lrow * ldl;
+  const int ns = rs.ns[r], lt = rs.last[r], pt = rs.pen[r], lts = rs.last_ts[r];
+  const bool last_ts = ns >= 1 && lt >= o.tb;
+  const bool pen_ts = ns < 2 || pt >= o.tb;
+  const int tid = threadIdx.x;
+  MS text{-INFINITY, 0.f}, ts{-INFINITY, 0.f};
+  float tmax = -INFINITY;
+  for (int t = tid; t < o.V; t += kSelThreads) {
+    if (!allowed(o, t, ns, last_ts, pen_ts, lts)) continue;
+    const float v = x[t];
+    if (t < o.tb) {
+      text = ms_add(text, v);
+      tmax = fmaxf(tmax, v);
+    } else {
+      ts = ms_add(ts, v);
+    }
+  }
+  __shared__ float sm[3][kSelThreads / 64];
+  __shared__ float ss[2][kSelThreads / 64];
+  // wave reduce
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    MS a{__shfl_xor(text.m, off), __shfl_xor(text.s, off)};
+    MS b{__shfl_xor(ts.m, off), __shfl_xor(ts.s, off)};
+    text = ms_merge(text, a);
+    ts = ms_merge(ts, b);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, off));
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane == 0) {
+    sm[0][wave] = text.m;
+    ss[0][wave] = text.s;
+    sm[1][wave] = ts.m;
+    ss[1][wave] = ts.s;
+    sm[2][wave] = tmax;
+  }
+  __syncthreads();
+  MS T{-INFINITY, 0.f}, S{-INFINITY, 0.f};
+  tmax = -INFINITY;
+  for (int w = 0; w < kSelThreads / 64; ++w) {
+    T = ms_merge(T, MS{sm[0][w], ss[0][w]});
+    S = ms_merge(S, MS{sm[1][w], ss[1][w]});
+    tmax = fmaxf(tmax, sm[2][w]);
+  }
+  const float lse_ts = ms_lse(S);
+  const bool mask_text = !o.without_ts && (lse_ts > tmax);
+  const float lse_text = ms_lse(T);
+  float lse_all;
+  if (mask_text) {
+    lse_all = lse_ts;
+  } else {
+    const float m = fmaxf(lse_text, lse_ts);
+    lse_all = m == -INFINITY ? -INFINITY : m + __logf(__expf(lse_text - m) + __expf(lse_ts - m));
+  }
+  // thread-local top-KP (sorted, best first)
+  float tv[kMaxKP];
+  int ti[kMaxKP];
+#pragma unroll
+  for (int k = 0; k < kMaxKP; ++k) {
+    tv[k] = -INFINITY;
+    ti[k] = 0x7FFFFFFF;
+  }
+  for (int t = tid; t < o.V; t += kSelThreads) {
+    if (mask_text && t < o.tb) continue;
+    if (!allowed(o, t, ns, last_ts, pen_ts, lts)) continue;
+    const float v = x[t];
+    if (!better(v, t, tv[KP - 1], ti[KP - 1])) continue;
+    // insert (KP small)
+    int k = KP - 1;
+    while (k > 0 && better(v, t, tv[k - 1], ti[k - 1])) {
+      tv[k] = tv[k - 1];
+      ti[k] = ti[k - 1];
+      --k;
+    }
+    tv[k] = v;
+    ti[k] = t;
+  }
+  // KP rounds of block argmax over the list heads
+  __shared__ float rv[kSelThreads / 64];
+  __shared__ int ri[kSelThreads / 64];
+  int head = 0;
+  for (int k = 0; k < KP; ++k) {
+    float v = head < KP ? tv[head] : -INFINITY;
+    int i = head < KP ? ti[head] : 0x7FFFFFFF;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float v2 = __shfl_xor(v, off);
+      const int i2 = __shfl_xor(i, off);
+      if (better(v2, i2, v, i)) {
+        v = v2;
+        i = i2;
+      }
+    }
+    if (lane == 0) {
+      rv[wave] = v;
+      ri[wave] = i;
+    }
+    __syncthreads();
+    float bv = rv[0];
+    int bi = ri[0];
+    for (int w = 1; w < kSelThreads / 64; ++w)
+      if (better(rv[w], ri[w], bv, bi)) {
+        bv = rv[w];
+        bi = ri[w];
+      }
+    __syncthreads();
+    if (head < KP && ti[head] == bi && bi != 0x7FFFFFFF) ++head;  // winner pops (indices are unique)
+    if (tid == 0) {
+      out_tok[r * KP + k] = bi == 0x7FFFFFFF ? o.eot : bi;
+      out_lp[r * KP + k] = bv == -INFINITY ? -INFINITY : bv - lse_all;
+    }
+  }
+}
+
+// greedy: single block of R threads; appends the token at slot+1, then advances the slot
+__global__ void greedy_update_kernel(RowState rs, const int* __restrict__ tok, const float* __restrict__ lp, int R, int tb,
+                                     int eot, int* __restrict__ hist, int hist_ld, int* __restrict__ slot,
+                                     int* __restrict__ n_done) {
+  const int r = threadIdx.x;
+  const int s = *slot;
+  if (r < R && !rs.done[r]) {
+    const int t = tok[r];
+    rs.sum_lp[r] += lp[r];
+    if (t == eot) {
+      rs.done[r] = 1;
+      atomicAdd(n_done, 1);
+    } else {
+      hist[(long)r * hist_ld + s + 1] = t;
+      rs.pen[r] = rs.last[r];
+      rs.last[r] = t;
+      rs.ns[r] += 1;
+      if (t >= tb) rs.last_ts[r] = t;
+    }
+  }
+  __syncthreads();
+  if (r == 0) *slot = s + 1;
+}
+
+// beam: one wave per window ranks K*(K+1) candidates (or K+1 at the first step: all beams identical)
+__global__ void beam_select_kernel(RowState rs, const int* __restrict__ ctok, const float* __restrict__ clp, int K,
+                                   int max_cand, int eot, const int* __restrict__ slot, const int* __restrict__ hist,
+                                   int hist_ld, BeamState bs, int* __restrict__ n_done) {
+  const int w = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (bs.win_done[w]) {
+    if (lane == 0) bs.win_active[w] = 0;
+    return;
+  }
+  const int KP = K + 1;
+  const int r0 = w * K;
+  const bool first = rs.ns[r0] == 0;
+  const int nc = first ? KP : K * KP;
+  __shared__ float cv[kMaxKP * 8];
+  __shared__ int cb[kMaxKP * 8], ct[kMaxKP * 8];
+  __shared__ int order[kMaxKP * 8];
+  __shared__ int newf[kMaxKP], nnew;
+  for (int c = lane; c < nc; c += 64) {
+    const int j = c / KP, k = c % KP;
+    const int r = r0 + j;
+    cv[c] = rs.sum_lp[r] + clp[r * KP + k];
+    cb[c] = j;
+    ct[c] = ctok[r * KP + k];
+  }
+  __syncthreads();
+  const int s = *slot;
+  if (lane == 0) {
+    bs.win_active[w] = 1;
+    for (int c = 0; c < nc; ++c) order[c] = c;
+    for (int a = 1; a < nc; ++a) {  // insertion sort: score desc, beam asc, token asc
+      const int x = order[a];
+      int b = a - 1;
+      while (b >= 0) {
+        const int y = order[b];
+        const bool xb = cv[x] > cv[y] || (cv[x] == cv[y] && (cb[x] < cb[y] || (cb[x] == cb[y] && ct[x] < ct[y])));
+        if (!xb) break;
+        order[b + 1] = y;
+        --b;
+      }
+      order[b + 1] = x;
+    }
+    int saved = 0, nn = 0;
+    int nf = bs.fin_count[w];
+    for (int q = 0; q < nc && saved < K; ++q) {
+      const int c = order[q];
+      const int parent = r0 + cb[c];
+      if (ct[c] == eot) {
+        if (nf < max_cand) {
+          const int f = w * max_cand + nf;
+          bs.fin_score[f] = cv[c];
+          bs.fin_parent[f] = parent;
+          bs.fin_len[f] = s + 1;  // history slots [0, s] of the parent; EOT implied
+          newf[nn++] = f;
+          ++nf;
+        }
+      } else {
+        bs.new_parent[r0 + saved] = parent;
+        bs.new_tok[r0 + saved] = ct[c];
+        bs.new_score[r0 + saved] = cv[c];
+        ++saved;
+      }
+    }
+    nnew = nn;
+    bs.fin_count[w] = nf;
+    if (nf >= max_cand) {
+      bs.win_done[w] = 1;
+      atomicAdd(n_done, 1);
+    }
+  }
+  __syncthreads();
+  // copy the histories of newly finished hypotheses (parents are still unmodified here)
+  for (int q = 0; q < nnew; ++q) {
+    const int f = newf[q];
+    const int p = bs.fin_parent[f];
+    for (int t = lane; t <= s; t += 64) bs.fin_hist[(long)f * hist_ld + t] = hist[(long)p * hist_ld + t];
+  }
+}
+
+// block per row: new row r' <- parent history + token; ancestry row; state.  Windows inactive this step are frozen.
+__global__ void beam_reorder_kernel(RowState rs, int K, int tb, const int* __restrict__ slot, const int* __restrict__ hist,
+                                    int* __restrict__ hist_tmp, const int* __restrict__ anc, int* __restrict__ anc_tmp,
+                                    int ld, BeamState bs, RowState tmp) {
+  const int r = blockIdx.x;
+  const int w = r / K;
+  const int s = *slot;
+  const bool frozen = !bs.win_active[w];
+  const int p = frozen ? r : bs.new_parent[r];
+  for (int t = threadIdx.x; t <= s; t += blockDim.x) {
+    hist_tmp[(long)r * ld + t] = hist[(long)p * ld + t];
+    anc_tmp[(long)r * ld + t] = anc[(long)p * ld + t];
+  }
+  if (threadIdx.x == 0) {
+    if (frozen) {
+      tmp.ns[r] = rs.ns[r];
+      tmp.last[r] = rs.last[r];
+      tmp.pen[r] = rs.pen[r];
+      tmp.last_ts[r] = rs.last_ts[r];
+      tmp.sum_lp[r] = rs.sum_lp[r];
+      hist_tmp[(long)r * ld + s + 1] = 0;
+    } else {
+      const int t = bs.new_tok[r];
+      hist_tmp[(long)r * ld + s + 1] = t;
+      tmp.ns[r] = rs.ns[p] + 1;
+      tmp.pen[r] = rs.last[p];
+      tmp.last[r] = t;
+      tmp.last_ts[r] = t >= tb ? t : rs.last_ts[p];
+      tmp.sum_lp[r] = bs.new_score[r];
+    }
+    anc_tmp[(long)r * ld + s + 1] = r;
+  }
+}
+
+__global__ void beam_commit_kernel(RowState rs, const int* __restrict__ hist_tmp, int* __restrict__ hist,
+                                   const int* __restrict__ anc_tmp, int* __restrict__ anc, int ld, RowState tmp,
+                                   const int* __restrict__ slot) {
+  const int r = blockIdx.x;
+  const int s = *slot;
+  for (int t = threadIdx.x; t <= s + 1; t += blockDim.x) {
+    hist[(long)r * ld + t] = hist_tmp[(long)r * ld + t];
+    anc[(long)r * ld + t] = anc_tmp[(long)r * ld + t];
+  }
+  if (threadIdx.x == 0) {
+    rs.ns[r] = tmp.ns[r];
+    rs.last[r] = tmp.last[r];
+    rs.pen[r] = tmp.pen[r];
+    rs.last_ts[r] = tmp.last_ts[r];
+    rs.sum_lp[r] = tmp.sum_lp[r];
+  }
+}
+
+__global__ void advance_slot_kernel(int* slot) { *slot += 1; }
+
+// language detection: argmax over language tokens of the logits at <|startoftranscript|>; writes the token into
+// the prompt of every row of the window
+__global__ void lang_detect_kernel(const float* __restrict__ logits, int ldl, int lang0, int nlang, int K,
+                                   int* __restrict__ hist, int hist_ld, const int* __restrict__ lang_slot,
+                                   int* __restrict__ lang_out, float* __restrict__ prob_out) {
+  const int w = blockIdx.x;
+  const float* x = logits + (long)w * ldl + lang0;
+  const int lane = threadIdx.x;
+  float bv = -INFINITY;
+  int bi = 0x7FFFFFFF;
+  for (int i = lane; i < nlang; i += 64)
+    if (better(x[i], i, bv, bi)) {
+      bv = x[i];
+      bi = i;
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float v2 = __shfl_xor(bv, off);
+    const int i2 = __shfl_xor(bi, off);
+    if (better(v2, i2, bv, bi)) {
+      bv = v2;
+      bi = i2;
+    }
+  }
+  float s = 0.f;
+  for (int i = lane; i < nlang; i += 64) s += __expf(x[i] - bv);
+  s = wave_sum(s);
+  if (lane == 0) {
+    lang_out[w] = lang0 + bi;
+    prob_out[w] = 1.0f / s;
+  }
+  if (hist && lane < K) hist[(long)(w * K + lane) * hist_ld + lang_slot[w]] = lang0 + bi;
+}
+
+// softmax(logits)[token] per row (no-speech probability at the SOT position)
+__global__ void token_prob_kernel(const float* __restrict__ logits, int ldl, int V, int token, float* __restrict__ out) {
+  const int r = blockIdx.x;
+  const float* x = logits + (long)r * ldl;
+  MS a{-INFINITY, 0.f};
+  for (int t = threadIdx.x; t < V; t += 256) a = ms_add(a, x[t]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) a = ms_merge(a, MS{__shfl_xor(a.m, off), __shfl_xor(a.s, off)});
+  __shared__ float sm[4], ss[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    sm[wave] = a.m;
+    ss[wave] = a.s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    MS t{-INFINITY, 0.f};
+    for (int w = 0; w < 4; ++w) t = ms_merge(t, MS{sm[w], ss[w]});
+    out[r] = __expf(x[token] - ms_lse(t));
+  }
+}
+
+// text-token probabilities of the alignment forward: softmax over [0, eot) at row m, prob of target[m]
+__global__ void text_prob_kernel(const float* __restrict__ logits, int ldl, int eot, const int* __restrict__ target,
+                                 float* __restrict__ out) {
+  const int r = blockIdx.x;
+  const int tg = target[r];
+  if (tg < 0) return;
+  const float* x = logits + (long)r * ldl;
+  MS a{-INFINITY, 0.f};
+  for (int t = threadIdx.x; t < eot; t += 256) a = ms_add(a, x[t]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) a = ms_merge(a, MS{__shfl_xor(a.m, off), __shfl_xor(a.s, off)});
+  __shared__ float sm[4], ss[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    sm[wave] = a.m;
+    ss[wave] = a.s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    MS t{-INFINITY, 0.f};
+    for (int w = 0; w < 4; ++w) t = ms_merge(t, MS{sm[w], ss[w]});
+    out[r] = __expf(x[tg] - ms_lse(t));
+  }
+}
+
+// alignment matrix of one window: for every alignment head softmax over the first nf frames, normalise each frame
+// column over the T tokens (population std), median filter (width W, reflect), mean over heads.
+__device__ inline float median7(float* v, int n) {
+  for (int i = 1; i < n; ++i) {
+    const float x = v[i];
+    int j = i - 1;
+    while (j >= 0 && v[j] > x) {
+      v[j + 1] = v[j];
+      --j;
+    }
+    v[j + 1] = x;
+  }
+  return v[n / 2];
+}
+
+__global__ __launch_bounds__(256) void align_acc_kernel(const float* __restrict__ scores, int nh, int rows_total, int Tk,
+                                                        int Tn, const int* __restrict__ ntok,
+                                                        const int* __restrict__ nframes, int width,
+                                                        float* __restrict__ scratch, float* __restrict__ out) {
+  const int w = blockIdx.x;
+  const int T = ntok[w];
+  const int nf = nframes[w] / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* sc = scratch + (long)w * Tn * Tk;
+  float* o = out + (long)w * Tn * Tk;
+  const int pad = width / 2;
+  for (int hh = 0; hh < nh; ++hh) {
+    const float* s = scores + ((long)hh * rows_total + (long)w * Tn) * Tk;
+    for (int t = wave; t < T; t += 4) {
+      float mx = -INFINITY;
+      for (int f = lane; f < nf; f += 64) mx = fmaxf(mx, s[(long)t * Tk + f]);
+      mx = wave_max(mx);
+      float sum = 0.f;
+      for (int f = lane; f < nf; f += 64) sum += __expf(s[(long)t * Tk + f] - mx);
+      sum = wave_sum(sum);
+      const float inv = 1.0f / sum;
+      for (int f = lane; f < nf; f += 64) sc[(long)t * Tk + f] = __expf(s[(long)t * Tk + f] - mx) * inv;
+    }
+    __syncthreads();
+    for (int f = tid; f < nf; f += 256) {
+      float mean = 0.f;
+      for (int t = 0; t < T; ++t) mean += sc[(long)t * Tk + f];
+      mean /= T;
+      float var = 0.f;
+      for (int t = 0; t < T; ++t) {
+        const float dlt = sc[(long)t * Tk + f] - mean;
+        var += dlt * dlt;
+      }
+      const float inv = 1.0f / sqrtf(var / T);
+      for (int t = 0; t < T; ++t) sc[(long)t * Tk + f] = (sc[(long)t * Tk + f] - mean) * inv;
+    }
+    __syncthreads();
+    for (int i = tid; i < T * nf; i += 256) {
+      const int t = i / nf, f = i % nf;
+      float v;
+      if (nf <= pad) {
+        v = sc[(long)t * Tk + f];
+      } else {
+        float win[15];
+        for (int k = 0; k < width; ++k) {
+          int j = f - pad + k;
+          if (j < 0) j = -j;
+          if (j >= nf) j = 2 * (nf - 1) - j;
+          win[k] = sc[(long)t * Tk + j];
+        }
+        v = median7(win, width);
+      }
+      o[(long)t * Tk + f] += v;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void align_scale_kernel(float* __restrict__ out, int Tn, int Tk, const int* __restrict__ ntok,
+                                   const int* __restrict__ nframes, float scale) {
+  const int w = blockIdx.x;
+  const int T = ntok[w], nf = nframes[w] / 2;
+  float* o = out + (long)w * Tn * Tk;
+  for (int i = threadIdx.x; i < T * nf; i += 256) o[(long)(i / nf) * Tk + i % nf] *= scale;
+}
+
+// ------------------------------------------------------------------------------------------------
+void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const RowPtrs& rp, int R, int KP, int* tok,
+                          float* lp, const int* row_map, hipStream_t st) {
+  WMX_CHECK(KP <= kMaxKP, "beam too large");
+  RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
+  hipLaunchKernelGGL(logits_select_kernel, dim3(R), dim3(kSelThreads), 0, st, logits, ldl, o, rs, KP, tok, lp, row_map);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_greedy_update(const RowPtrs& rp, const int* tok, const float* lp, int R, int tb, int eot, int* hist,
+                          int hist_ld, int* slot, int* n_done, hipStream_t st) {
+  WMX_CHECK(R <= 1024, "greedy: too many rows");
+  RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
+  hipLaunchKernelGGL(greedy_update_kernel, dim3(1), dim3(std::max(64, ((R + 63) / 64) * 64)), 0, st, rs, tok, lp, R, tb,
+                     eot, hist, hist_ld, slot, n_done);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_beam_step(const RowPtrs& rp, const RowPtrs& tmp, const int* ctok, const float* clp, int nwin, int K,
+                      int max_cand, int tb, int eot, int* slot, int* hist, int* hist_tmp, int* anc, int* anc_tmp, int ld,
+                      const BeamState& bs, int* n_done, hipStream_t st) {
+  RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
+  RowState ts{tmp.ns, tmp.last, tmp.pen, tmp.last_ts, tmp.done, tmp.sum_lp};
+  const int R = nwin * K;
+  hipLaunchKernelGGL(beam_select_kernel, dim3(nwin), dim3(64), 0, st, rs, ctok, clp, K, max_cand, eot, slot, hist, ld, bs,
+                     n_done);
+  hipLaunchKernelGGL(beam_reorder_kernel, dim3(R), dim3(128), 0, st, rs, K, tb, slot, hist, hist_tmp, anc, anc_tmp, ld,
+                     bs, ts);
+  hipLaunchKernelGGL(beam_commit_kernel, dim3(R), dim3(128), 0, st, rs, hist_tmp, hist, anc_tmp, anc, ld, ts, slot);
+  hipLaunchKernelGGL(advance_slot_kernel, dim3(1), dim3(1), 0, st, slot);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_lang_detect(const float* logits, int ldl, int lang0, int nlang, int nwin, int K, int* hist, int hist_ld,
+                        const int* lang_slot, int* lang_out, float* prob_out, hipStream_t st) {
+  hipLaunchKernelGGL(lang_detect_kernel, dim3(nwin), dim3(64), 0, st, logits, ldl, lang0, nlang, K, hist, hist_ld,
+                     lang_slot, lang_out, prob_out);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_token_prob(const float* logits, int ldl, int V, int token, int rows, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(token_prob_kernel, dim3(rows), dim3(256), 0, st, logits, ldl, V, token, out);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_text_prob(const float* logits, int ldl, int eot, const int* target, int rows, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(text_prob_kernel, dim3(rows), dim3(256), 0, st, logits, ldl, eot, target, out);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_align_matrix_zero(float* out, int nwin, int Tn, int Tk, hipStream_t st) {
+  WMX_HIP(hipMemsetAsync(out, 0, (size_t)nwin * Tn * Tk * sizeof(float), st));
+}
+
+void launch_align_matrix_acc(const float* scores, int nh, int rows_total, int Tk, int Tn, const int* ntok,
+                             const int* nframes, int width, int nwin, float* scratch, float* out, hipStream_t st) {
+  WMX_CHECK(width <= 15 && width % 2 == 1, "median filter width");
+  hipLaunchKernelGGL(align_acc_kernel, dim3(nwin), dim3(256), 0, st, scores, nh, rows_total, Tk, Tn, ntok, nframes, width,
+                     scratch, out);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_align_matrix_scale(float* out, int nwin, int Tn, int Tk, const int* ntok, const int* nframes, float scale,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(align_scale_kernel, dim3(nwin), dim3(256), 0, st, out, Tn, Tk, ntok, nframes, scale);
+  WMX_HIP(hipGetLastError());
+}
+
+}  // namespace wmx

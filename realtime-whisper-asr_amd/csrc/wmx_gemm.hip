@@ -1,0 +1,231 @@
+// MFMA GEMM  C[M,N] = A[M,K] . W[N,K]^T  with fused epilogues (SURVEY.md §2a "GEMM", "Conv1D", "Logits").
+//
+// Both operands are K-contiguous 16-bit (bf16 or f16) so A and W tiles share one LDS image and one fragment
+// read.  Tiles are staged HBM -> LDS with global_load_lds_dwordx4 (lane-linear 1 KiB per wave instruction);
+// the bank-conflict XOR swizzle (16-B piece ^= row & 7) is applied on the global SOURCE address and on the
+// ds_read, never on the LDS destination (cdna_hip_programming.md §5.4 rule 21).  Two LDS buffers, BK = 64,
+// v_mfma_f32_16x16x32_{bf16,f16}, fp32 accumulation.  Block index is XCD-remapped so consecutive N tiles of
+// one row panel share an XCD's L2 (§5.5 T1, bijective form).
+//
+// Epilogues are fused: bias, exact-erf GELU, fp32 residual add (the residual stream stays fp32), conv2's
+// GELU + sinusoidal position add, the decoder QKV scatter straight into the self-attention KV cache, and
+// split-K fp32 partial slabs reduced deterministically (fixed order) by gemm_splitk_reduce.
+#include "wmx_common.h"
+#include "wmx_kernels.h"
+
+namespace wmx {
+
+template <DT T>
+__device__ inline void epi_store(const Epi& e, int m, int n, float v) {
+  if (e.bias) v += e.bias[n];
+  switch (e.kind) {
+    case EPI_STORE16:
+      reinterpret_cast<uint16_t*>(e.out)[(long)m * e.ldc + n] = from_f32<T>(v);
+      break;
+    case EPI_GELU16:
+      reinterpret_cast<uint16_t*>(e.out)[(long)m * e.ldc + n] = from_f32<T>(gelu_erf(v));
+      break;
+    case EPI_RESID32: {
+      float* o = reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n;
+      *o = *o + v;
+      break;
+    }
+    case EPI_GELU_POS32:
+      reinterpret_cast<float*>(e.out)[(long)m * e.ldc + n] = gelu_erf(v) + e.pos[(long)(m % e.posT) * e.ldc + n];
+      break;
+    case EPI_STORE32:
+      reinterpret_cast<float*>(e.out)[(long)m * e.ldc + n] = v;
+      break;
+    case EPI_QKV_CACHE: {
+      // m = row * Tn + i ; slot = *slot0 + i ; cols [0,d) q, [d,2d) k -> cache, [2d,3d) v -> cache
+      const int d = e.d;
+      const uint16_t h = from_f32<T>(v);
+      if (n < d) {
+        reinterpret_cast<uint16_t*>(e.out)[(long)m * d + n] = h;
+      } else {
+        const int r = m / e.Tn, i = m - r * e.Tn;
+        const long slot = (long)(*e.slot0) + i;
+        uint16_t* cache = n < 2 * d ? e.kc : e.vc;
+        cache[(slot * e.R + (long)r * e.rmul) * d + (n % d)] = h;
+      }
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+template <DT T, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __restrict__ A, long lda,
+                                                           const uint16_t* __restrict__ W, long ldw, int M, int N,
+                                                           int K, int kchunk, Epi e, float* __restrict__ ws) {
+  constexpr int NW = WM * WN;
+  constexpr int A_CH = BM / 8, B_CH = BN / 8;  // 1 KiB chunks (8 rows x 64 k) per tile
+  static_assert(A_CH % NW == 0 && B_CH % NW == 0, "tile/wave mismatch");
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int TILE_BYTES = (BM + BN) * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tilesN = (N + BN - 1) / BN;
+  const int tilesM = (M + BM - 1) / BM;
+  const int nwg = tilesN * tilesM;
+  // bijective XCD remap: blocks b and b+8 share an XCD; give each XCD a contiguous range of tiles
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tm = bid / tilesN, tn = bid - tm * tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kb = blockIdx.y * kchunk;
+  const int ke = min(K, kb + kchunk);
+  const int nk = (ke - kb) / 64;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+
+  // per-lane staging source offsets (row and swizzled piece are loop-invariant)
+  const int srow = lane >> 3;
+  auto issue = [&](int kt, int buf) {
+    char* base = smem + buf * TILE_BYTES;
+    const int k0 = kb + kt * 64;
+#pragma unroll
+    for (int c = wave; c < A_CH; c += NW) {
+      const int row = c * 8 + srow;
+      const int gp = (lane & 7) ^ (row & 7);
+      const int gr = min(m0 + row, M - 1);
+      const uint16_t* src = A + (long)gr * lda + k0 + gp * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(base + c * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int c = wave; c < B_CH; c += NW) {
+      const int row = c * 8 + srow;
+      const int gp = (lane & 7) ^ (row & 7);
+      const int gr = min(n0 + row, N - 1);
+      const uint16_t* src = W + (long)gr * ldw + k0 + gp * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(base + BM * 128 + c * 1024), 16, 0,
+                                       0);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+
+  if (nk > 0) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    const char* As = smem + buf * TILE_BYTES;
+    const char* Bs = As + BM * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int p = s * 4 + fq;
+      u16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * (BM / WM) + i * 16 + fr;
+        af[i] = *reinterpret_cast<const u16x8*>(As + row * 128 + ((p ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * (BN / WN) + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const u16x8*>(Bs + row * 128 + ((p ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16<T>(af[i], bfr[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: lane holds rows fq*4 + r, col fr of each 16x16 tile
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * (BN / WN) + j * 16 + fr;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * (BM / WM) + i * 16 + fq * 4 + r;
+        if (m >= M) continue;
+        if (ws) {
+          ws[((long)blockIdx.y * M + m) * N + n] = acc[i][j][r];
+        } else {
+          epi_store<T>(e, m, n, acc[i][j][r]);
+        }
+      }
+    }
+  }
+}
+
+template <DT T>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N,
+                                                          Epi e) {
+  const long total = (long)M * N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += ws[s * total + i];
+    epi_store<T>(e, (int)(i / N), (int)(i % N), v);
+  }
+}
+
+template <DT T, int BM, int BN, int WM, int WN>
+static void launch_cfg(const GemmCall& g, hipStream_t st) {
+  constexpr int TILE_BYTES = (BM + BN) * 128;
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  int splits = std::max(1, g.splits);
+  int kchunk = ((g.K / 64 + splits - 1) / splits) * 64;
+  splits = (g.K + kchunk - 1) / kchunk;
+  float* ws = splits > 1 ? g.ws : nullptr;
+  if (splits > 1) WMX_CHECK(ws != nullptr && (long)splits * g.M * g.N <= g.ws_elems, "gemm: split-K workspace too small");
+  dim3 grid(tiles, splits);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 2 * TILE_BYTES, st, g.A, g.lda, g.W,
+                     g.ldw, g.M, g.N, g.K, kchunk, g.epi, ws);
+  if (splits > 1) {
+    long total = (long)g.M * g.N;
+    int blocks = (int)std::min<long>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL((gemm_splitk_reduce<T>), dim3(blocks), dim3(256), 0, st, g.ws, splits, g.M, g.N, g.epi);
+  }
+}
+
+template <DT T>
+static void launch_t(const GemmCall& g, hipStream_t st) {
+  WMX_CHECK(g.K % 64 == 0, "gemm: K must be a multiple of 64");
+  switch (g.tile) {
+    case TILE_128x128:
+      launch_cfg<T, 128, 128, 2, 2>(g, st);
+      break;
+    case TILE_64x64:
+      launch_cfg<T, 64, 64, 2, 2>(g, st);
+      break;
+    case TILE_32x64:
+      launch_cfg<T, 32, 64, 1, 4>(g, st);
+      break;
+    default:
+      WMX_CHECK(false, "gemm: bad tile");
+  }
+}
+
+void launch_gemm(DT dt, const GemmCall& g, hipStream_t st) {
+  if (g.M <= 0 || g.N <= 0) return;
+  if (dt == DT::BF16)
+    launch_t<DT::BF16>(g, st);
+  else
+    launch_t<DT::F16>(g, st);
+  WMX_HIP(hipGetLastError());
+}
+
+}  // namespace wmx

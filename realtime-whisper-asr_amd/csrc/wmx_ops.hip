@@ -1,0 +1,219 @@
+// Memory-bound helper kernels: LayerNorm (fp32 residual -> 16-bit GEMM operand), conv im2col, token+position
+// embedding, dtype conversion, and the build-owned synthetic weight generator (same counter PRNG as
+// oracle/whisper_np.py prng_uniform, bit-exact).
+#include "wmx_common.h"
+#include "wmx_kernels.h"
+
+namespace wmx {
+
+// ---------------- LayerNorm: one wave per row, two-pass (mean, then centred variance), eps 1e-5 ----------------
+template <DT T>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const int* __restrict__ rows_idx,
+                                                        const float* __restrict__ g, const float* __restrict__ bb,
+                                                        uint16_t* __restrict__ out, int rows, int d) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const int src = rows_idx ? rows_idx[row] : row;
+  const float4* xr = reinterpret_cast<const float4*>(x + (long)src * d);
+  const int n4 = d >> 2;
+  float4 v[8];  // d <= 2048
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      v[i] = xr[c];
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+  }
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, e = v[i].w - mean;
+      q += a * a + b * b + cc * cc + e * e;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / d + 1e-5f);
+  uint16_t* o = out + (long)row * d;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      const float4 gg = reinterpret_cast<const float4*>(g)[c];
+      const float4 be = reinterpret_cast<const float4*>(bb)[c];
+      u16x4 w;
+      w[0] = from_f32<T>((v[i].x - mean) * rstd * gg.x + be.x);
+      w[1] = from_f32<T>((v[i].y - mean) * rstd * gg.y + be.y);
+      w[2] = from_f32<T>((v[i].z - mean) * rstd * gg.z + be.z);
+      w[3] = from_f32<T>((v[i].w - mean) * rstd * gg.w + be.w);
+      reinterpret_cast<u16x4*>(o)[c] = w;
+    }
+  }
+}
+
+void launch_layernorm_rows(DT dt, const float* x, const int* rows_idx, const float* g, const float* b, uint16_t* out,
+                           int rows, int d, hipStream_t st) {
+  if (rows <= 0) return;
+  WMX_CHECK(d % 4 == 0 && d <= 2048, "layernorm: d");
+  dim3 grid(cdiv(rows, 4));
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(layernorm_kernel<DT::BF16>, grid, dim3(256), 0, st, x, rows_idx, g, b, out, rows, d);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<DT::F16>, grid, dim3(256), 0, st, x, rows_idx, g, b, out, rows, d);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_layernorm(DT dt, const float* x, const float* g, const float* b, uint16_t* out, int rows, int d,
+                      hipStream_t st) {
+  launch_layernorm_rows(dt, x, nullptr, g, b, out, rows, d, st);
+}
+
+// ---------------- conv1 im2col: out[b*3000+t][kk*M + c] = mel[b][c][t+kk-1] (0 outside / in the K pad) ----------------
+template <DT T>
+__global__ __launch_bounds__(256) void im2col1_kernel(const float* __restrict__ mel, int B, int M, int Kp,
+                                                      uint16_t* __restrict__ out) {
+  // tile: 64 frames x all channels of one window, transposed through LDS for coalesced reads and writes
+  __shared__ float tile[128][67];
+  const int b = blockIdx.y, t0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < M * 66; i += 256) {  // channels x frames t0-1 .. t0+64
+    const int cc = i / 66, tt = t0 - 1 + i % 66;
+    tile[cc][i % 66] = (tt >= 0 && tt < 3000) ? mel[((long)b * M + cc) * 3000 + tt] : 0.f;
+  }
+  __syncthreads();
+  for (int i = tid; i < 64 * Kp; i += 256) {
+    const int tl = i / Kp, col = i % Kp;
+    const int t = t0 + tl;
+    if (t >= 3000) continue;
+    float v = 0.f;
+    if (col < 3 * M) {
+      const int kk = col / M, c = col % M;
+      v = tile[c][tl + kk];
+    }
+    out[((long)b * 3000 + t) * Kp + col] = from_f32<T>(v);
+  }
+}
+
+void launch_im2col_conv1(DT dt, const float* mel, int B, int n_mels, int Kp, uint16_t* out, hipStream_t st) {
+  WMX_CHECK(n_mels <= 128, "im2col1: n_mels");
+  dim3 grid(cdiv(3000, 64), B);
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(im2col1_kernel<DT::BF16>, grid, dim3(256), 0, st, mel, B, n_mels, Kp, out);
+  else
+    hipLaunchKernelGGL(im2col1_kernel<DT::F16>, grid, dim3(256), 0, st, mel, B, n_mels, Kp, out);
+  WMX_HIP(hipGetLastError());
+}
+
+// ---------------- conv2 im2col (stride 2): out[b*1500+t][kk*d + c] = h1[b*3000 + 2t+kk-1][c] ----------------
+__global__ __launch_bounds__(256) void im2col2_kernel(const uint16_t* __restrict__ h1, int B, int d,
+                                                      uint16_t* __restrict__ out) {
+  const int n8 = d / 8;
+  const long total = (long)B * 1500 * 3 * n8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c8 = (int)(i % n8);
+    const long r = i / n8;
+    const int kk = (int)(r % 3);
+    const long bt = r / 3;
+    const int t = (int)(bt % 1500), b = (int)(bt / 1500);
+    const int ts = 2 * t + kk - 1;
+    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (ts >= 0 && ts < 3000) v = reinterpret_cast<const u16x8*>(h1 + ((long)b * 3000 + ts) * d)[c8];
+    reinterpret_cast<u16x8*>(out + bt * 3 * d + kk * d)[c8] = v;
+  }
+}
+
+void launch_im2col_conv2(DT, const uint16_t* h1, int B, int d, uint16_t* out, hipStream_t st) {
+  const long total = (long)B * 1500 * 3 * (d / 8);
+  hipLaunchKernelGGL(im2col2_kernel, dim3((int)std::min<long>((total + 255) / 256, 8192)), dim3(256), 0, st, h1, B, d,
+                     out);
+  WMX_HIP(hipGetLastError());
+}
+
+template <DT T>
+__global__ void cvt_kernel(const uint16_t* __restrict__ in, float* __restrict__ out, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = to_f32<T>(in[i]);
+}
+void launch_cvt16_to_f32(DT dt, const uint16_t* in, float* out, long n, hipStream_t st) {
+  dim3 g((int)std::min<long>((n + 255) / 256, 8192));
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(cvt_kernel<DT::BF16>, g, dim3(256), 0, st, in, out, n);
+  else
+    hipLaunchKernelGGL(cvt_kernel<DT::F16>, g, dim3(256), 0, st, in, out, n);
+  WMX_HIP(hipGetLastError());
+}
+
+// ---------------- token + learned position embedding into the fp32 residual stream ----------------
+template <DT T>
+__global__ __launch_bounds__(256) void embed_kernel(const uint16_t* __restrict__ tok_emb, const uint16_t* __restrict__ pos_emb,
+                                                    const int* __restrict__ hist, long hist_ld, int Tn,
+                                                    const int* __restrict__ pad, const int* __restrict__ slot0, int d,
+                                                    float* __restrict__ x) {
+  const int m = blockIdx.x;
+  const int r = m / Tn, i = m - r * Tn;
+  const int slot = *slot0 + i;
+  const int tok = hist[(long)r * hist_ld + slot];
+  int pos = slot - (pad ? pad[r] : 0);
+  pos = max(pos, 0);
+  for (int c = threadIdx.x; c < d; c += 256)
+    x[(long)m * d + c] = to_f32<T>(tok_emb[(long)tok * d + c]) + to_f32<T>(pos_emb[(long)pos * d + c]);
+}
+
+void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R, int Tn,
+                  const int* pad, const int* slot0, int d, float* x, hipStream_t st) {
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(embed_kernel<DT::BF16>, dim3(R * Tn), dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, Tn, pad,
+                       slot0, d, x);
+  else
+    hipLaunchKernelGGL(embed_kernel<DT::F16>, dim3(R * Tn), dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, Tn, pad,
+                       slot0, d, x);
+  WMX_HIP(hipGetLastError());
+}
+
+// ---------------- synthetic weights: u = splitmix64(seed*G1 + tid*G2 + i) top 24 bits -> [-1,1) ----------------
+__device__ inline float prng_u(uint64_t key, uint64_t i) {
+  uint64_t z = key + i;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  const float k = (float)(uint32_t)(z >> 40);
+  return __fsub_rn(__fmul_rn(k, 1.1920928955078125e-7f), 1.0f);
+}
+
+template <DT T>
+__global__ void init_kernel(uint64_t key, InitSpec s) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < s.n; i += (long)gridDim.x * 256) {
+    float v = __fmul_rn(prng_u(key, (uint64_t)i), s.scale);
+    if (s.offset != 0.f) v = __fadd_rn(v, s.offset);
+    long di = i;
+    if (s.kind == 1) {  // conv [O][C][3] -> [O][Kp] at kk*C + c
+      const int kk = (int)(i % 3);
+      const long oc = i / 3;
+      const int c = (int)(oc % s.C);
+      const long o = oc / s.C;
+      di = o * s.Kp + (long)kk * s.C + c;
+    }
+    if (s.store_f32) {
+      // f32 storage of a 16-bit parameter: keep the value the 16-bit storage would hold
+      const uint16_t h = from_f32<T>(v);
+      reinterpret_cast<float*>(s.dst)[di] = to_f32<T>(h);
+    } else {
+      reinterpret_cast<uint16_t*>(s.dst)[di] = from_f32<T>(v);
+    }
+  }
+}
+
+void launch_init_tensor(DT dt, uint64_t seed, const InitSpec& s, hipStream_t st) {
+  const uint64_t key = seed * 0x9E3779B97F4A7C15ull + (uint64_t)s.tid * 0xBF58476D1CE4E5B9ull;
+  dim3 g((int)std::min<long>((s.n + 255) / 256, 16384));
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(init_kernel<DT::BF16>, g, dim3(256), 0, st, key, s);
+  else
+    hipLaunchKernelGGL(init_kernel<DT::F16>, g, dim3(256), 0, st, key, s);
+  WMX_HIP(hipGetLastError());
+}
+
+}  // namespace wmx

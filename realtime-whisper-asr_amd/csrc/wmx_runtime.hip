@@ -1,0 +1,1583 @@
+// libwmx runtime: model weight arena, per-context buffers, the transcribe pipeline and the C ABI (include/wmx.h).
+//
+// Pipeline (SURVEY.md §3 stack C, re-designed for one MI355X):
+//   pcm (HBM) -> log-mel (f32 MFMA DFT) -> encoder (bf16/f16 MFMA GEMMs, flash attention, fp32 residual)
+//   -> cross K/V of every decoder layer in ONE GEMM (once per window, shared by all beams)
+//   -> [language detect: one decoder step on <|startoftranscript|>]
+//   -> prompt prefill (left-padded so all windows advance in lock-step; beams alias beam 0's prompt cache
+//      through the ancestry table) -> decode loop, one step = one hipGraph replay, state entirely on device
+//   -> [alignment forward over sot + text + eot: alignment-head scores -> softmax/normalise/median on device,
+//      DTW on host threads].
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/wmx.h"
+#include "wmx_common.h"
+#include "wmx_decode.h"
+#include "wmx_kernels.h"
+
+namespace wmx {
+
+static thread_local std::string g_err;
+
+// ------------------------------------------------------------------------------------------------
+// host helpers
+// ------------------------------------------------------------------------------------------------
+static uint16_t host_f32_to_bf16(float f) { return f32_to_bf16(f); }
+static uint16_t host_f32_to_f16(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+static float host_bf16_to_f32(uint16_t h) { return bf16_to_f32(h); }
+static float host_f16_to_f32(uint16_t u) {
+  _Float16 h;
+  std::memcpy(&h, &u, 2);
+  return (float)h;
+}
+
+// faster-whisper FeatureExtractor.get_mel_filters (slaney), evaluated in double
+static std::vector<double> mel_filters(int n_mels) {
+  const int nb = 201;
+  std::vector<double> fft(nb), mels(n_mels + 2), freqs(n_mels + 2);
+  for (int i = 0; i < nb; ++i) fft[i] = i * 16000.0 / 400.0;
+  for (int i = 0; i < n_mels + 2; ++i) mels[i] = 45.245640471924965 * i / (n_mels + 1);
+  const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = std::log(6.4) / 27.0;
+  for (int i = 0; i < n_mels + 2; ++i)
+    freqs[i] = mels[i] >= min_log_mel ? min_log_hz * std::exp(logstep * (mels[i] - min_log_mel)) : f_sp * mels[i];
+  std::vector<double> w((size_t)n_mels * nb);
+  for (int m = 0; m < n_mels; ++m) {
+    const double enorm = 2.0 / (freqs[m + 2] - freqs[m]);
+    for (int k = 0; k < nb; ++k) {
+      const double lower = -(freqs[m] - fft[k]) / (freqs[m + 1] - freqs[m]);
+      const double upper = (freqs[m + 2] - fft[k]) / (freqs[m + 2] - freqs[m + 1]);
+      w[(size_t)m * nb + k] = std::max(0.0, std::min(lower, upper)) * enorm;
+    }
+  }
+  return w;
+}
+
+static std::vector<float> sinusoids(int length, int channels) {
+  std::vector<float> out((size_t)length * channels);
+  const int half = channels / 2;
+  const double inc = std::log(10000.0) / (half - 1);
+  for (int t = 0; t < length; ++t)
+    for (int i = 0; i < half; ++i) {
+      const double v = t * std::exp(-inc * i);
+      out[(size_t)t * channels + i] = (float)std::sin(v);
+      out[(size_t)t * channels + half + i] = (float)std::cos(v);
+    }
+  return out;
+}
+
+struct Special {
+  int eot = 50257, sot = 50258, lang0 = 50259, n_langs, translate, transcribe, sot_lm, sot_prev, no_speech,
+      no_timestamps, timestamp_begin, blank = 220;
+  explicit Special(int n_vocab) {
+    n_langs = n_vocab >= 51866 ? 100 : 99;
+    const int base = 50259 + n_langs;
+    translate = base;
+    transcribe = base + 1;
+    sot_lm = base + 2;
+    sot_prev = base + 3;
+    no_speech = base + 4;
+    no_timestamps = base + 5;
+    timestamp_begin = base + 6;
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// model
+// ------------------------------------------------------------------------------------------------
+struct TensorEntry {
+  std::string name;
+  int tid;
+  long n;           // logical elements
+  float scale, offset;
+  int kind;         // 0 plain, 1 conv permute
+  int C, Kp, O;
+  void* dst;
+  int store_f32;
+  std::vector<long> shape;
+};
+
+struct EncLayer {
+  float *ln1g, *ln1b, *bqkv, *bo, *ln2g, *ln2b, *bfc1, *bfc2;
+  uint16_t *wqkv, *wo, *wfc1, *wfc2;
+};
+struct DecLayer {
+  float *ln1g, *ln1b, *bqkv, *bo, *ln2g, *ln2b, *bcq, *bco, *ln3g, *ln3b, *bfc1, *bfc2;
+  uint16_t *wqkv, *wo, *wcq, *wco, *wfc1, *wfc2;
+};
+
+struct Model {
+  wmx_dims d{};
+  int device = 0;
+  DT dt = DT::BF16;
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
+  int K1p = 0;
+  uint16_t *conv1w = nullptr, *conv2w = nullptr, *tok_emb = nullptr, *dec_pos = nullptr, *wckv = nullptr;
+  float *conv1b = nullptr, *conv2b = nullptr, *enc_pos = nullptr, *lnpg = nullptr, *lnpb = nullptr, *bckv = nullptr,
+        *lng = nullptr, *lnb = nullptr;
+  std::vector<EncLayer> enc;
+  std::vector<DecLayer> dec;
+  std::vector<TensorEntry> entries;
+  std::map<std::string, int> by_name;
+  // log-mel constants
+  float* mel_basis = nullptr;
+  int *mel_first = nullptr, *mel_count = nullptr, *mel_off = nullptr;
+  float* mel_w = nullptr;
+  bool initialized = false;
+  hipStream_t st = nullptr;
+};
+
+struct Planner {
+  size_t off = 0;
+  std::vector<std::pair<void**, size_t>> items;
+  template <class T>
+  void add(T** p, size_t elems) {
+    items.push_back({(void**)p, off});
+    off += (elems * sizeof(T) + 255) / 256 * 256;
+  }
+  void bind(char* base) {
+    for (auto& it : items) *it.first = base + it.second;
+  }
+};
+
+static void build_model(Model& m) {
+  const wmx_dims& d = m.d;
+  const int da = d.n_audio_state, dt = d.n_text_state, M = d.n_mels, V = d.n_vocab;
+  WMX_CHECK(da % 64 == 0 && dt % 64 == 0 && da / 64 == d.n_audio_head && dt / 64 == d.n_text_head,
+            "model: head_dim must be 64 and width a multiple of 64");
+  WMX_CHECK(d.n_audio_ctx == 1500 && d.n_text_ctx <= 448 && M <= 128, "model: unsupported context sizes");
+  m.K1p = (3 * M + 63) / 64 * 64;
+  Planner P;
+  P.add(&m.conv1w, (size_t)da * m.K1p);
+  P.add(&m.conv1b, da);
+  P.add(&m.conv2w, (size_t)da * 3 * da);
+  P.add(&m.conv2b, da);
+  P.add(&m.enc_pos, (size_t)1500 * da);
+  m.enc.resize(d.n_audio_layer);
+  for (auto& L : m.enc) {
+    P.add(&L.ln1g, da);
+    P.add(&L.ln1b, da);
+    P.add(&L.wqkv, (size_t)3 * da * da);
+    P.add(&L.bqkv, 3 * da);
+    P.add(&L.wo, (size_t)da * da);
+    P.add(&L.bo, da);
+    P.add(&L.ln2g, da);
+    P.add(&L.ln2b, da);
+    P.add(&L.wfc1, (size_t)4 * da * da);
+    P.add(&L.bfc1, 4 * da);
+    P.add(&L.wfc2, (size_t)4 * da * da);
+    P.add(&L.bfc2, da);
+  }
+  P.add(&m.lnpg, da);
+  P.add(&m.lnpb, da);
+  P.add(&m.tok_emb, (size_t)V * dt);
+  P.add(&m.dec_pos, (size_t)d.n_text_ctx * dt);
+  m.dec.resize(d.n_text_layer);
+  for (auto& L : m.dec) {
+    P.add(&L.ln1g, dt);
+    P.add(&L.ln1b, dt);
+    P.add(&L.wqkv, (size_t)3 * dt * dt);
+    P.add(&L.bqkv, 3 * dt);
+    P.add(&L.wo, (size_t)dt * dt);
+    P.add(&L.bo, dt);
+    P.add(&L.ln2g, dt);
+    P.add(&L.ln2b, dt);
+    P.add(&L.wcq, (size_t)dt * dt);
+    P.add(&L.bcq, dt);
+    P.add(&L.wco, (size_t)dt * dt);
+    P.add(&L.bco, dt);
+    P.add(&L.ln3g, dt);
+    P.add(&L.ln3b, dt);
+    P.add(&L.wfc1, (size_t)4 * dt * dt);
+    P.add(&L.bfc1, 4 * dt);
+    P.add(&L.wfc2, (size_t)4 * dt * dt);
+    P.add(&L.bfc2, dt);
+  }
+  P.add(&m.wckv, (size_t)d.n_text_layer * 2 * dt * dt);
+  P.add(&m.bckv, (size_t)d.n_text_layer * 2 * dt);
+  P.add(&m.lng, dt);
+  P.add(&m.lnb, dt);
+  // log-mel constants
+  P.add(&m.mel_basis, (size_t)400 * 416);
+  P.add(&m.mel_first, M);
+  P.add(&m.mel_count, M);
+  P.add(&m.mel_off, M);
+  P.add(&m.mel_w, (size_t)M * 201);
+  m.arena_bytes = P.off;
+  WMX_HIP(hipMalloc(&m.arena, m.arena_bytes));
+  WMX_HIP(hipMemsetAsync(m.arena, 0, m.arena_bytes, m.st));
+  P.bind(m.arena);
+
+  // tensor registry, in oracle/whisper_np.py tensor_specs order (tid = index)
+  auto f32s = [](double v) { return (float)v; };
+  auto add = [&](const std::string& name, std::vector<long> shape, float scale, float offset, void* dst, int store_f32,
+                 int kind = 0, int C = 0, int Kp = 0) {
+    TensorEntry e;
+    e.name = name;
+    e.tid = (int)m.entries.size();
+    e.n = 1;
+    for (long s : shape) e.n *= s;
+    e.shape = shape;
+    e.scale = scale;
+    e.offset = offset;
+    e.kind = kind;
+    e.C = C;
+    e.Kp = Kp;
+    e.O = (int)shape[0];
+    e.dst = dst;
+    e.store_f32 = store_f32;
+    m.by_name[name] = (int)m.entries.size();
+    m.entries.push_back(e);
+  };
+  auto lin = [&](const std::string& p, long n_out, long n_in, uint16_t* w, float* b) {
+    add(p + ".weight", {n_out, n_in}, f32s(1.0 / std::sqrt((double)n_in)), 0.f, w, 0);
+    if (b) add(p + ".bias", {n_out}, 0.02f, 0.f, b, 1);
+  };
+  auto ln = [&](const std::string& p, long n, float* g, float* b) {
+    add(p + ".weight", {n}, 0.1f, 1.0f, g, 1);
+    add(p + ".bias", {n}, 0.02f, 0.f, b, 1);
+  };
+  add("encoder.conv1.weight", {da, M, 3}, f32s(1.0 / std::sqrt(3.0 * M)), 0.f, m.conv1w, 0, 1, M, m.K1p);
+  add("encoder.conv1.bias", {da}, 0.02f, 0.f, m.conv1b, 1);
+  add("encoder.conv2.weight", {da, da, 3}, f32s(1.0 / std::sqrt(3.0 * da)), 0.f, m.conv2w, 0, 1, da, 3 * da);
+  add("encoder.conv2.bias", {da}, 0.02f, 0.f, m.conv2b, 1);
+  for (int i = 0; i < d.n_audio_layer; ++i) {
+    EncLayer& L = m.enc[i];
+    const std::string p = "encoder.layers." + std::to_string(i);
+    ln(p + ".self_attn_layer_norm", da, L.ln1g, L.ln1b);
+    lin(p + ".self_attn.q_proj", da, da, L.wqkv, L.bqkv);
+    lin(p + ".self_attn.k_proj", da, da, L.wqkv + (size_t)da * da, nullptr);
+    lin(p + ".self_attn.v_proj", da, da, L.wqkv + (size_t)2 * da * da, L.bqkv + 2 * da);
+    lin(p + ".self_attn.out_proj", da, da, L.wo, L.bo);
+    ln(p + ".final_layer_norm", da, L.ln2g, L.ln2b);
+    lin(p + ".fc1", 4 * da, da, L.wfc1, L.bfc1);
+    lin(p + ".fc2", da, 4 * da, L.wfc2, L.bfc2);
+  }
+  ln("encoder.layer_norm", da, m.lnpg, m.lnpb);
+  add("decoder.embed_tokens.weight", {V, dt}, f32s(6.0 / std::sqrt((double)dt)), 0.f, m.tok_emb, 0);
+  add("decoder.embed_positions.weight", {d.n_text_ctx, dt}, 0.05f, 0.f, m.dec_pos, 0);
+  for (int i = 0; i < d.n_text_layer; ++i) {
+    DecLayer& L = m.dec[i];
+    const std::string p = "decoder.layers." + std::to_string(i);
+    ln(p + ".self_attn_layer_norm", dt, L.ln1g, L.ln1b);
+    lin(p + ".self_attn.q_proj", dt, dt, L.wqkv, L.bqkv);
+    lin(p + ".self_attn.k_proj", dt, dt, L.wqkv + (size_t)dt * dt, nullptr);
+    lin(p + ".self_attn.v_proj", dt, dt, L.wqkv + (size_t)2 * dt * dt, L.bqkv + 2 * dt);
+    lin(p + ".self_attn.out_proj", dt, dt, L.wo, L.bo);
+    ln(p + ".encoder_attn_layer_norm", dt, L.ln2g, L.ln2b);
+    lin(p + ".encoder_attn.q_proj", dt, dt, L.wcq, L.bcq);
+    lin(p + ".encoder_attn.k_proj", dt, dt, m.wckv + (size_t)i * 2 * dt * dt, nullptr);
+    lin(p + ".encoder_attn.v_proj", dt, dt, m.wckv + ((size_t)i * 2 * dt + dt) * dt, m.bckv + (size_t)i * 2 * dt + dt);
+    lin(p + ".encoder_attn.out_proj", dt, dt, L.wco, L.bco);
+    ln(p + ".final_layer_norm", dt, L.ln3g, L.ln3b);
+    lin(p + ".fc1", 4 * dt, dt, L.wfc1, L.bfc1);
+    lin(p + ".fc2", dt, 4 * dt, L.wfc2, L.bfc2);
+  }
+  ln("decoder.layer_norm", dt, m.lng, m.lnb);
+
+  // constants: sinusoids, DFT basis (Hann folded, re | im blocks of 208), sparse mel filterbank
+  auto pos = sinusoids(1500, da);
+  WMX_HIP(hipMemcpyAsync(m.enc_pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, m.st));
+  std::vector<float> basis((size_t)400 * 416, 0.f);
+  for (int n = 0; n < 400; ++n) {
+    const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * n / 400.0);
+    for (int k = 0; k < 201; ++k) {
+      const double ang = 2.0 * M_PI * (double)((long)n * k % 400) / 400.0;
+      basis[(size_t)n * 416 + k] = (float)(w * std::cos(ang));
+      basis[(size_t)n * 416 + 208 + k] = (float)(-w * std::sin(ang));
+    }
+  }
+  WMX_HIP(hipMemcpyAsync(m.mel_basis, basis.data(), basis.size() * 4, hipMemcpyHostToDevice, m.st));
+  auto fw = mel_filters(M);
+  std::vector<int> first(M), count(M), off(M);
+  std::vector<float> wts;
+  for (int i = 0; i < M; ++i) {
+    int lo = -1, hi = -1;
+    for (int k = 0; k < 201; ++k)
+      if (fw[(size_t)i * 201 + k] > 0) {
+        if (lo < 0) lo = k;
+        hi = k;
+      }
+    if (lo < 0) lo = hi = 0;
+    first[i] = lo;
+    count[i] = hi - lo + 1;
+    off[i] = (int)wts.size();
+    for (int k = lo; k <= hi; ++k) wts.push_back((float)fw[(size_t)i * 201 + k]);
+  }
+  WMX_HIP(hipMemcpyAsync(m.mel_first, first.data(), M * 4, hipMemcpyHostToDevice, m.st));
+  WMX_HIP(hipMemcpyAsync(m.mel_count, count.data(), M * 4, hipMemcpyHostToDevice, m.st));
+  WMX_HIP(hipMemcpyAsync(m.mel_off, off.data(), M * 4, hipMemcpyHostToDevice, m.st));
+  WMX_HIP(hipMemcpyAsync(m.mel_w, wts.data(), wts.size() * 4, hipMemcpyHostToDevice, m.st));
+  WMX_HIP(hipStreamSynchronize(m.st));
+}
+
+// ------------------------------------------------------------------------------------------------
+// context
+// ------------------------------------------------------------------------------------------------
+struct WindowOut {
+  std::vector<int32_t> tokens;
+  std::vector<float> jump_times, probs;
+};
+struct ResultHolder {
+  wmx_result r{};
+  std::vector<wmx_window_result> win;
+  std::vector<WindowOut> data;
+};
+
+struct Ctx {
+  Model* m = nullptr;
+  wmx_opts o{};
+  std::vector<int32_t> suppress, align_heads;  // owned copies
+  hipStream_t st = nullptr;
+  DT dt = DT::BF16;
+  int maxB = 1, K = 1, R = 1, Tctx = 448;
+  long max_samples = 480000;
+  int fcap = 3001;
+  Special sp{51865};
+  // ---- buffers ----
+  char* buf = nullptr;
+  float* pcm = nullptr;
+  long* lens = nullptr;
+  int* seek = nullptr;
+  float *mel_raw = nullptr, *mel = nullptr;
+  int* wmax = nullptr;
+  uint16_t *im1 = nullptr, *h1 = nullptr, *im2 = nullptr, *ehb = nullptr, *eqkv = nullptr, *eao = nullptr, *ef1 = nullptr,
+           *enc_out = nullptr, *ckv = nullptr;
+  float* ex = nullptr;
+  // decoder
+  int dec_rows_max = 0;  // rows*Tn capacity of the decoder activation buffers
+  float* dx = nullptr;
+  uint16_t *dhb = nullptr, *dq = nullptr, *dao = nullptr, *dcq = nullptr, *df1 = nullptr, *kc = nullptr, *vc = nullptr;
+  float* logits = nullptr;
+  int logits_rows = 0;
+  float* ws = nullptr;
+  long ws_elems = 0;
+  int *hist = nullptr, *hist_tmp = nullptr, *anc = nullptr, *anc_tmp = nullptr, *pad_row = nullptr, *pad_win = nullptr;
+  int *slot = nullptr, *n_done = nullptr, *lang_slot = nullptr, *lang_tok = nullptr, *row_map = nullptr, *gather = nullptr;
+  float *lang_prob = nullptr, *nospeech = nullptr;
+  RowPtrs rp{}, rtmp{};
+  BeamState bs{};
+  int max_cand = 1;
+  int *ctok = nullptr;
+  float* clp = nullptr;
+  uint32_t* mask = nullptr;
+  // alignment
+  float *scores = nullptr, *align_scratch = nullptr, *align_out = nullptr, *tprob = nullptr;
+  int *a_ntok = nullptr, *a_nframes = nullptr, *a_target = nullptr, *a_heads = nullptr;
+  int a_heads_cap = 0;
+  int* pinned_i = nullptr;
+  // graph
+  hipGraphExec_t graph = nullptr;
+  int graph_B = -1;
+  // profiling
+  hipEvent_t ev[8];
+  float stage_ms[7] = {0};
+  int last_steps = 0;
+};
+
+static void sync(Ctx& c) { WMX_HIP(hipStreamSynchronize(c.st)); }
+
+static void alloc_ctx(Ctx& c) {
+  const wmx_dims& d = c.m->d;
+  const int da = d.n_audio_state, dt = d.n_text_state, M = d.n_mels, V = d.n_vocab, Lt = d.n_text_layer;
+  const int B = c.maxB, R = c.R, T = c.Tctx;
+  c.fcap = (int)(c.max_samples / 160) + 1;
+  c.dec_rows_max = std::max(R, B * T);
+  c.logits_rows = std::max({R, 2 * B, 256});
+  int nheads = c.align_heads.empty() ? (Lt - Lt / 2) * d.n_text_head : (int)c.align_heads.size() / 2;
+  int heads_per_layer = d.n_text_head;
+  c.a_heads_cap = std::max(nheads, heads_per_layer);
+  // split-K workspace: up to 8 splits of the widest decoder GEMM (4*dt) over R rows
+  c.ws_elems = (long)8 * std::max(R, 64) * 4 * dt;
+  Planner P;
+  P.add(&c.pcm, (size_t)B * c.max_samples);
+  P.add(&c.lens, B);
+  P.add(&c.seek, B);
+  P.add(&c.mel_raw, (size_t)B * M * c.fcap);
+  P.add(&c.wmax, B);
+  P.add(&c.mel, (size_t)B * M * 3000);
+  P.add(&c.im1, (size_t)B * 3000 * c.m->K1p);
+  P.add(&c.h1, (size_t)B * 3000 * da);
+  P.add(&c.im2, (size_t)B * 1500 * 3 * da);
+  P.add(&c.ex, (size_t)B * 1500 * da);
+  P.add(&c.ehb, (size_t)B * 1500 * da);
+  P.add(&c.eqkv, (size_t)B * 1500 * 3 * da);
+  P.add(&c.eao, (size_t)B * 1500 * da);
+  P.add(&c.ef1, (size_t)B * 1500 * 4 * da);
+  P.add(&c.enc_out, (size_t)B * 1500 * da);
+  P.add(&c.ckv, (size_t)B * 1500 * Lt * 2 * dt);
+  const int DR = c.dec_rows_max;
+  P.add(&c.dx, (size_t)DR * dt);
+  P.add(&c.dhb, (size_t)DR * dt);
+  P.add(&c.dq, (size_t)DR * dt);
+  P.add(&c.dao, (size_t)DR * dt);
+  P.add(&c.dcq, (size_t)DR * dt);
+  P.add(&c.df1, (size_t)DR * 4 * dt);
+  P.add(&c.kc, (size_t)Lt * T * R * dt);
+  P.add(&c.vc, (size_t)Lt * T * R * dt);
+  P.add(&c.logits, (size_t)c.logits_rows * V);
+  P.add(&c.ws, (size_t)c.ws_elems);
+  P.add(&c.hist, (size_t)R * T);
+  P.add(&c.hist_tmp, (size_t)R * T);
+  P.add(&c.anc, (size_t)R * T);
+  P.add(&c.anc_tmp, (size_t)R * T);
+  P.add(&c.pad_row, R);
+  P.add(&c.pad_win, B);
+  P.add(&c.slot, 4);
+  P.add(&c.n_done, 4);
+  P.add(&c.lang_slot, B);
+  P.add(&c.lang_tok, B);
+  P.add(&c.row_map, R);
+  P.add(&c.gather, 2 * B + R + B * T);
+  P.add(&c.lang_prob, B);
+  P.add(&c.nospeech, B);
+  for (RowPtrs* rp : {&c.rp, &c.rtmp}) {
+    P.add(&rp->ns, R);
+    P.add(&rp->last, R);
+    P.add(&rp->pen, R);
+    P.add(&rp->last_ts, R);
+    P.add(&rp->done, R);
+    P.add(&rp->sum_lp, R);
+  }
+  c.max_cand = std::max(1, (int)std::lround(c.K * (double)c.o.patience));
+  const int nf = B * c.max_cand;
+  P.add(&c.bs.win_done, B);
+  P.add(&c.bs.win_active, B);
+  P.add(&c.bs.fin_count, B);
+  P.add(&c.bs.fin_score, nf);
+  P.add(&c.bs.fin_parent, nf);
+  P.add(&c.bs.fin_len, nf);
+  P.add(&c.bs.fin_hist, (size_t)nf * T);
+  P.add(&c.bs.new_parent, R);
+  P.add(&c.bs.new_tok, R);
+  P.add(&c.bs.new_score, R);
+  P.add(&c.ctok, (size_t)R * 9);
+  P.add(&c.clp, (size_t)R * 9);
+  P.add(&c.mask, (V + 31) / 32);
+  P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
+  P.add(&c.align_scratch, (size_t)B * T * 1500);
+  P.add(&c.align_out, (size_t)B * T * 1500);
+  P.add(&c.tprob, (size_t)B * T);
+  P.add(&c.a_ntok, B);
+  P.add(&c.a_nframes, B);
+  P.add(&c.a_target, (size_t)B * T);
+  P.add(&c.a_heads, c.a_heads_cap + 8);
+  WMX_HIP(hipMalloc(&c.buf, P.off));
+  WMX_HIP(hipMemsetAsync(c.buf, 0, P.off, c.st));
+  P.bind(c.buf);
+  WMX_HIP(hipHostMalloc(&c.pinned_i, 64));
+  // suppress bitmask
+  std::vector<uint32_t> mask((V + 31) / 32, 0u);
+  for (int t : c.suppress)
+    if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
+  WMX_HIP(hipMemcpyAsync(c.mask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, c.st));
+  for (auto& e : c.ev) WMX_HIP(hipEventCreate(&e));
+  sync(c);
+}
+
+// ------------------------------------------------------------------------------------------------
+// GEMM dispatch
+// ------------------------------------------------------------------------------------------------
+static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ldw, int M, int N, int K, const Epi& e) {
+  GemmCall g;
+  g.A = A;
+  g.lda = lda;
+  g.W = W;
+  g.ldw = ldw;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.epi = e;
+  int bm, bn;
+  if (M >= 1024) {
+    g.tile = TILE_128x128;
+    bm = 128;
+    bn = 128;
+  } else if (M > 32) {
+    g.tile = TILE_64x64;
+    bm = 64;
+    bn = 64;
+  } else {
+    g.tile = TILE_32x64;
+    bm = 32;
+    bn = 64;
+  }
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  int splits = 1;
+  if (tiles < 200 && K >= 512) {
+    splits = (int)std::min<long>({8, K / 256, (256 + tiles - 1) / tiles});
+    while (splits > 1 && (long)splits * M * N > c.ws_elems) --splits;
+  }
+  g.splits = splits;
+  g.ws = c.ws;
+  g.ws_elems = c.ws_elems;
+  launch_gemm(c.dt, g, c.st);
+}
+
+static Epi epi(int kind, const float* bias, void* out, long ldc) {
+  Epi e;
+  e.kind = kind;
+  e.bias = bias;
+  e.out = out;
+  e.ldc = ldc;
+  return e;
+}
+
+// ------------------------------------------------------------------------------------------------
+// encoder
+// ------------------------------------------------------------------------------------------------
+static void encode(Ctx& c, int B) {
+  Model& m = *c.m;
+  const int da = m.d.n_audio_state, H = m.d.n_audio_head, M = m.d.n_mels;
+  const long rows = (long)B * 1500;
+  launch_im2col_conv1(c.dt, c.mel, B, M, m.K1p, c.im1, c.st);
+  gemm(c, c.im1, m.K1p, m.conv1w, m.K1p, B * 3000, da, m.K1p, epi(EPI_GELU16, m.conv1b, c.h1, da));
+  launch_im2col_conv2(c.dt, c.h1, B, da, c.im2, c.st);
+  Epi e2 = epi(EPI_GELU_POS32, m.conv2b, c.ex, da);
+  e2.pos = m.enc_pos;
+  e2.posT = 1500;
+  gemm(c, c.im2, 3 * da, m.conv2w, 3 * da, (int)rows, da, 3 * da, e2);
+  for (auto& L : m.enc) {
+    launch_layernorm(c.dt, c.ex, L.ln1g, L.ln1b, c.ehb, (int)rows, da, c.st);
+    gemm(c, c.ehb, da, L.wqkv, da, (int)rows, 3 * da, da, epi(EPI_STORE16, L.bqkv, c.eqkv, 3 * da));
+    AttnArgs a{};
+    a.q = c.eqkv;
+    a.k = c.eqkv + da;
+    a.v = c.eqkv + 2 * da;
+    a.q_ld = a.k_ld = a.v_ld = 3 * da;
+    a.q_bstride = a.k_bstride = a.v_bstride = 1500L * 3 * da;
+    a.o = c.eao;
+    a.o_ld = da;
+    a.o_bstride = 1500L * da;
+    a.B = B;
+    a.H = H;
+    a.Tq = a.Tk = 1500;
+    a.head_stride = 64;
+    launch_attn_encoder(c.dt, a, c.st);
+    gemm(c, c.eao, da, L.wo, da, (int)rows, da, da, epi(EPI_RESID32, L.bo, c.ex, da));
+    launch_layernorm(c.dt, c.ex, L.ln2g, L.ln2b, c.ehb, (int)rows, da, c.st);
+    gemm(c, c.ehb, da, L.wfc1, da, (int)rows, 4 * da, da, epi(EPI_GELU16, L.bfc1, c.ef1, 4 * da));
+    gemm(c, c.ef1, 4 * da, L.wfc2, 4 * da, (int)rows, da, 4 * da, epi(EPI_RESID32, L.bfc2, c.ex, da));
+  }
+  launch_layernorm(c.dt, c.ex, m.lnpg, m.lnpb, c.enc_out, (int)rows, da, c.st);
+}
+
+static void cross_kv(Ctx& c, int B) {
+  Model& m = *c.m;
+  const int dt = m.d.n_text_state, Lt = m.d.n_text_layer;
+  WMX_CHECK(m.d.n_audio_state == dt, "cross K/V: audio and text widths differ");
+  gemm(c, c.enc_out, dt, m.wckv, dt, B * 1500, Lt * 2 * dt, dt, epi(EPI_STORE16, m.bckv, c.ckv, (long)Lt * 2 * dt));
+}
+
+// ------------------------------------------------------------------------------------------------
+// decoder forward
+//   rows sequences x Tn new tokens at slots *slot .. *slot+Tn-1.  Token of (r, i) = tok[r*tok_ld + slot + i].
+//   The KV cache row of sequence r is r*rmul.  prefill: flash kernels (causal, first valid key pad_seq[r]);
+//   decode (Tn == 1): gather kernels through `anc` (null -> identity).  `align`: alignment-head scores.
+// ------------------------------------------------------------------------------------------------
+struct FwdArgs {
+  int rows, Tn, rmul;
+  const int* tok;
+  long tok_ld;
+  const int* pad_seq;  // per sequence (embed positions + flash kbegin)
+  bool prefill;
+  const int* anc;
+  bool align = false;
+};
+
+static void dec_forward(Ctx& c, const FwdArgs& f) {
+  Model& m = *c.m;
+  const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
+  const int rowsT = f.rows * f.Tn;
+  WMX_CHECK(rowsT <= c.dec_rows_max, "decoder: too many rows");
+  launch_embed(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, f.rows, f.Tn, f.pad_seq, c.slot, dt, c.dx, c.st);
+  const long ck_ld = (long)Lt * 2 * dt;
+  const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
+  for (int l = 0; l < Lt; ++l) {
+    DecLayer& L = m.dec[l];
+    uint16_t* kcl = c.kc + l * cache_layer;
+    uint16_t* vcl = c.vc + l * cache_layer;
+    launch_layernorm(c.dt, c.dx, L.ln1g, L.ln1b, c.dhb, rowsT, dt, c.st);
+    Epi eq = epi(EPI_QKV_CACHE, L.bqkv, c.dq, dt);
+    eq.d = dt;
+    eq.Tn = f.Tn;
+    eq.R = c.R;
+    eq.rmul = f.rmul;
+    eq.slot0 = c.slot;
+    eq.kc = kcl;
+    eq.vc = vcl;
+    gemm(c, c.dhb, dt, L.wqkv, dt, rowsT, 3 * dt, dt, eq);
+    if (f.prefill) {
+      AttnArgs a{};
+      a.q = c.dq;
+      a.q_ld = dt;
+      a.q_bstride = (long)f.Tn * dt;
+      a.k = kcl;
+      a.v = vcl;
+      a.k_ld = a.v_ld = (long)c.R * dt;
+      a.k_bstride = a.v_bstride = (long)f.rmul * dt;
+      a.o = c.dao;
+      a.o_ld = dt;
+      a.o_bstride = (long)f.Tn * dt;
+      a.B = f.rows;
+      a.H = H;
+      a.Tq = f.Tn;
+      a.Tk = f.Tn;  // prefill always starts at slot 0
+      a.head_stride = 64;
+      launch_attn_flash(c.dt, a, 1, 0, f.pad_seq, c.st);
+    } else {
+      DecAttnArgs a{};
+      a.q = c.dq;
+      a.q_ld = dt;
+      a.o = c.dao;
+      a.R = f.rows;
+      a.Tn = 1;
+      a.H = H;
+      a.d = dt;
+      a.kc = kcl;
+      a.vc = vcl;
+      a.anc = f.anc;
+      a.anc_ld = c.Tctx;
+      a.pad = f.pad_seq;
+      a.slot0 = c.slot;
+      launch_self_attn(c.dt, a, c.st);
+    }
+    gemm(c, c.dao, dt, L.wo, dt, rowsT, dt, dt, epi(EPI_RESID32, L.bo, c.dx, dt));
+    launch_layernorm(c.dt, c.dx, L.ln2g, L.ln2b, c.dhb, rowsT, dt, c.st);
+    gemm(c, c.dhb, dt, L.wcq, dt, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt));
+    const uint16_t* ckl = c.ckv + (size_t)l * 2 * dt;
+    if (f.prefill) {
+      AttnArgs a{};
+      a.q = c.dcq;
+      a.q_ld = dt;
+      a.q_bstride = (long)f.Tn * dt;
+      a.k = ckl;
+      a.v = ckl + dt;
+      a.k_ld = a.v_ld = ck_ld;
+      a.k_bstride = a.v_bstride = 1500L * ck_ld;
+      a.o = c.dao;
+      a.o_ld = dt;
+      a.o_bstride = (long)f.Tn * dt;
+      a.B = f.rows;
+      a.H = H;
+      a.Tq = f.Tn;
+      a.Tk = 1500;
+      a.head_stride = 64;
+      launch_attn_flash(c.dt, a, 0, 0, nullptr, c.st);
+    } else {
+      DecAttnArgs a{};
+      a.q = c.dcq;
+      a.q_ld = dt;
+      a.o = c.dao;
+      a.R = f.rows;
+      a.Tn = 1;
+      a.H = H;
+      a.d = dt;
+      a.ck = ckl;
+      a.ck_ld = ck_ld;
+      a.Tk = 1500;
+      a.rows_per_win = c.K;
+      launch_cross_attn(c.dt, a, c.st);
+    }
+    if (f.align) {
+      // alignment heads of this layer
+      std::vector<int> hs;
+      for (size_t i = 0; i + 1 < c.align_heads.size(); i += 2)
+        if (c.align_heads[i] == l) hs.push_back(c.align_heads[i + 1]);
+      if (!hs.empty()) {
+        WMX_HIP(hipMemcpyAsync(c.a_heads, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, c.st));
+        DecAttnArgs a{};
+        a.q = c.dcq;
+        a.q_ld = dt;
+        a.R = f.rows;
+        a.Tn = f.Tn;
+        a.H = H;
+        a.d = dt;
+        a.ck = ckl;
+        a.ck_ld = ck_ld;
+        a.Tk = 1500;
+        a.rows_per_win = 1;
+        launch_cross_scores(c.dt, a, c.a_heads, (int)hs.size(), c.scores, c.st);
+        launch_align_matrix_acc(c.scores, (int)hs.size(), rowsT, 1500, f.Tn, c.a_ntok, c.a_nframes,
+                                c.o.median_filter_width, f.rows, c.align_scratch, c.align_out, c.st);
+        // hipMemcpyAsync of a host vector: make sure it completed before hs goes out of scope
+        sync(c);
+      }
+    }
+    gemm(c, c.dao, dt, L.wco, dt, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt));
+    launch_layernorm(c.dt, c.dx, L.ln3g, L.ln3b, c.dhb, rowsT, dt, c.st);
+    gemm(c, c.dhb, dt, L.wfc1, dt, rowsT, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
+    gemm(c, c.df1, 4 * dt, L.wfc2, 4 * dt, rowsT, dt, 4 * dt, epi(EPI_RESID32, L.bfc2, c.dx, dt));
+  }
+}
+
+// final LN of selected rows + logits GEMM into c.logits [n][V]
+static void dec_logits(Ctx& c, const int* rows_idx, int n) {
+  Model& m = *c.m;
+  const int dt = m.d.n_text_state, V = m.d.n_vocab;
+  WMX_CHECK(n <= c.logits_rows, "logits: too many rows");
+  launch_layernorm_rows(c.dt, c.dx, rows_idx, m.lng, m.lnb, c.dhb, n, dt, c.st);
+  gemm(c, c.dhb, dt, m.tok_emb, dt, n, V, dt, epi(EPI_STORE32, nullptr, c.logits, V));
+}
+
+static void set_slot(Ctx& c, int v) {
+  c.pinned_i[0] = v;
+  WMX_HIP(hipMemcpyAsync(c.slot, c.pinned_i, 4, hipMemcpyHostToDevice, c.st));
+  sync(c);
+}
+
+// ------------------------------------------------------------------------------------------------
+// DTW (openai timing.dtw_cpu + backtrace), float32 cost accumulation like the oracle
+// ------------------------------------------------------------------------------------------------
+static void dtw(const float* x, int N, int Mc, int ld, std::vector<int>& ti, std::vector<int>& tj) {
+  std::vector<float> cost((size_t)(N + 1) * (Mc + 1), INFINITY);
+  std::vector<signed char> tr((size_t)(N + 1) * (Mc + 1), -1);
+  auto C = [&](int i, int j) -> float& { return cost[(size_t)i * (Mc + 1) + j]; };
+  auto Tr = [&](int i, int j) -> signed char& { return tr[(size_t)i * (Mc + 1) + j]; };
+  C(0, 0) = 0.f;
+  for (int j = 1; j <= Mc; ++j)
+    for (int i = 1; i <= N; ++i) {
+      const float c0 = C(i - 1, j - 1), c1 = C(i - 1, j), c2 = C(i, j - 1);
+      float v;
+      signed char t;
+      if (c0 < c1 && c0 < c2) {
+        v = c0;
+        t = 0;
+      } else if (c1 < c0 && c1 < c2) {
+        v = c1;
+        t = 1;
+      } else {
+        v = c2;
+        t = 2;
+      }
+      C(i, j) = -x[(size_t)(i - 1) * ld + (j - 1)] + v;
+      Tr(i, j) = t;
+    }
+  for (int j = 0; j <= Mc; ++j) Tr(0, j) = 2;
+  for (int i = 0; i <= N; ++i) Tr(i, 0) = 1;
+  int i = N, j = Mc;
+  ti.clear();
+  tj.clear();
+  while (i > 0 || j > 0) {
+    ti.push_back(i - 1);
+    tj.push_back(j - 1);
+    const signed char t = Tr(i, j);
+    if (t == 0) {
+      --i;
+      --j;
+    } else if (t == 1) {
+      --i;
+    } else {
+      --j;
+    }
+  }
+  std::reverse(ti.begin(), ti.end());
+  std::reverse(tj.begin(), tj.end());
+}
+
+// ------------------------------------------------------------------------------------------------
+// transcribe
+// ------------------------------------------------------------------------------------------------
+static void rec(Ctx& c, int i) { WMX_HIP(hipEventRecord(c.ev[i], c.st)); }
+
+static void logmel_dev(Ctx& c, const float* pcm_dev, long stride, const long* lens_host, const int32_t* seek_host, int B,
+                       float* out_dev) {
+  Model& m = *c.m;
+  long maxlen = 0;
+  for (int b = 0; b < B; ++b) {
+    WMX_CHECK(lens_host[b] >= 0 && lens_host[b] <= c.max_samples && lens_host[b] <= stride, "logmel: bad length");
+    maxlen = std::max(maxlen, lens_host[b]);
+  }
+  std::vector<int> sk(B, 0);
+  if (seek_host)
+    for (int b = 0; b < B; ++b) sk[b] = seek_host[b];
+  WMX_HIP(hipMemcpyAsync(c.lens, lens_host, B * sizeof(long), hipMemcpyHostToDevice, c.st));
+  WMX_HIP(hipMemcpyAsync(c.seek, sk.data(), B * 4, hipMemcpyHostToDevice, c.st));
+  launch_logmel(pcm_dev, stride, c.lens, c.seek, B, (int)(maxlen / 160) + 1, m.mel_basis, m.mel_first, m.mel_count,
+                m.mel_off, m.mel_w, m.d.n_mels, c.mel_raw, c.fcap, c.wmax, out_dev, c.st);
+  sync(c);  // sk / lens host vectors
+}
+
+static void run_step(Ctx& c, int B) {
+  // one decode step: forward all rows at slot *slot, select, update (advances *slot)
+  Model& m = *c.m;
+  FwdArgs f;
+  f.rows = c.K * B;
+  f.Tn = 1;
+  f.rmul = 1;
+  f.tok = c.hist;
+  f.tok_ld = c.Tctx;
+  f.pad_seq = c.pad_row;
+  f.prefill = false;
+  f.anc = c.K > 1 ? c.anc : nullptr;
+  dec_forward(c, f);
+  dec_logits(c, nullptr, f.rows);
+  RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
+              c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
+  launch_logits_select(c.logits, m.d.n_vocab, ro, c.rp, f.rows, c.K + (c.K > 1 ? 1 : 0), c.ctok, c.clp, nullptr, c.st);
+  if (c.K == 1)
+    launch_greedy_update(c.rp, c.ctok, c.clp, f.rows, c.sp.timestamp_begin, c.sp.eot, c.hist, c.Tctx, c.slot, c.n_done,
+                         c.st);
+  else
+    launch_beam_step(c.rp, c.rtmp, c.ctok, c.clp, B, c.K, c.max_cand, c.sp.timestamp_begin, c.sp.eot, c.slot, c.hist,
+                     c.hist_tmp, c.anc, c.anc_tmp, c.Tctx, c.bs, c.n_done, c.st);
+}
+
+static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const long* lens, const int32_t* seek, int B,
+                                const int32_t* prompt_ids, const int32_t* prompt_lens) {
+  Model& m = *c.m;
+  WMX_CHECK(m.initialized, "transcribe: model weights not initialised");
+  WMX_CHECK(B >= 1 && B <= c.maxB, "transcribe: batch exceeds max_batch");
+  const int K = c.K, R = K * B, V = m.d.n_vocab, T = c.Tctx;
+  const Special& sp = c.sp;
+  rec(c, 0);
+  logmel_dev(c, pcm_dev, stride, lens, seek, B, c.mel);
+  rec(c, 1);
+  encode(c, B);
+  rec(c, 2);
+  cross_kv(c, B);
+  rec(c, 3);
+
+  // ---- prompts (left padded to Pmax) ----
+  std::vector<std::vector<int>> seqs(B);
+  const bool detect = c.o.language < 0;
+  const int lang_ph = detect ? sp.lang0 : c.o.language;
+  const int task_tok = c.o.task == WMX_TASK_TRANSLATE ? sp.translate : sp.transcribe;
+  long poff = 0;
+  for (int b = 0; b < B; ++b) {
+    std::vector<int>& s = seqs[b];
+    const int pl = prompt_lens ? prompt_lens[b] : 0;
+    if (pl > 0) {
+      s.push_back(sp.sot_prev);
+      const int keep = std::min(pl, T / 2 - 1);
+      for (int i = pl - keep; i < pl; ++i) s.push_back(prompt_ids[poff + i]);
+    }
+    poff += pl;
+    s.push_back(sp.sot);
+    s.push_back(lang_ph);
+    s.push_back(task_tok);
+    if (c.o.without_timestamps) s.push_back(sp.no_timestamps);
+  }
+  int Pmax = 0;
+  for (auto& s : seqs) Pmax = std::max(Pmax, (int)s.size());
+  const int sot_tail = c.o.without_timestamps ? 4 : 3;  // sot sits at Pmax - sot_tail
+  std::vector<int> hist((size_t)R * T, 0), pad_row(R), pad_win(B), anc((size_t)R * T, 0), lslot(B, Pmax - sot_tail + 1);
+  for (int b = 0; b < B; ++b) {
+    const int pad = Pmax - (int)seqs[b].size();
+    pad_win[b] = pad;
+    for (int j = 0; j < K; ++j) {
+      const int r = b * K + j;
+      pad_row[r] = pad;
+      for (size_t i = 0; i < seqs[b].size(); ++i) hist[(size_t)r * T + pad + i] = seqs[b][i];
+      for (int s = 0; s < T; ++s) anc[(size_t)r * T + s] = s < Pmax ? b * K : r;
+    }
+  }
+  WMX_HIP(hipMemcpyAsync(c.hist, hist.data(), hist.size() * 4, hipMemcpyHostToDevice, c.st));
+  WMX_HIP(hipMemcpyAsync(c.anc, anc.data(), anc.size() * 4, hipMemcpyHostToDevice, c.st));
+  WMX_HIP(hipMemcpyAsync(c.pad_row, pad_row.data(), R * 4, hipMemcpyHostToDevice, c.st));
+  WMX_HIP(hipMemcpyAsync(c.pad_win, pad_win.data(), B * 4, hipMemcpyHostToDevice, c.st));
+  WMX_HIP(hipMemcpyAsync(c.lang_slot, lslot.data(), B * 4, hipMemcpyHostToDevice, c.st));
+  // row state reset
+  WMX_HIP(hipMemsetAsync(c.rp.ns, 0, R * 4, c.st));
+  WMX_HIP(hipMemsetAsync(c.rp.last, 0, R * 4, c.st));
+  WMX_HIP(hipMemsetAsync(c.rp.pen, 0, R * 4, c.st));
+  WMX_HIP(hipMemsetD32Async((hipDeviceptr_t)c.rp.last_ts, -1, R, c.st));
+  WMX_HIP(hipMemsetAsync(c.rp.done, 0, R * 4, c.st));
+  WMX_HIP(hipMemsetAsync(c.rp.sum_lp, 0, R * 4, c.st));
+  WMX_HIP(hipMemsetAsync(c.bs.win_done, 0, B * 4, c.st));
+  WMX_HIP(hipMemsetAsync(c.bs.fin_count, 0, B * 4, c.st));
+  WMX_HIP(hipMemsetAsync(c.n_done, 0, 4, c.st));
+  std::vector<int> rmap(R);
+  for (int r = 0; r < R; ++r) rmap[r] = r / K;
+  WMX_HIP(hipMemcpyAsync(c.row_map, rmap.data(), R * 4, hipMemcpyHostToDevice, c.st));
+  sync(c);
+
+  // ---- language detection: one decoder step on <|startoftranscript|> ----
+  std::vector<int> lang_out(B, c.o.language);
+  std::vector<float> lang_p(B, 1.0f);
+  if (detect) {
+    // a temporary token row per window: hist_tmp[b*K][0] = sot
+    std::vector<int> t1((size_t)B * K * T, sp.sot);
+    WMX_HIP(hipMemcpyAsync(c.hist_tmp, t1.data(), t1.size() * 4, hipMemcpyHostToDevice, c.st));
+    set_slot(c, 0);
+    FwdArgs f;
+    f.rows = B;
+    f.Tn = 1;
+    f.rmul = K;
+    f.tok = c.hist_tmp;
+    f.tok_ld = (long)K * T;
+    f.pad_seq = nullptr;
+    f.prefill = true;
+    f.anc = nullptr;
+    dec_forward(c, f);
+    dec_logits(c, nullptr, B);
+    launch_lang_detect(c.logits, V, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st);
+  }
+  rec(c, 4);
+
+  // ---- prompt prefill ----
+  set_slot(c, 0);
+  {
+    FwdArgs f;
+    f.rows = B;
+    f.Tn = Pmax;
+    f.rmul = K;
+    f.tok = c.hist;
+    f.tok_ld = (long)K * T;
+    f.pad_seq = c.pad_win;
+    f.prefill = true;
+    f.anc = nullptr;
+    dec_forward(c, f);
+    std::vector<int> g(2 * B);
+    for (int b = 0; b < B; ++b) {
+      g[b] = b * Pmax + Pmax - 1;
+      g[B + b] = b * Pmax + Pmax - sot_tail;
+    }
+    WMX_HIP(hipMemcpyAsync(c.gather, g.data(), g.size() * 4, hipMemcpyHostToDevice, c.st));
+    dec_logits(c, c.gather, 2 * B);
+    launch_token_prob(c.logits + (size_t)B * V, V, V, sp.no_speech, B, c.nospeech, c.st);
+    sync(c);
+  }
+  // first selection from the prefill logits (rows of a window share their window's logits row)
+  const int max_new = std::max(0, std::min(c.o.max_new_tokens, T - Pmax));
+  set_slot(c, Pmax - 1);
+  int steps = 0;
+  if (max_new > 0) {
+    RuleOpts ro{V, sp.eot, sp.timestamp_begin, sp.no_timestamps, sp.blank, c.o.suppress_blank,
+                c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
+    launch_logits_select(c.logits, V, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, c.row_map, c.st);
+    if (K == 1)
+      launch_greedy_update(c.rp, c.ctok, c.clp, R, sp.timestamp_begin, sp.eot, c.hist, T, c.slot, c.n_done, c.st);
+    else
+      launch_beam_step(c.rp, c.rtmp, c.ctok, c.clp, B, K, c.max_cand, sp.timestamp_begin, sp.eot, c.slot, c.hist,
+                       c.hist_tmp, c.anc, c.anc_tmp, T, c.bs, c.n_done, c.st);
+    steps = 1;
+  }
+  rec(c, 5);
+  // ---- decode loop: one hipGraph replay per step ----
+  const int need_done = K == 1 ? R : B;
+  hipGraphExec_t ge = nullptr;
+  hipGraph_t gph = nullptr;
+  if (c.o.use_graph && steps < max_new) {
+    WMX_HIP(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
+    run_step(c, B);
+    WMX_HIP(hipStreamEndCapture(c.st, &gph));
+    WMX_HIP(hipGraphInstantiate(&ge, gph, nullptr, nullptr, 0));
+  }
+  while (steps < max_new) {
+    const int chunk = std::min(8, max_new - steps);
+    for (int i = 0; i < chunk; ++i) {
+      if (ge)
+        WMX_HIP(hipGraphLaunch(ge, c.st));
+      else
+        run_step(c, B);
+    }
+    steps += chunk;
+    WMX_HIP(hipMemcpyAsync(c.pinned_i, c.n_done, 4, hipMemcpyDeviceToHost, c.st));
+    sync(c);
+    if (c.pinned_i[0] >= need_done) break;
+  }
+  if (ge) WMX_HIP(hipGraphExecDestroy(ge));
+  if (gph) WMX_HIP(hipGraphDestroy(gph));
+  c.last_steps = steps;
+  rec(c, 6);
+
+  // ---- read back and finalise (openai BeamSearchDecoder.finalize + MaximumLikelihoodRanker) ----
+  std::vector<int> h((size_t)R * T), ns(R), done(R);
+  std::vector<float> slp(R), nosp(B);
+  WMX_HIP(hipMemcpyAsync(h.data(), c.hist, h.size() * 4, hipMemcpyDeviceToHost, c.st));
+  WMX_HIP(hipMemcpyAsync(ns.data(), c.rp.ns, R * 4, hipMemcpyDeviceToHost, c.st));
+  WMX_HIP(hipMemcpyAsync(done.data(), c.rp.done, R * 4, hipMemcpyDeviceToHost, c.st));
+  WMX_HIP(hipMemcpyAsync(slp.data(), c.rp.sum_lp, R * 4, hipMemcpyDeviceToHost, c.st));
+  WMX_HIP(hipMemcpyAsync(nosp.data(), c.nospeech, B * 4, hipMemcpyDeviceToHost, c.st));
+  if (detect) {
+    WMX_HIP(hipMemcpyAsync(lang_out.data(), c.lang_tok, B * 4, hipMemcpyDeviceToHost, c.st));
+    WMX_HIP(hipMemcpyAsync(lang_p.data(), c.lang_prob, B * 4, hipMemcpyDeviceToHost, c.st));
+  }
+  const int nfin = B * c.max_cand;
+  std::vector<int> fcount(B), flen(nfin), fh;
+  std::vector<float> fscore(nfin);
+  if (K > 1) {
+    fh.resize((size_t)nfin * T);
+    WMX_HIP(hipMemcpyAsync(fcount.data(), c.bs.fin_count, B * 4, hipMemcpyDeviceToHost, c.st));
+    WMX_HIP(hipMemcpyAsync(flen.data(), c.bs.fin_len, nfin * 4, hipMemcpyDeviceToHost, c.st));
+    WMX_HIP(hipMemcpyAsync(fscore.data(), c.bs.fin_score, nfin * 4, hipMemcpyDeviceToHost, c.st));
+    WMX_HIP(hipMemcpyAsync(fh.data(), c.bs.fin_hist, fh.size() * 4, hipMemcpyDeviceToHost, c.st));
+  }
+  sync(c);
+  auto* res = new ResultHolder();
+  res->data.resize(B);
+  res->win.resize(B);
+  std::vector<float> sum_lp(B);
+  for (int b = 0; b < B; ++b) {
+    std::vector<int>& toks = res->data[b].tokens;
+    if (K == 1) {
+      for (int i = 0; i < ns[b]; ++i) toks.push_back(h[(size_t)b * T + Pmax + i]);
+      sum_lp[b] = slp[b];
+    } else {
+      struct Cand {
+        std::vector<int> t;
+        float s;
+      };
+      std::vector<Cand> fin;
+      for (int f = 0; f < fcount[b]; ++f) {
+        const int idx = b * c.max_cand + f;
+        Cand cd;
+        for (int s = Pmax; s < flen[idx]; ++s) cd.t.push_back(fh[(size_t)idx * T + s]);
+        cd.s = fscore[idx];
+        fin.push_back(cd);
+      }
+      if ((int)fin.size() < K) {
+        std::vector<int> order(K);
+        for (int j = 0; j < K; ++j) order[j] = j;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int a, int bb) { return slp[b * K + a] > slp[b * K + bb]; });
+        for (int j : order) {
+          const int r = b * K + j;
+          Cand cd;
+          for (int i = 0; i < ns[r]; ++i) cd.t.push_back(h[(size_t)r * T + Pmax + i]);
+          cd.s = slp[r];
+          bool dup = false;
+          for (auto& e : fin) dup = dup || e.t == cd.t;
+          if (!dup) fin.push_back(cd);
+          if ((int)fin.size() >= K) break;
+        }
+      }
+      int best = -1;
+      double best_score = -INFINITY;
+      for (size_t i = 0; i < fin.size(); ++i) {
+        const double L = std::max<size_t>(fin[i].t.size(), 1);
+        const double pen = c.o.length_penalty == 1.0f ? L : std::pow((5.0 + L) / 6.0, (double)c.o.length_penalty);
+        const double sc = fin[i].s / pen;
+        if (best < 0 || sc > best_score) {
+          best = (int)i;
+          best_score = sc;
+        }
+      }
+      if (best >= 0) {
+        toks = fin[best].t;
+        sum_lp[b] = fin[best].s;
+      }
+    }
+    wmx_window_result& w = res->win[b];
+    w.language = lang_out[b];
+    w.language_prob = lang_p[b];
+    w.n_tokens = (int)toks.size();
+    w.sum_logprob = sum_lp[b];
+    w.avg_logprob = sum_lp[b] / (toks.size() + 1);
+    w.no_speech_prob = nosp[b];
+    const int F = (int)(lens[b] / 160) + 1;
+    const int sk = seek ? seek[b] : 0;
+    w.seek_frames = std::max(0, std::min(3000, F - 1 - sk));
+  }
+
+  // ---- word alignment: forward sot + text + eot, alignment-head attention -> matrix -> DTW ----
+  if (c.o.word_timestamps) {
+    std::vector<std::vector<int>> rows(B);
+    std::vector<int> ntext(B);
+    int Tn = 0;
+    for (int b = 0; b < B; ++b) {
+      std::vector<int>& s = rows[b];
+      // openai timing.find_alignment: sot_sequence + <|notimestamps|> + text tokens + eot
+      s = {sp.sot, res->win[b].language, task_tok, sp.no_timestamps};
+      for (int t : res->data[b].tokens)
+        if (t < sp.eot) s.push_back(t);
+      ntext[b] = (int)s.size() - 4;
+      s.push_back(sp.eot);
+      Tn = std::max(Tn, (int)s.size());
+    }
+    WMX_CHECK(Tn <= T, "alignment: sequence too long");
+    std::vector<int> tok((size_t)B * K * T, 0), ntok(B), nframes(B), target((size_t)B * Tn, -1);
+    for (int b = 0; b < B; ++b) {
+      for (size_t i = 0; i < rows[b].size(); ++i) tok[(size_t)b * K * T + i] = rows[b][i];
+      ntok[b] = (int)rows[b].size();
+      nframes[b] = res->win[b].seek_frames;
+      for (int i = 0; i < ntext[b]; ++i) target[(size_t)b * Tn + 3 + i] = rows[b][4 + i];
+    }
+    WMX_HIP(hipMemcpyAsync(c.hist_tmp, tok.data(), tok.size() * 4, hipMemcpyHostToDevice, c.st));
+    WMX_HIP(hipMemcpyAsync(c.a_ntok, ntok.data(), B * 4, hipMemcpyHostToDevice, c.st));
+    WMX_HIP(hipMemcpyAsync(c.a_nframes, nframes.data(), B * 4, hipMemcpyHostToDevice, c.st));
+    WMX_HIP(hipMemcpyAsync(c.a_target, target.data(), target.size() * 4, hipMemcpyHostToDevice, c.st));
+    set_slot(c, 0);
+    launch_align_matrix_zero(c.align_out, B, Tn, 1500, c.st);
+    FwdArgs f;
+    f.rows = B;
+    f.Tn = Tn;
+    f.rmul = K;
+    f.tok = c.hist_tmp;
+    f.tok_ld = (long)K * T;
+    f.pad_seq = nullptr;
+    f.prefill = true;
+    f.anc = nullptr;
+    f.align = true;
+    dec_forward(c, f);
+    const int nh_total = (int)c.align_heads.size() / 2;
+    launch_align_matrix_scale(c.align_out, B, Tn, 1500, c.a_ntok, c.a_nframes, 1.0f / nh_total, c.st);
+    // text-token probabilities: logits of every position, in chunks of logits_rows
+    const int rows_all = B * Tn;
+    for (int r0 = 0; r0 < rows_all; r0 += c.logits_rows) {
+      const int n = std::min(c.logits_rows, rows_all - r0);
+      std::vector<int> g(n);
+      for (int i = 0; i < n; ++i) g[i] = r0 + i;
+      WMX_HIP(hipMemcpyAsync(c.gather, g.data(), n * 4, hipMemcpyHostToDevice, c.st));
+      dec_logits(c, c.gather, n);
+      launch_text_prob(c.logits, V, sp.eot, c.a_target + r0, n, c.tprob + r0, c.st);
+      sync(c);
+    }
+    std::vector<float> mat((size_t)B * Tn * 1500), tp((size_t)B * Tn);
+    WMX_HIP(hipMemcpyAsync(mat.data(), c.align_out, mat.size() * 4, hipMemcpyDeviceToHost, c.st));
+    WMX_HIP(hipMemcpyAsync(tp.data(), c.tprob, tp.size() * 4, hipMemcpyDeviceToHost, c.st));
+    sync(c);
+    // DTW per window on host threads
+    std::vector<std::thread> th;
+    std::atomic<int> next{0};
+    const int nth = std::min<int>(B, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    for (int t = 0; t < nth; ++t)
+      th.emplace_back([&]() {
+        std::vector<int> ti, tj;
+        for (int b = next++; b < B; b = next++) {
+          WindowOut& wo = res->data[b];
+          const int n = ntext[b] + 1, nf = nframes[b] / 2;
+          wo.probs.assign(tp.begin() + (size_t)b * Tn + 3, tp.begin() + (size_t)b * Tn + 3 + ntext[b]);
+          if (nf <= 0) {
+            wo.jump_times.assign(n, 0.f);
+            continue;
+          }
+          dtw(mat.data() + ((size_t)b * Tn + 3) * 1500, n, nf, 1500, ti, tj);
+          wo.jump_times.clear();
+          for (size_t k = 0; k < ti.size(); ++k)
+            if (k == 0 || ti[k] != ti[k - 1]) wo.jump_times.push_back(tj[k] / 50.0f);
+          wo.jump_times.resize(n, wo.jump_times.empty() ? 0.f : wo.jump_times.back());
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  rec(c, 7);
+  WMX_HIP(hipEventSynchronize(c.ev[7]));
+  for (int i = 0; i < 7; ++i) WMX_HIP(hipEventElapsedTime(&c.stage_ms[i], c.ev[i], c.ev[i + 1]));
+
+  for (int b = 0; b < B; ++b) {
+    wmx_window_result& w = res->win[b];
+    WindowOut& wo = res->data[b];
+    w.tokens = wo.tokens.data();
+    w.n_text_tokens = 0;
+    for (int t : wo.tokens) w.n_text_tokens += t < sp.eot;
+    w.jump_times = wo.jump_times.empty() ? nullptr : wo.jump_times.data();
+    w.text_token_probs = wo.probs.empty() ? nullptr : wo.probs.data();
+  }
+  res->r.n_windows = B;
+  res->r.windows = res->win.data();
+  return res;
+}
+
+}  // namespace wmx
+
+// =================================================================================================
+// C ABI
+// =================================================================================================
+using namespace wmx;
+
+struct wmx_model {
+  Model m;
+};
+struct wmx_ctx {
+  Ctx c;
+};
+
+template <class F>
+static wmx_status guard(F&& f) {
+  try {
+    f();
+    return WMX_OK;
+  } catch (const Error& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "out of memory";
+    return WMX_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return WMX_ERR_STATE;
+  }
+}
+
+extern "C" {
+
+const char* wmx_last_error(void) { return g_err.c_str(); }
+const char* wmx_version(void) { return "wmx 0.1 (gfx950)"; }
+int wmx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_model** out) {
+  return guard([&] {
+    WMX_CHECK(dims && out, "null argument");
+    WMX_CHECK(dtype == WMX_DTYPE_BF16 || dtype == WMX_DTYPE_F16, "dtype");
+    auto* w = new wmx_model();
+    try {
+      w->m.d = *dims;
+      w->m.device = device;
+      w->m.dt = dtype == WMX_DTYPE_F16 ? DT::F16 : DT::BF16;
+      WMX_HIP(hipSetDevice(device));
+      WMX_HIP(hipStreamCreateWithFlags(&w->m.st, hipStreamNonBlocking));
+      build_model(w->m);
+    } catch (...) {
+      if (w->m.arena) (void)hipFree(w->m.arena);
+      delete w;
+      throw;
+    }
+    *out = w;
+  });
+}
+
+void wmx_model_free(wmx_model* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->m.device);
+  if (m->m.arena) (void)hipFree(m->m.arena);
+  if (m->m.st) (void)hipStreamDestroy(m->m.st);
+  delete m;
+}
+
+wmx_status wmx_model_init_synthetic(wmx_model* w, uint64_t seed) {
+  return guard([&] {
+    Model& m = w->m;
+    WMX_HIP(hipSetDevice(m.device));
+    for (const TensorEntry& e : m.entries) {
+      InitSpec s{};
+      s.tid = e.tid;
+      s.scale = e.scale;
+      s.offset = e.offset;
+      s.n = e.n;
+      s.kind = e.kind;
+      s.O = e.O;
+      s.C = e.C;
+      s.Kp = e.Kp;
+      s.dst = e.dst;
+      s.store_f32 = e.store_f32;
+      launch_init_tensor(m.dt, seed, s, m.st);
+    }
+    WMX_HIP(hipStreamSynchronize(m.st));
+    m.initialized = true;
+  });
+}
+
+static const TensorEntry& find_entry(Model& m, const char* name, int64_t n) {
+  auto it = m.by_name.find(name);
+  WMX_CHECK(it != m.by_name.end(), std::string("unknown tensor ") + name);
+  const TensorEntry& e = m.entries[it->second];
+  WMX_CHECK(n == e.n, std::string("size mismatch for ") + name);
+  return e;
+}
+
+wmx_status wmx_model_set_tensor(wmx_model* w, const char* name, const float* data, int64_t n) {
+  return guard([&] {
+    Model& m = w->m;
+    WMX_HIP(hipSetDevice(m.device));
+    if (std::string(name) == "encoder.embed_positions.weight") {
+      WMX_CHECK(n == 1500L * m.d.n_audio_state, "size mismatch");
+      WMX_HIP(hipMemcpy(m.enc_pos, data, n * 4, hipMemcpyHostToDevice));
+      return;
+    }
+    const TensorEntry& e = find_entry(m, name, n);
+    if (e.store_f32) {
+      WMX_HIP(hipMemcpy(e.dst, data, n * 4, hipMemcpyHostToDevice));
+      return;
+    }
+    if (e.kind == 1) {
+      std::vector<uint16_t> h((size_t)e.O * e.Kp, 0);
+      for (long i = 0; i < n; ++i) {
+        const int kk = (int)(i % 3), c = (int)((i / 3) % e.C);
+        const long o = i / 3 / e.C;
+        h[o * e.Kp + (long)kk * e.C + c] = m.dt == DT::BF16 ? host_f32_to_bf16(data[i]) : host_f32_to_f16(data[i]);
+      }
+      WMX_HIP(hipMemcpy(e.dst, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    } else {
+      std::vector<uint16_t> h(n);
+      for (long i = 0; i < n; ++i) h[i] = m.dt == DT::BF16 ? host_f32_to_bf16(data[i]) : host_f32_to_f16(data[i]);
+      WMX_HIP(hipMemcpy(e.dst, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    }
+  });
+}
+
+wmx_status wmx_model_get_tensor(wmx_model* w, const char* name, float* out, int64_t n) {
+  return guard([&] {
+    Model& m = w->m;
+    WMX_HIP(hipSetDevice(m.device));
+    WMX_HIP(hipStreamSynchronize(m.st));
+    if (std::string(name) == "encoder.embed_positions.weight") {
+      WMX_CHECK(n == 1500L * m.d.n_audio_state, "size mismatch");
+      WMX_HIP(hipMemcpy(out, m.enc_pos, n * 4, hipMemcpyDeviceToHost));
+      return;
+    }
+    const TensorEntry& e = find_entry(m, name, n);
+    if (e.store_f32) {
+      WMX_HIP(hipMemcpy(out, e.dst, n * 4, hipMemcpyDeviceToHost));
+      return;
+    }
+    const long dn = e.kind == 1 ? (long)e.O * e.Kp : n;
+    std::vector<uint16_t> h(dn);
+    WMX_HIP(hipMemcpy(h.data(), e.dst, dn * 2, hipMemcpyDeviceToHost));
+    for (long i = 0; i < n; ++i) {
+      long di = i;
+      if (e.kind == 1) {
+        const int kk = (int)(i % 3), c = (int)((i / 3) % e.C);
+        const long o = i / 3 / e.C;
+        di = o * e.Kp + (long)kk * e.C + c;
+      }
+      out[i] = m.dt == DT::BF16 ? host_bf16_to_f32(h[di]) : host_f16_to_f32(h[di]);
+    }
+  });
+}
+
+int64_t wmx_model_n_params(const wmx_model* w) {
+  int64_t n = 0;
+  for (auto& e : w->m.entries) n += e.n;
+  return n;
+}
+
+wmx_status wmx_model_arena(wmx_model* w, void** ptr, size_t* bytes) {
+  return guard([&] {
+    *ptr = w->m.arena;
+    *bytes = w->m.arena_bytes;
+  });
+}
+
+wmx_status wmx_model_arena_loaded(wmx_model* w) {
+  return guard([&] { w->m.initialized = true; });
+}
+
+void wmx_opts_default(wmx_opts* o) {
+  std::memset(o, 0, sizeof(*o));
+  o->max_batch = 1;
+  o->beam_size = 5;
+  o->patience = 1.0f;
+  o->length_penalty = 1.0f;
+  o->max_new_tokens = 448;
+  o->task = WMX_TASK_TRANSCRIBE;
+  o->language = -1;
+  o->without_timestamps = 0;
+  o->max_initial_timestamp_index = 50;
+  o->suppress_blank = 1;
+  o->word_timestamps = 1;
+  o->median_filter_width = 7;
+  o->use_graph = 1;
+  o->max_audio_samples = 480000;
+}
+
+wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
+  return guard([&] {
+    WMX_CHECK(w && o && out, "null argument");
+    WMX_CHECK(o->max_batch >= 1 && o->beam_size >= 1 && o->beam_size <= 8, "opts: batch / beam");
+    WMX_CHECK(o->beam_size * o->max_batch <= 1024, "opts: beam * batch <= 1024");
+    WMX_CHECK(o->median_filter_width >= 1 && o->median_filter_width <= 15 && o->median_filter_width % 2 == 1,
+              "opts: median_filter_width");
+    WMX_HIP(hipSetDevice(w->m.device));
+    auto* x = new wmx_ctx();
+    Ctx& c = x->c;
+    try {
+      c.m = &w->m;
+      c.o = *o;
+      c.dt = w->m.dt;
+      c.maxB = o->max_batch;
+      c.K = o->beam_size;
+      c.R = c.K * c.maxB;
+      c.Tctx = w->m.d.n_text_ctx;
+      c.max_samples = o->max_audio_samples > 0 ? o->max_audio_samples : 480000;
+      c.sp = Special(w->m.d.n_vocab);
+      if (o->suppress_tokens && o->n_suppress_tokens > 0)
+        c.suppress.assign(o->suppress_tokens, o->suppress_tokens + o->n_suppress_tokens);
+      const int Lt = w->m.d.n_text_layer, Ht = w->m.d.n_text_head;
+      if (o->alignment_heads && o->n_alignment_heads > 0) {
+        c.align_heads.assign(o->alignment_heads, o->alignment_heads + 2 * o->n_alignment_heads);
+        for (size_t i = 0; i + 1 < c.align_heads.size(); i += 2)
+          WMX_CHECK(c.align_heads[i] >= 0 && c.align_heads[i] < Lt && c.align_heads[i + 1] >= 0 &&
+                        c.align_heads[i + 1] < Ht,
+                    "opts: alignment head out of range");
+      } else {
+        for (int l = Lt / 2; l < Lt; ++l)
+          for (int h = 0; h < Ht; ++h) {
+            c.align_heads.push_back(l);
+            c.align_heads.push_back(h);
+          }
+      }
+      c.o.suppress_tokens = nullptr;
+      c.o.alignment_heads = nullptr;
+      WMX_HIP(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
+      alloc_ctx(c);
+    } catch (...) {
+      if (c.buf) (void)hipFree(c.buf);
+      delete x;
+      throw;
+    }
+    *out = x;
+  });
+}
+
+void wmx_ctx_destroy(wmx_ctx* x) {
+  if (!x) return;
+  Ctx& c = x->c;
+  (void)hipSetDevice(c.m->device);
+  (void)hipStreamSynchronize(c.st);
+  if (c.buf) (void)hipFree(c.buf);
+  if (c.pinned_i) (void)hipHostFree(c.pinned_i);
+  for (auto& e : c.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c.st) (void)hipStreamDestroy(c.st);
+  delete x;
+}
+
+void* wmx_ctx_stream(wmx_ctx* x) { return (void*)x->c.st; }
+
+wmx_status wmx_logmel_device(wmx_ctx* x, const float* pcm_dev, int64_t stride, const int64_t* lens, const int32_t* seek,
+                             int B, float* mel_out_dev) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(B >= 1 && B <= c.maxB, "logmel: batch");
+    WMX_HIP(hipSetDevice(c.m->device));
+    std::vector<long> l(lens, lens + B);
+    logmel_dev(c, pcm_dev, (long)stride, l.data(), seek, B, mel_out_dev);
+  });
+}
+
+wmx_status wmx_logmel(wmx_ctx* x, const float* pcm, int64_t stride, const int64_t* lens, const int32_t* seek, int B,
+                      float* mel_out) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(B >= 1 && B <= c.maxB, "logmel: batch");
+    WMX_CHECK(stride <= c.max_samples, "logmel: stride exceeds max_audio_samples");
+    WMX_HIP(hipSetDevice(c.m->device));
+    WMX_HIP(hipMemcpyAsync(c.pcm, pcm, (size_t)B * stride * 4, hipMemcpyHostToDevice, c.st));
+    std::vector<long> l(lens, lens + B);
+    logmel_dev(c, c.pcm, (long)stride, l.data(), seek, B, c.mel);
+    WMX_HIP(hipMemcpyAsync(mel_out, c.mel, (size_t)B * c.m->d.n_mels * 3000 * 4, hipMemcpyDeviceToHost, c.st));
+    sync(c);
+  });
+}
+
+wmx_status wmx_encode_device(wmx_ctx* x, const float* mel_dev, int B) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(c.m->initialized, "encode: weights not initialised");
+    WMX_CHECK(B >= 1 && B <= c.maxB, "encode: batch");
+    WMX_HIP(hipSetDevice(c.m->device));
+    if (mel_dev != c.mel)
+      WMX_HIP(hipMemcpyAsync(c.mel, mel_dev, (size_t)B * c.m->d.n_mels * 3000 * 4, hipMemcpyDeviceToDevice, c.st));
+    encode(c, B);
+    cross_kv(c, B);
+    sync(c);
+  });
+}
+
+wmx_status wmx_encode(wmx_ctx* x, const float* mel, int B, float* enc_out) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(c.m->initialized, "encode: weights not initialised");
+    WMX_CHECK(B >= 1 && B <= c.maxB, "encode: batch");
+    WMX_HIP(hipSetDevice(c.m->device));
+    WMX_HIP(hipMemcpyAsync(c.mel, mel, (size_t)B * c.m->d.n_mels * 3000 * 4, hipMemcpyHostToDevice, c.st));
+    encode(c, B);
+    cross_kv(c, B);
+    if (enc_out) {
+      const long n = (long)B * 1500 * c.m->d.n_audio_state;
+      launch_cvt16_to_f32(c.dt, c.enc_out, c.ex, n, c.st);
+      WMX_HIP(hipMemcpyAsync(enc_out, c.ex, n * 4, hipMemcpyDeviceToHost, c.st));
+    }
+    sync(c);
+  });
+}
+
+wmx_status wmx_decoder_logits(wmx_ctx* x, const int32_t* tokens, const int32_t* lens, int B, int T, float* logits_out) {
+  return guard([&] {
+    Ctx& c = x->c;
+    Model& m = *c.m;
+    WMX_CHECK(B >= 1 && B <= c.maxB && T >= 1 && T <= c.Tctx, "decoder_logits: shape");
+    WMX_HIP(hipSetDevice(m.device));
+    const int K = c.K, Tc = c.Tctx, V = m.d.n_vocab;
+    std::vector<int> tok((size_t)B * K * Tc, 0);
+    for (int b = 0; b < B; ++b)
+      for (int i = 0; i < T; ++i) tok[(size_t)b * K * Tc + i] = tokens[(size_t)b * T + i];
+    WMX_HIP(hipMemcpyAsync(c.hist_tmp, tok.data(), tok.size() * 4, hipMemcpyHostToDevice, c.st));
+    set_slot(c, 0);
+    FwdArgs f;
+    f.rows = B;
+    f.Tn = T;
+    f.rmul = K;
+    f.tok = c.hist_tmp;
+    f.tok_ld = (long)K * Tc;
+    f.pad_seq = nullptr;
+    f.prefill = true;
+    f.anc = nullptr;
+    dec_forward(c, f);
+    const int rows_all = B * T;
+    for (int r0 = 0; r0 < rows_all; r0 += c.logits_rows) {
+      const int n = std::min(c.logits_rows, rows_all - r0);
+      std::vector<int> g(n);
+      for (int i = 0; i < n; ++i) g[i] = r0 + i;
+      WMX_HIP(hipMemcpyAsync(c.gather, g.data(), n * 4, hipMemcpyHostToDevice, c.st));
+      dec_logits(c, c.gather, n);
+      WMX_HIP(hipMemcpyAsync(logits_out + (size_t)r0 * V, c.logits, (size_t)n * V * 4, hipMemcpyDeviceToHost, c.st));
+      sync(c);
+    }
+    (void)lens;
+  });
+}
+
+wmx_status wmx_transcribe_device(wmx_ctx* x, const float* pcm_dev, int64_t stride, const int64_t* lens,
+                                 const int32_t* seek, int B, const int32_t* prompt_ids, const int32_t* prompt_lens,
+                                 wmx_result** out) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(out, "null out");
+    WMX_HIP(hipSetDevice(c.m->device));
+    std::vector<long> l(lens, lens + B);
+    ResultHolder* r = transcribe(c, pcm_dev, (long)stride, l.data(), seek, B, prompt_ids, prompt_lens);
+    *out = &r->r;
+  });
+}
+
+wmx_status wmx_transcribe(wmx_ctx* x, const float* pcm, int64_t stride, const int64_t* lens, const int32_t* seek, int B,
+                          const int32_t* prompt_ids, const int32_t* prompt_lens, wmx_result** out) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(out, "null out");
+    WMX_CHECK(B >= 1 && B <= c.maxB, "transcribe: batch");
+    WMX_CHECK(stride <= c.max_samples, "transcribe: stride exceeds max_audio_samples");
+    WMX_HIP(hipSetDevice(c.m->device));
+    WMX_HIP(hipMemcpyAsync(c.pcm, pcm, (size_t)B * stride * 4, hipMemcpyHostToDevice, c.st));
+    std::vector<long> l(lens, lens + B);
+    ResultHolder* r = transcribe(c, c.pcm, (long)stride, l.data(), seek, B, prompt_ids, prompt_lens);
+    *out = &r->r;
+  });
+}
+
+void wmx_result_free(wmx_result* r) {
+  if (!r) return;
+  // r is the first member of ResultHolder
+  delete reinterpret_cast<ResultHolder*>(r);
+}
+
+wmx_status wmx_ctx_stage_ms(wmx_ctx* x, float* out7) {
+  return guard([&] { std::memcpy(out7, x->c.stage_ms, sizeof(float) * 7); });
+}
+
+int wmx_ctx_last_steps(wmx_ctx* x) { return x->c.last_steps; }
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""ctypes binding of libwmx.so (include/wmx.h).  No torch types cross this boundary.
+
+The library is the product path: if it is missing this module raises on import — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("WMX_LIB", os.path.join(_HERE, "libwmx.so"))
+
+WMX_DTYPE_BF16, WMX_DTYPE_F16 = 0, 1
+WMX_TASK_TRANSCRIBE, WMX_TASK_TRANSLATE = 0, 1
+
+
+class Dims(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "n_mels", "n_vocab", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer",
+        "n_text_ctx", "n_text_state", "n_text_head", "n_text_layer")]
+
+
+class Opts(C.Structure):
+    _fields_ = [
+        ("max_batch", C.c_int32), ("beam_size", C.c_int32), ("patience", C.c_float),
+        ("length_penalty", C.c_float), ("max_new_tokens", C.c_int32), ("task", C.c_int32),
+        ("language", C.c_int32), ("without_timestamps", C.c_int32),
+        ("max_initial_timestamp_index", C.c_int32), ("suppress_blank", C.c_int32),
+        ("suppress_tokens", C.POINTER(C.c_int32)), ("n_suppress_tokens", C.c_int32),
+        ("word_timestamps", C.c_int32), ("alignment_heads", C.POINTER(C.c_int32)),
+        ("n_alignment_heads", C.c_int32), ("median_filter_width", C.c_int32),
+        ("use_graph", C.c_int32), ("max_audio_samples", C.c_int32),
+    ]
+
+
+class WindowResult(C.Structure):
+    _fields_ = [
+        ("language", C.c_int32), ("language_prob", C.c_float), ("n_tokens", C.c_int32),
+        ("tokens", C.POINTER(C.c_int32)), ("sum_logprob", C.c_float), ("avg_logprob", C.c_float),
+        ("no_speech_prob", C.c_float), ("seek_frames", C.c_int32), ("n_text_tokens", C.c_int32),
+        ("jump_times", C.POINTER(C.c_float)), ("text_token_probs", C.POINTER(C.c_float)),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [("n_windows", C.c_int32), ("windows", C.POINTER(WindowResult))]
+
+
+EXPORTS = [
+    "wmx_last_error", "wmx_version", "wmx_device_count", "wmx_model_create", "wmx_model_free",
+    "wmx_model_init_synthetic", "wmx_model_set_tensor", "wmx_model_get_tensor", "wmx_model_n_params",
+    "wmx_model_arena", "wmx_model_arena_loaded", "wmx_opts_default", "wmx_ctx_create", "wmx_ctx_destroy",
+    "wmx_ctx_stream", "wmx_logmel", "wmx_logmel_device", "wmx_encode", "wmx_encode_device",
+    "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device", "wmx_result_free",
+    "wmx_ctx_stage_ms", "wmx_ctx_last_steps",
+]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libwmx.so not found at {LIB_PATH}: build it with `make -C realtime-whisper-asr_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    P, I32, I64, F, VP = C.POINTER, C.c_int32, C.c_int64, C.c_float, C.c_void_p
+    sig = {
+        "wmx_last_error": (C.c_char_p, []),
+        "wmx_version": (C.c_char_p, []),
+        "wmx_device_count": (C.c_int, []),
+        "wmx_model_create": (C.c_int, [P(Dims), C.c_int, C.c_int, P(VP)]),
+        "wmx_model_free": (None, [VP]),
+        "wmx_model_init_synthetic": (C.c_int, [VP, C.c_uint64]),
+        "wmx_model_set_tensor": (C.c_int, [VP, C.c_char_p, P(F), I64]),
+        "wmx_model_get_tensor": (C.c_int, [VP, C.c_char_p, P(F), I64]),
+        "wmx_model_n_params": (I64, [VP]),
+        "wmx_model_arena": (C.c_int, [VP, P(VP), P(C.c_size_t)]),
+        "wmx_model_arena_loaded": (C.c_int, [VP]),
+        "wmx_opts_default": (None, [P(Opts)]),
+        "wmx_ctx_create": (C.c_int, [VP, P(Opts), P(VP)]),
+        "wmx_ctx_destroy": (None, [VP]),
+        "wmx_ctx_stream": (VP, [VP]),
+        "wmx_logmel": (C.c_int, [VP, P(F), I64, P(I64), P(I32), C.c_int, P(F)]),
+        "wmx_logmel_device": (C.c_int, [VP, VP, I64, P(I64), P(I32), C.c_int, VP]),
+        "wmx_encode": (C.c_int, [VP, P(F), C.c_int, P(F)]),
+        "wmx_encode_device": (C.c_int, [VP, VP, C.c_int]),
+        "wmx_decoder_logits": (C.c_int, [VP, P(I32), P(I32), C.c_int, C.c_int, P(F)]),
+        "wmx_transcribe": (C.c_int, [VP, P(F), I64, P(I64), P(I32), C.c_int, P(I32), P(I32), P(P(Result))]),
+        "wmx_transcribe_device": (C.c_int, [VP, VP, I64, P(I64), P(I32), C.c_int, P(I32), P(I32), P(P(Result))]),
+        "wmx_result_free": (None, [P(Result)]),
+        "wmx_ctx_stage_ms": (C.c_int, [VP, P(F)]),
+        "wmx_ctx_last_steps": (C.c_int, [VP]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class WmxError(RuntimeError):
+    pass
+
+
+def check(status: int):
+    if status != 0:
+        raise WmxError(f"libwmx error {status}: {lib.wmx_last_error().decode(errors='replace')}")
+
+
+def fptr(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def lptr(a: np.ndarray):
+    assert a.dtype == np.int64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
