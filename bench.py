@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X streaming-Whisper hot path (BASELINE.json metric: real-time factor + p50 chunk
+latency, Whisper large-v3 30 s @ 16 kHz, 1/2/4/8 GPUs).
+
+Workload (BASELINE.json configs[2]/[3]): Whisper large-v3 dims, bf16, synthetic weights (build-owned PRNG; no
+checkpoint is reachable offline), B concurrent synthetic 30 s mic streams per GPU; one step = one batched
+transcribe call over the B windows = log-mel -> encoder -> cross K/V -> language detection -> prompt prefill ->
+beam-5 decode (hipGraph per step) -> word alignment (alignment forward + DTW), inputs resident in HBM.
+Streams are independent (data parallel): stream s runs on rank s // B; the only collective is the RCCL broadcast
+of the weight arena from rank 0 at start-up ("scaling": "weak").
+
+value = audio seconds processed by all ranks / max-over-ranks wall time  (x real time = 1 / RTF).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "realtime-whisper-asr_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "real-time factor + p50 chunk latency, Whisper large-v3 30s@16kHz, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0
+MFMA_BF16_PEAK_TFLOPS = 2500.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--model", default="large-v3")
+    p.add_argument("--batch", type=int, default=8, help="concurrent 30 s streams per GPU")
+    p.add_argument("--beam", type=int, default=5)
+    p.add_argument("--max-new-tokens", type=int, default=224)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--roofline-kernel", default="auto",
+                   choices=["auto", "cross_attn", "enc_fc1", "enc_attn", "logmel", "dec_fc1", "self_attn"])
+    return p.parse_args()
+
+
+class _ArenaView:
+    """Zero-copy torch view of the library's weight arena (for the RCCL broadcast)."""
+
+    def __init__(self, ptr, nbytes):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+
+def cpu_baseline(model, args, steps_done):
+    """The oracle (numpy fp32 restatement, oracle/whisper_np.py) timed on this host on a bounded sample:
+    one 30 s window: log-mel + encoder + language detection + prompt prefill + 4 beam decode steps; the per-step
+    time is extrapolated to the same number of decode steps the GPU run executed."""
+    from oracle import whisper_np as O
+    from wmx import synth
+
+    d = O.DIMS[args.model] if args.model in O.DIMS else None
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    t0 = time.perf_counter()
+    W = {}
+    for name, shape, _, _ in O.tensor_specs(d):
+        W[name] = model.get_tensor(name, shape)
+    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
+    t_load = time.perf_counter() - t0
+    audio = synth.speech_like(10_000, 480000)
+    t = time.perf_counter()
+    mel = O.logmel_segment(audio, d.n_mels)
+    t_mel = time.perf_counter() - t
+    t = time.perf_counter()
+    enc = O.encoder(W, d, mel)
+    t_enc = time.perf_counter() - t
+    t = time.perf_counter()
+    lang, _ = O.detect_language(W, d, enc)
+    t_lang = time.perf_counter() - t
+    sp = O.special_tokens(d.n_vocab)
+    t = time.perf_counter()
+    cache = O.DecoderCache(W, d, enc)
+    O.decoder_forward(W, d, O.sot_sequence(sp, lang, "transcribe"), cache)
+    t_pre = time.perf_counter() - t
+    caches = [cache.copy() for _ in range(args.beam)]
+    n_dec = 4
+    t = time.perf_counter()
+    for s in range(n_dec):
+        for c in caches:
+            O.decoder_forward(W, d, [sp.timestamp_begin + s], c)
+    t_step = (time.perf_counter() - t) / n_dec
+    total = t_mel + t_enc + t_lang + t_pre + t_step * max(steps_done, 1)
+    log(f"[cpu] load {t_load:.1f}s mel {t_mel:.3f}s enc {t_enc:.2f}s lang {t_lang:.2f}s prefill {t_pre:.2f}s "
+        f"step {t_step:.3f}s x {steps_done} -> {total:.1f}s per 30 s window")
+    return {"value": round(30.0 / total, 4), "unit": "x_realtime", "cores": cores, "kind": "port",
+            "sample": f"1 x 30 s window of {args.model} (numpy fp32 oracle): log-mel + encoder + language detect + "
+                      f"prefill + {n_dec} beam-{args.beam} decode steps timed, per-step time extrapolated to "
+                      f"{steps_done} steps; word alignment not included"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    # torch (plumbing only: RCCL + the resident input buffer) must bring up its HIP runtime before libwmx is
+    # loaded, so the process holds ONE libamdhip64.so.7 and device pointers are shared.
+    import torch
+    torch.cuda.set_device(local)
+    torch.zeros(1, device=f"cuda:{local}")
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from wmx import engine, synth
+
+    dt = {"bf16": "bfloat16", "f16": "float16"}[args.dtype]
+    model = engine.Model(args.model, local, dt)
+    t = time.time()
+    if world > 1:
+        if rank == 0:
+            model.init_synthetic(args.seed)
+        ptr, nbytes = model.arena()
+        view = torch.as_tensor(_ArenaView(ptr, nbytes), device=f"cuda:{local}")
+        torch.cuda.synchronize()
+        dist.broadcast(view, src=0)  # RCCL over xGMI: the only collective of the job
+        torch.cuda.synchronize()
+        model.mark_loaded()
+    else:
+        model.init_synthetic(args.seed)
+    log(f"[rank {rank}] weights ready in {time.time() - t:.2f}s ({model.n_params() / 1e9:.2f} B params)")
+
+    B = args.batch
+    heads = engine.ALIGNMENT_HEADS.get(args.model)
+    ctx = engine.Context(model, max_batch=B, beam_size=args.beam, max_new_tokens=args.max_new_tokens,
+                         language=None, word_timestamps=True, alignment_heads=heads, use_graph=not args.no_graph)
+    # synthetic 30 s streams, resident in HBM before the timed region
+    audio = np.stack([synth.speech_like(rank * B + i, 480000) for i in range(B)])
+    pcm = torch.from_numpy(audio).to(f"cuda:{local}")
+    lens = np.full(B, 480000, np.int64)
+    torch.cuda.synchronize()
+
+    def step():
+        return ctx.transcribe_device(pcm.data_ptr(), 480000, lens)
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    lat = []
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        res = step()
+        lat.append(time.perf_counter() - ts)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    stages = ctx.stage_ms()
+    steps_done = ctx.last_steps()
+    n_tok = [len(r.tokens) for r in res]
+    log(f"[rank {rank}] stage ms (logmel, enc, xkv, lang, prefill, decode, align): "
+        f"{[round(s, 2) for s in stages]}  decode steps {steps_done}  tokens/window {n_tok}")
+
+    audio_s = 30.0 * B * world * args.steps
+    value = audio_s / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+    p50 = 1000.0 * float(np.median(lat))
+
+    # roofline of the dominant kernel, measured live with HIP events on the context stream
+    per_step_ms = {}
+    kern_stats = {}
+    R = B * args.beam
+    counts = {  # launches per transcribe step
+        "cross_attn": steps_done * model.dims.n_text_layer,
+        "self_attn": steps_done * model.dims.n_text_layer,
+        "dec_fc1": steps_done * model.dims.n_text_layer,
+        "enc_fc1": model.dims.n_audio_layer,
+        "enc_attn": model.dims.n_audio_layer,
+        "logmel": 1,
+    }
+    for k in counts:
+        log(f"[rank {rank}] timing kernel {k}")
+        ms, by, fl = ctx.bench_kernel(k, B, iters=20)
+        kern_stats[k] = (ms, by, fl)
+        per_step_ms[k] = ms * counts[k]
+    dom = max(per_step_ms, key=per_step_ms.get) if args.roofline_kernel == "auto" else args.roofline_kernel
+    ms, by, fl = kern_stats[dom]
+    if dom in ("enc_fc1", "enc_attn"):
+        ach = fl / (ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None}
+    else:
+        ach = by / (ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    roof["kernel"] = dom
+    roof["launch_ms"] = round(ms, 4)
+    roof["algorithmic_per_launch"] = {"bytes": by, "flops": fl}
+    log(f"[rank {rank}] kernel ms/launch: " + ", ".join(f"{k}={v[0]:.4f}" for k, v in kern_stats.items()))
+    log(f"[rank {rank}] est. ms per transcribe step: " + ", ".join(f"{k}={v:.1f}" for k, v in per_step_ms.items()))
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "x_realtime (audio s / wall s, all GPUs)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "p50_chunk_latency_ms": round(p50, 2),
+        "rtf": round(1.0 / value * world, 6),
+        "chunks_per_s": round(B * world * args.steps / elapsed, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded speech-like 30 s audio; build-owned PRNG weights of the named architecture)",
+        "config": {"workload": f"whisper-{args.model} transcribe, {B} x 30 s windows per GPU, beam {args.beam}, "
+                               f"word_timestamps, language auto-detect, max_new_tokens {args.max_new_tokens}",
+                   "model": f"whisper-{args.model}", "global_batch": B * world, "seq_len": 480000,
+                   "parallelism": f"dp{world} (independent streams)", "decode_steps": steps_done,
+                   "use_graph": not args.no_graph},
+        "stage_ms": [round(s, 2) for s in stages],
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(model, args, steps_done)
+        except Exception as e:  # the baseline is reported, never the target
+            log(f"[cpu] baseline failed: {e!r}")
+            out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

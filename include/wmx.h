@@ -164,6 +164,14 @@ wmx_status wmx_ctx_stage_ms(wmx_ctx* c, float* out7);
 /* total decode steps executed by the last wmx_transcribe */
 int wmx_ctx_last_steps(wmx_ctx* c);
 
+/* roofline hook: replay ONE kernel of the hot path `iters` times on the context stream (geometry and data of
+ * the last wmx_transcribe, B windows) between two HIP events; returns the average launch duration and the
+ * ALGORITHMIC bytes / flops of one launch.  kernel: 0 decoder cross-attention (one layer, decode step),
+ * 1 encoder fc1 GEMM, 2 encoder self-attention (one layer), 3 log-mel (raw pass), 4 decoder fc1 GEMM (step),
+ * 5 decoder self-attention (one layer, at the last decoded length). */
+wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float* avg_ms, double* bytes,
+                                double* flops);
+
 #ifdef __cplusplus
 }
 #endif

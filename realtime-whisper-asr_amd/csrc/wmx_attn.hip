@@ -189,15 +189,17 @@ void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) { launch_attn
 // decoder self attention (decode step or small Tn), keys through the ancestry table
 // ------------------------------------------------------------------------------------------------
 template <DT T>
-__global__ __launch_bounds__(64) void dec_self_attn_kernel(DecAttnArgs a) {
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = blockIdx.x;
   const int m = blockIdx.y;  // r * Tn + i
   __shared__ float s[512];
+  __shared__ float red[4];
+  __shared__ float fin[4][64];
   const int r = m / a.Tn, i = m - r * a.Tn;
   const int slot_q = *a.slot0 + i;
   const int beg = a.pad ? a.pad[r] : 0;
-  const int gi = lane >> 3, j = lane & 7;
+  const int gi = lane >> 3, j = lane & 7;  // 8 key groups x 8 dim chunks per wave
   float q[8];
   {
     const u16x8 qv = *reinterpret_cast<const u16x8*>(a.q + (long)m * a.q_ld + h * 64 + j * 8);
@@ -205,44 +207,60 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(DecAttnArgs a) {
     for (int e = 0; e < 8; ++e) q[e] = to_f32<T>(qv[e]) * 0.125f;
   }
   const int* anc = a.anc ? a.anc + (long)r * a.anc_ld : nullptr;
+  constexpr int U = 4;  // per wave per iteration: 32 keys, 4 independent 16-B loads per lane
   float mx = -INFINITY;
-  for (int s0 = beg; s0 <= slot_q; s0 += 8) {
-    const int key = s0 + gi;
-    float part = 0.f;
-    if (key <= slot_q) {
-      const int row = anc ? anc[key] : r;
-      const u16x8 kv = *reinterpret_cast<const u16x8*>(a.kc + ((long)key * a.R + row) * a.d + h * 64 + j * 8);
+  for (int s0 = beg + wave * 8 * U; s0 <= slot_q; s0 += 4 * 8 * U) {
+    u16x8 kv[U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) part += q[e] * to_f32<T>(kv[e]);
+    for (int u = 0; u < U; ++u) {
+      const int key = min(s0 + 8 * u + gi, slot_q);
+      const int row = anc ? anc[key] : r;
+      kv[u] = *reinterpret_cast<const u16x8*>(a.kc + ((long)key * a.R + row) * a.d + h * 64 + j * 8);
     }
-    part += __shfl_xor(part, 1);
-    part += __shfl_xor(part, 2);
-    part += __shfl_xor(part, 4);
-    if (key <= slot_q) {
-      if (j == 0) s[key - beg] = part;
-      mx = fmaxf(mx, part);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int key = s0 + 8 * u + gi;
+      float part = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part += q[e] * to_f32<T>(kv[u][e]);
+      part += __shfl_xor(part, 1);
+      part += __shfl_xor(part, 2);
+      part += __shfl_xor(part, 4);
+      if (key <= slot_q) {
+        if (j == 0) s[key - beg] = part;
+        mx = fmaxf(mx, part);
+      }
     }
   }
   mx = wave_max(mx);
+  if (lane == 0) red[wave] = mx;
   __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   const int n = slot_q - beg + 1;
   float sum = 0.f;
-  for (int t = lane; t < n; t += 64) {
+  for (int t = tid; t < n; t += 256) {
     const float e = __expf(s[t] - mx);
     s[t] = e;
     sum += e;
   }
   sum = wave_sum(sum);
   __syncthreads();
+  if (lane == 0) red[wave] = sum;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int s0 = beg; s0 <= slot_q; s0 += 8) {
-    const int key = s0 + gi;
-    if (key <= slot_q) {
-      const int row = anc ? anc[key] : r;
-      const float p = s[key - beg];
-      const u16x8 vv = *reinterpret_cast<const u16x8*>(a.vc + ((long)key * a.R + row) * a.d + h * 64 + j * 8);
+  for (int s0 = beg + wave * 8 * U; s0 <= slot_q; s0 += 4 * 8 * U) {
+    u16x8 vv[U];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p * to_f32<T>(vv[e]);
+    for (int u = 0; u < U; ++u) {
+      const int key = min(s0 + 8 * u + gi, slot_q);
+      const int row = anc ? anc[key] : r;
+      vv[u] = *reinterpret_cast<const u16x8*>(a.vc + ((long)key * a.R + row) * a.d + h * 64 + j * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int key = s0 + 8 * u + gi;
+      const float p = key <= slot_q ? s[key - beg] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += p * to_f32<T>(vv[u][e]);
     }
   }
 #pragma unroll
@@ -252,20 +270,23 @@ __global__ __launch_bounds__(64) void dec_self_attn_kernel(DecAttnArgs a) {
     acc[e] += __shfl_xor(acc[e], 32);
   }
   if (gi == 0) {
-    const float inv = 1.0f / sum;
-    u16x8 ov;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) ov[e] = from_f32<T>(acc[e] * inv);
-    *reinterpret_cast<u16x8*>(a.o + (long)m * a.d + h * 64 + j * 8) = ov;
+    for (int e = 0; e < 8; ++e) fin[wave][j * 8 + e] = acc[e];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const float tot = red[0] + red[1] + red[2] + red[3];
+    const float o = (fin[0][tid] + fin[1][tid] + fin[2][tid] + fin[3][tid]) / tot;
+    a.o[(long)m * a.d + h * 64 + tid] = from_f32<T>(o);
   }
 }
 
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
   dim3 grid(a.H, a.R * a.Tn);
   if (dt == DT::BF16)
-    hipLaunchKernelGGL(dec_self_attn_kernel<DT::BF16>, grid, dim3(64), 0, st, a);
+    hipLaunchKernelGGL(dec_self_attn_kernel<DT::BF16>, grid, dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(dec_self_attn_kernel<DT::F16>, grid, dim3(64), 0, st, a);
+    hipLaunchKernelGGL(dec_self_attn_kernel<DT::F16>, grid, dim3(256), 0, st, a);
   WMX_HIP(hipGetLastError());
 }
 
@@ -273,129 +294,209 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 // decoder cross attention for a decode step: one workgroup per (window, head); nq = rows_per_win*Tn <= 8
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxQ = 8, kMaxTk = 1536;
+constexpr int kChunk = 384, kVPre = kChunk / 32;  // keys per workgroup, V rows prefetched per thread
 
+// Q.K^T on MFMA: A = Q (16 query rows, nq valid) from registers, B = K^T straight from HBM (lane: key l&15,
+// 16 B of head dims) — the dominant stream is read exactly once with 16-B loads, 8 key blocks in flight per
+// wave.  Softmax in LDS, P.V on VALU (thread = 8 keys-apart group x 8 dims, 16-B V loads).  KS key splits per
+// (window, head) keep all CUs streaming at small batch; partial (m, l, o) are merged by dec_cross_combine.
 template <DT T>
-__global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a) {
-  const int h = blockIdx.x, w = blockIdx.y;
+__global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int KS, float* __restrict__ part,
+                                                             int* __restrict__ cnt) {
+  const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nq = a.rows_per_win * a.Tn;
-  const int m0 = w * nq;  // rows of window w are contiguous: m = r*Tn + i, r in [w*rpw, (w+1)*rpw)
-  __shared__ float sc[kMaxQ][kMaxTk];
+  const int m0 = w * nq;
+  const int chunk = ((a.Tk + KS - 1) / KS + 15) / 16 * 16;  // <= kChunk
+  const int k0 = ks * chunk, k1 = min(a.Tk, k0 + chunk);
+  const int nk = max(0, k1 - k0);
+  __shared__ float sc[kMaxQ][kChunk + 4];
   __shared__ float red[kMaxQ][4];
   __shared__ float fin[4][kMaxQ][64];
-  // thread = (key group kg = tid >> 3 (32 groups), dh chunk c = tid & 7 (8 dims))
-  const int kg = tid >> 3, c = tid & 7;
-  float q[kMaxQ][8];
-#pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi) {
-    const int mq = m0 + min(qi, nq - 1);
-    const u16x8 qv = *reinterpret_cast<const u16x8*>(a.q + (long)mq * a.q_ld + h * 64 + c * 8);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[qi][e] = to_f32<T>(qv[e]) * 0.125f;
-  }
   const uint16_t* kbase = a.ck + (long)w * a.Tk * a.ck_ld + h * 64;
   const uint16_t* vbase = kbase + a.d;
+  // P.V mapping: thread = (key group kg = tid >> 3 of 32, dims c*8 .. c*8+7); prefetch all its V rows now
+  const int kg = tid >> 3, c = tid & 7;
+  u16x8 vpre[kVPre];
+#pragma unroll
+  for (int i = 0; i < kVPre; ++i) {
+    const int t = min(kg + 32 * i, nk - 1);
+    vpre[i] = *reinterpret_cast<const u16x8*>(vbase + (long)(k0 + max(t, 0)) * a.ck_ld + c * 8);
+  }
+  // Q fragments: lane row q = lane & 15, dims 32s + 8(lane>>4) .. +8
+  const int fr = lane & 15, g = lane >> 4;
+  u16x8 qa[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    u16x8 z = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (fr < nq) z = *reinterpret_cast<const u16x8*>(a.q + (long)(m0 + fr) * a.q_ld + h * 64 + 32 * s2 + 8 * g);
+    qa[s2] = z;
+  }
+  // ---- scores: wave handles key blocks wave, wave+4, ... (<= 6 per wave), all loads issued first ----
+  const int nblk = (nk + 15) / 16;
+  constexpr int NB = kChunk / 16 / 4;  // 6
+  u16x8 kb[NB][2];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int key = min(k0 + (wave + 4 * u) * 16 + fr, a.Tk - 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) kb[u][s2] = *reinterpret_cast<const u16x8*>(kbase + (long)key * a.ck_ld + 32 * s2 + 8 * g);
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int blk = wave + 4 * u;
+    if (blk >= nblk) break;
+    f32x4 acc = f32x4{0, 0, 0, 0};
+    acc = mfma16<T>(qa[0], kb[u][0], acc);
+    acc = mfma16<T>(qa[1], kb[u][1], acc);
+    const int kl = blk * 16 + fr;  // lane holds S[q = 4g + r][key kl]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = 4 * g + r;
+      if (q < nq && kl < nk) sc[q][kl] = acc[r] * 0.125f;
+    }
+  }
+  __syncthreads();
+  // ---- softmax (partial over this key range) ----
   float mx[kMaxQ];
 #pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi) mx[qi] = -INFINITY;
-  for (int s = kg; s < a.Tk; s += 32) {
-    const u16x8 kv = *reinterpret_cast<const u16x8*>(kbase + (long)s * a.ck_ld + c * 8);
-    float kf[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) kf[e] = to_f32<T>(kv[e]);
-#pragma unroll
-    for (int qi = 0; qi < kMaxQ; ++qi) {
-      float p = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) p += q[qi][e] * kf[e];
-      p += __shfl_xor(p, 1);
-      p += __shfl_xor(p, 2);
-      p += __shfl_xor(p, 4);
-      mx[qi] = fmaxf(mx[qi], p);
-      if (c == 0 && qi < nq) sc[qi][s] = p;
-    }
-  }
-#pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi) {
-    const float v = wave_max(mx[qi]);
-    if (lane == 0) red[qi][wave] = v;
+  for (int q = 0; q < kMaxQ; ++q) {
+    float v = -INFINITY;
+    if (q < nq)
+      for (int t = tid; t < nk; t += 256) v = fmaxf(v, sc[q][t]);
+    v = wave_max(v);
+    if (lane == 0) red[q][wave] = v;
   }
   __syncthreads();
 #pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi) mx[qi] = fmaxf(fmaxf(red[qi][0], red[qi][1]), fmaxf(red[qi][2], red[qi][3]));
+  for (int q = 0; q < kMaxQ; ++q) mx[q] = fmaxf(fmaxf(red[q][0], red[q][1]), fmaxf(red[q][2], red[q][3]));
   __syncthreads();
-  float sum[kMaxQ];
 #pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi) sum[qi] = 0.f;
-  for (int s = tid; s < a.Tk; s += 256) {
-#pragma unroll
-    for (int qi = 0; qi < kMaxQ; ++qi) {
-      if (qi < nq) {
-        const float e = __expf(sc[qi][s] - mx[qi]);
-        sc[qi][s] = e;
-        sum[qi] += e;
+  for (int q = 0; q < kMaxQ; ++q) {
+    float sum = 0.f;
+    if (q < nq)
+      for (int t = tid; t < nk; t += 256) {
+        const float e = __expf(sc[q][t] - mx[q]);
+        sc[q][t] = e;
+        sum += e;
       }
-    }
-  }
-#pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi) {
-    const float v = wave_sum(sum[qi]);
-    if (lane == 0) red[qi][wave] = v;
+    sum = wave_sum(sum);
+    if (lane == 0) red[q][wave] = sum;
   }
   __syncthreads();
+  // ---- P.V from the prefetched V rows ----
   float acc[kMaxQ][8];
 #pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi)
+  for (int q = 0; q < kMaxQ; ++q)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[qi][e] = 0.f;
-  for (int s = kg; s < a.Tk; s += 32) {
-    const u16x8 vv = *reinterpret_cast<const u16x8*>(vbase + (long)s * a.ck_ld + c * 8);
-    float vf[8];
+    for (int e = 0; e < 8; ++e) acc[q][e] = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) vf[e] = to_f32<T>(vv[e]);
+  for (int i = 0; i < kVPre; ++i) {
+    const int t = kg + 32 * i;
+    if (t < nk) {
+      float vf[8];
 #pragma unroll
-    for (int qi = 0; qi < kMaxQ; ++qi) {
-      if (qi < nq) {
-        const float p = sc[qi][s];
+      for (int e = 0; e < 8; ++e) vf[e] = to_f32<T>(vpre[i][e]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[qi][e] += p * vf[e];
+      for (int q = 0; q < kMaxQ; ++q) {
+        if (q < nq) {
+          const float p = sc[q][t];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[q][e] += p * vf[e];
+        }
       }
     }
   }
-  // reduce over the 8 key groups of a wave (lanes with equal c: xor 8, 16, 32), then over the 4 waves
 #pragma unroll
-  for (int qi = 0; qi < kMaxQ; ++qi)
+  for (int q = 0; q < kMaxQ; ++q) {
+    if (q < nq) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float v = acc[qi][e];
-      v += __shfl_xor(v, 8);
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      acc[qi][e] = v;
+      for (int e = 0; e < 8; ++e) {
+        float v = acc[q][e];
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        acc[q][e] = v;
+      }
     }
+  }
   if (lane < 8) {
 #pragma unroll
-    for (int qi = 0; qi < kMaxQ; ++qi)
+    for (int q = 0; q < kMaxQ; ++q)
+      if (q < nq)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) fin[wave][qi][c * 8 + e] = acc[qi][e];
+        for (int e = 0; e < 8; ++e) fin[wave][q][c * 8 + e] = acc[q][e];
   }
   __syncthreads();
   for (int t = tid; t < nq * 64; t += 256) {
-    const int qi = t >> 6, e = t & 63;
-    const float tot = red[qi][0] + red[qi][1] + red[qi][2] + red[qi][3];
-    const float v = (fin[0][qi][e] + fin[1][qi][e] + fin[2][qi][e] + fin[3][qi][e]) / tot;
-    a.o[(long)(m0 + qi) * a.d + h * 64 + e] = from_f32<T>(v);
+    const int q = t >> 6, e = t & 63;
+    const float tot = red[q][0] + red[q][1] + red[q][2] + red[q][3];
+    const float o = fin[0][q][e] + fin[1][q][e] + fin[2][q][e] + fin[3][q][e];
+    if (KS == 1) {
+      a.o[(long)(m0 + q) * a.d + h * 64 + e] = from_f32<T>(o / tot);
+    } else {
+      // partial record per (window, head, split, q): [m, l, o[64]]
+      float* pr = part + ((((long)w * a.H + h) * KS + ks) * kMaxQ + q) * 66;
+      if (e == 0) {
+        pr[0] = mx[q];
+        pr[1] = tot;
+      }
+      pr[2 + e] = o;
+    }
   }
+  if (KS == 1) return;
+  // ---- the last of the KS workgroups of (window, head) merges the partials (cdna_hip_programming.md
+  //      Guideline 16: drained plain stores -> agent release -> counter; last arriver: agent acquire -> loads) ----
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(cnt + w * a.H + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == KS - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int t = tid; t < nq * 64; t += 256) {
+    const int q = t >> 6, e = t & 63;
+    const float* pr = part + (((long)w * a.H + h) * KS * kMaxQ + q) * 66;
+    float M = -INFINITY;
+    for (int k = 0; k < KS; ++k) M = fmaxf(M, pr[(long)k * kMaxQ * 66]);
+    float l = 0.f, o = 0.f;
+    for (int k = 0; k < KS; ++k) {
+      const float* x = pr + (long)k * kMaxQ * 66;
+      const float sc2 = __expf(x[0] - M);
+      l += x[1] * sc2;
+      o += x[2 + e] * sc2;
+    }
+    a.o[(long)(m0 + q) * a.d + h * 64 + e] = from_f32<T>(o / l);
+  }
+  if (tid == 0) __hip_atomic_store(cnt + w * a.H + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-void launch_cross_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
+int cross_attn_splits(int Tk) { return (Tk + kChunk - 1) / kChunk; }
+
+// partial records + one arrival counter per (window, head) (the counters must start at 0; the last arriver resets)
+size_t cross_attn_ws_floats(int H, int nwin) { return (size_t)nwin * H * 8 * kMaxQ * 66 + (size_t)nwin * H; }
+
+void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {
   const int nq = a.rows_per_win * a.Tn;
   WMX_CHECK(nq <= kMaxQ && a.Tk <= kMaxTk, "cross attn: too many queries per window");
-  dim3 grid(a.H, a.R / a.rows_per_win);
+  const int nwin = a.R / a.rows_per_win;
+  const int KS = cross_attn_splits(a.Tk);
+  WMX_CHECK(KS == 1 || ws != nullptr, "cross attn: split workspace required");
+  dim3 grid(a.H, nwin, KS);
+  int* cnt = ws ? reinterpret_cast<int*>(ws + (size_t)nwin * a.H * 8 * kMaxQ * 66) : nullptr;
   if (dt == DT::BF16)
-    hipLaunchKernelGGL(dec_cross_attn_kernel<DT::BF16>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(dec_cross_attn_kernel<DT::BF16>, grid, dim3(256), 0, st, a, KS, ws, cnt);
   else
-    hipLaunchKernelGGL(dec_cross_attn_kernel<DT::F16>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(dec_cross_attn_kernel<DT::F16>, grid, dim3(256), 0, st, a, KS, ws, cnt);
   WMX_HIP(hipGetLastError());
 }
 

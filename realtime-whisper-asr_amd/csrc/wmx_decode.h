@@ -34,8 +34,10 @@ struct BeamState {  // device arrays
   float* new_score;
 };
 
+// rules + log-softmax + top-KP per row, two phases over kSlices vocab slices; ws: logits_select_ws_floats(R, KP)
+size_t logits_select_ws_floats(int R, int KP);
 void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const RowPtrs& rp, int R, int KP, int* tok,
-                          float* lp, const int* row_map, hipStream_t st);
+                          float* lp, const int* row_map, float* ws, hipStream_t st);
 void launch_greedy_update(const RowPtrs& rp, const int* tok, const float* lp, int R, int tb, int eot, int* hist,
                           int hist_ld, int* slot, int* n_done, hipStream_t st);
 void launch_beam_step(const RowPtrs& rp, const RowPtrs& tmp, const int* ctok, const float* clp, int nwin, int K,

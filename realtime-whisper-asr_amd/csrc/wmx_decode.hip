@@ -73,95 +73,53 @@ constexpr int kMaxKP = 9;
 // better(a, b): value desc, index asc
 __device__ inline bool better(float va, int ia, float vb, int ib) { return va > vb || (va == vb && ia < ib); }
 
-__global__ __launch_bounds__(kSelThreads) void logits_select_kernel(const float* __restrict__ logits, int ldl, RuleOpts o,
-                                                                    RowState rs, int KP, int* __restrict__ out_tok,
-                                                                    float* __restrict__ out_lp, const int* row_map) {
-  const int r = blockIdx.x;
-  const int lrow = row_map ? row_map[r] : r;  // logits row
-  const float* x = logits + (long)lrow * ldl;
-  const int ns = rs.ns[r], lt = rs.last[r], pt = rs.pen[r], lts = rs.last_ts[r];
-  const bool last_ts = ns >= 1 && lt >= o.tb;
-  const bool pen_ts = ns < 2 || pt >= o.tb;
-  const int tid = threadIdx.x;
-  MS text{-INFINITY, 0.f}, ts{-INFINITY, 0.f};
-  float tmax = -INFINITY;
-  for (int t = tid; t < o.V; t += kSelThreads) {
-    if (!allowed(o, t, ns, last_ts, pen_ts, lts)) continue;
-    const float v = x[t];
-    if (t < o.tb) {
-      text = ms_add(text, v);
-      tmax = fmaxf(tmax, v);
-    } else {
-      ts = ms_add(ts, v);
-    }
-  }
-  __shared__ float sm[3][kSelThreads / 64];
-  __shared__ float ss[2][kSelThreads / 64];
-  // wave reduce
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    MS a{__shfl_xor(text.m, off), __shfl_xor(text.s, off)};
-    MS b{__shfl_xor(ts.m, off), __shfl_xor(ts.s, off)};
-    text = ms_merge(text, a);
-    ts = ms_merge(ts, b);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, off));
-  }
-  const int wave = tid >> 6, lane = tid & 63;
-  if (lane == 0) {
-    sm[0][wave] = text.m;
-    ss[0][wave] = text.s;
-    sm[1][wave] = ts.m;
-    ss[1][wave] = ts.s;
-    sm[2][wave] = tmax;
-  }
-  __syncthreads();
-  MS T{-INFINITY, 0.f}, S{-INFINITY, 0.f};
-  tmax = -INFINITY;
-  for (int w = 0; w < kSelThreads / 64; ++w) {
-    T = ms_merge(T, MS{sm[0][w], ss[0][w]});
-    S = ms_merge(S, MS{sm[1][w], ss[1][w]});
-    tmax = fmaxf(tmax, sm[2][w]);
-  }
-  const float lse_ts = ms_lse(S);
-  const bool mask_text = !o.without_ts && (lse_ts > tmax);
-  const float lse_text = ms_lse(T);
-  float lse_all;
-  if (mask_text) {
-    lse_all = lse_ts;
-  } else {
-    const float m = fmaxf(lse_text, lse_ts);
-    lse_all = m == -INFINITY ? -INFINITY : m + __logf(__expf(lse_text - m) + __expf(lse_ts - m));
-  }
-  // thread-local top-KP (sorted, best first)
-  float tv[kMaxKP];
-  int ti[kMaxKP];
+// ---- phase A: one block per (row, vocab slice): masked statistics + top-KP of allowed text and timestamp
+//      tokens, kept separately because whether text is masked depends on the whole row ----
+constexpr int kSlices = 8, kSelA = 256;
+
+struct TopK {
+  float v[kMaxKP];
+  int i[kMaxKP];
+};
+
+__device__ inline void topk_init(TopK& t) {
 #pragma unroll
   for (int k = 0; k < kMaxKP; ++k) {
-    tv[k] = -INFINITY;
-    ti[k] = 0x7FFFFFFF;
+    t.v[k] = -INFINITY;
+    t.i[k] = 0x7FFFFFFF;
   }
-  for (int t = tid; t < o.V; t += kSelThreads) {
-    if (mask_text && t < o.tb) continue;
-    if (!allowed(o, t, ns, last_ts, pen_ts, lts)) continue;
-    const float v = x[t];
-    if (!better(v, t, tv[KP - 1], ti[KP - 1])) continue;
-    // insert (KP small)
-    int k = KP - 1;
-    while (k > 0 && better(v, t, tv[k - 1], ti[k - 1])) {
-      tv[k] = tv[k - 1];
-      ti[k] = ti[k - 1];
-      --k;
+}
+// sorted insert with compile-time indices only (runtime-indexed register arrays would spill to scratch)
+__device__ inline void topk_push(TopK& t, float v, int i, int KP) {
+#pragma unroll
+  for (int k = 0; k < kMaxKP; ++k) {
+    if (k < KP && better(v, i, t.v[k], t.i[k])) {
+      const float tv = t.v[k];
+      const int ti = t.i[k];
+      t.v[k] = v;
+      t.i[k] = i;
+      v = tv;
+      i = ti;
     }
-    tv[k] = v;
-    ti[k] = t;
   }
-  // KP rounds of block argmax over the list heads
-  __shared__ float rv[kSelThreads / 64];
-  __shared__ int ri[kSelThreads / 64];
-  int head = 0;
+}
+__device__ inline void topk_pop(TopK& t) {
+#pragma unroll
+  for (int k = 0; k + 1 < kMaxKP; ++k) {
+    t.v[k] = t.v[k + 1];
+    t.i[k] = t.i[k + 1];
+  }
+  t.v[kMaxKP - 1] = -INFINITY;
+  t.i[kMaxKP - 1] = 0x7FFFFFFF;
+}
+
+// block-wide: extract the KP best heads of all threads' lists into out (rank order)
+template <int NT>
+__device__ inline void block_topk(TopK& t, int KP, float* ov, int* oi, float* rv, int* ri) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int k = 0; k < KP; ++k) {
-    float v = head < KP ? tv[head] : -INFINITY;
-    int i = head < KP ? ti[head] : 0x7FFFFFFF;
+    float v = t.v[0];
+    int i = t.i[0];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const float v2 = __shfl_xor(v, off);
@@ -178,17 +136,146 @@ __global__ __launch_bounds__(kSelThreads) void logits_select_kernel(const float*
     __syncthreads();
     float bv = rv[0];
     int bi = ri[0];
-    for (int w = 1; w < kSelThreads / 64; ++w)
+    for (int w = 1; w < NT / 64; ++w)
       if (better(rv[w], ri[w], bv, bi)) {
         bv = rv[w];
         bi = ri[w];
       }
     __syncthreads();
-    if (head < KP && ti[head] == bi && bi != 0x7FFFFFFF) ++head;  // winner pops (indices are unique)
+    if (t.i[0] == bi && bi != 0x7FFFFFFF) topk_pop(t);
     if (tid == 0) {
-      out_tok[r * KP + k] = bi == 0x7FFFFFFF ? o.eot : bi;
-      out_lp[r * KP + k] = bv == -INFINITY ? -INFINITY : bv - lse_all;
+      ov[k] = bv;
+      oi[k] = bi;
     }
+  }
+}
+
+// workspace per (row, slice): [0..4] stats (text.m, text.s, ts.m, ts.s, text max), then KP text (v,i), KP ts (v,i)
+__device__ inline int sel_ws_stride(int KP) { return 5 + 4 * KP; }
+
+__global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict__ logits, int ldl, RuleOpts o,
+                                                         RowState rs, int KP, const int* row_map, float* __restrict__ ws) {
+  const int r = blockIdx.x, sl = blockIdx.y;
+  const int lrow = row_map ? row_map[r] : r;
+  const float* x = logits + (long)lrow * ldl;
+  const int ns = rs.ns[r], lt = rs.last[r], pt = rs.pen[r], lts = rs.last_ts[r];
+  const bool last_ts = ns >= 1 && lt >= o.tb;
+  const bool pen_ts = ns < 2 || pt >= o.tb;
+  const int per = (o.V + kSlices - 1) / kSlices;
+  const int t0 = sl * per, t1 = min(o.V, t0 + per);
+  const int tid = threadIdx.x;
+  MS text{-INFINITY, 0.f}, ts{-INFINITY, 0.f};
+  float tmax = -INFINITY;
+  TopK ktx, kts;
+  topk_init(ktx);
+  topk_init(kts);
+  for (int t = t0 + tid; t < t1; t += kSelA) {
+    if (!allowed(o, t, ns, last_ts, pen_ts, lts)) continue;
+    const float v = x[t];
+    if (t < o.tb) {
+      text = ms_add(text, v);
+      tmax = fmaxf(tmax, v);
+      topk_push(ktx, v, t, KP);
+    } else {
+      ts = ms_add(ts, v);
+      topk_push(kts, v, t, KP);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    text = ms_merge(text, MS{__shfl_xor(text.m, off), __shfl_xor(text.s, off)});
+    ts = ms_merge(ts, MS{__shfl_xor(ts.m, off), __shfl_xor(ts.s, off)});
+    tmax = fmaxf(tmax, __shfl_xor(tmax, off));
+  }
+  __shared__ float sm[5][kSelA / 64];
+  __shared__ float rv[kSelA / 64];
+  __shared__ int ri[kSelA / 64];
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane == 0) {
+    sm[0][wave] = text.m;
+    sm[1][wave] = text.s;
+    sm[2][wave] = ts.m;
+    sm[3][wave] = ts.s;
+    sm[4][wave] = tmax;
+  }
+  __syncthreads();
+  float* w = ws + ((long)r * kSlices + sl) * sel_ws_stride(KP);
+  if (tid == 0) {
+    MS T{-INFINITY, 0.f}, S{-INFINITY, 0.f};
+    float mx = -INFINITY;
+    for (int q = 0; q < kSelA / 64; ++q) {
+      T = ms_merge(T, MS{sm[0][q], sm[1][q]});
+      S = ms_merge(S, MS{sm[2][q], sm[3][q]});
+      mx = fmaxf(mx, sm[4][q]);
+    }
+    w[0] = T.m;
+    w[1] = T.s;
+    w[2] = S.m;
+    w[3] = S.s;
+    w[4] = mx;
+  }
+  __shared__ float ov[kMaxKP];
+  __shared__ int oi[kMaxKP];
+  block_topk<kSelA>(ktx, KP, ov, oi, rv, ri);
+  __syncthreads();
+  if (tid < KP) {
+    w[5 + tid] = ov[tid];
+    w[5 + KP + tid] = __int_as_float(oi[tid]);
+  }
+  __syncthreads();
+  block_topk<kSelA>(kts, KP, ov, oi, rv, ri);
+  __syncthreads();
+  if (tid < KP) {
+    w[5 + 2 * KP + tid] = ov[tid];
+    w[5 + 3 * KP + tid] = __int_as_float(oi[tid]);
+  }
+}
+
+// ---- phase B: one wave per row merges the slices: timestamp-forcing rule, log-softmax normaliser, top-KP ----
+__global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ ws, RuleOpts o, int KP,
+                                                      int* __restrict__ out_tok, float* __restrict__ out_lp) {
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
+  const float* w = ws + (long)r * kSlices * sel_ws_stride(KP);
+  MS T{-INFINITY, 0.f}, S{-INFINITY, 0.f};
+  float tmax = -INFINITY;
+  for (int q = 0; q < kSlices; ++q) {
+    const float* x = w + q * sel_ws_stride(KP);
+    T = ms_merge(T, MS{x[0], x[1]});
+    S = ms_merge(S, MS{x[2], x[3]});
+    tmax = fmaxf(tmax, x[4]);
+  }
+  const float lse_ts = ms_lse(S);
+  const bool mask_text = !o.without_ts && (lse_ts > tmax);
+  const float lse_text = ms_lse(T);
+  float lse_all;
+  if (mask_text) {
+    lse_all = lse_ts;
+  } else {
+    const float m = fmaxf(lse_text, lse_ts);
+    lse_all = m == -INFINITY ? -INFINITY : m + __logf(__expf(lse_text - m) + __expf(lse_ts - m));
+  }
+  // candidates: lane owns up to 3 (slice, kind, k) entries of the 2 * kSlices * KP list
+  TopK t;
+  topk_init(t);
+  const int ncand = 2 * kSlices * KP;
+  for (int c = lane; c < ncand; c += 64) {
+    const int q = c / (2 * KP), rem = c % (2 * KP), kind = rem / KP, k = rem % KP;
+    if (kind == 0 && mask_text) continue;
+    const float* x = w + q * sel_ws_stride(KP) + 5 + 2 * KP * kind;
+    topk_push(t, x[k], __float_as_int(x[KP + k]), KP);
+  }
+  __shared__ float rv[1];
+  __shared__ int ri[1];
+  __shared__ float ov[kMaxKP];
+  __shared__ int oi[kMaxKP];
+  block_topk<64>(t, KP, ov, oi, rv, ri);
+  __syncthreads();
+  if (lane < KP) {
+    const int bi = oi[lane];
+    const float bv = ov[lane];
+    out_tok[r * KP + lane] = bi == 0x7FFFFFFF ? o.eot : bi;
+    out_lp[r * KP + lane] = bv == -INFINITY ? -INFINITY : bv - lse_all;
   }
 }
 
@@ -512,11 +599,14 @@ __global__ void align_scale_kernel(float* __restrict__ out, int Tn, int Tk, cons
 }
 
 // ------------------------------------------------------------------------------------------------
+size_t logits_select_ws_floats(int R, int KP) { return (size_t)R * kSlices * (5 + 4 * KP); }
+
 void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const RowPtrs& rp, int R, int KP, int* tok,
-                          float* lp, const int* row_map, hipStream_t st) {
+                          float* lp, const int* row_map, float* ws, hipStream_t st) {
   WMX_CHECK(KP <= kMaxKP, "beam too large");
   RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
-  hipLaunchKernelGGL(logits_select_kernel, dim3(R), dim3(kSelThreads), 0, st, logits, ldl, o, rs, KP, tok, lp, row_map);
+  hipLaunchKernelGGL(logits_select_a, dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, KP, row_map, ws);
+  hipLaunchKernelGGL(logits_select_b, dim3(R), dim3(64), 0, st, ws, o, KP, tok, lp);
   WMX_HIP(hipGetLastError());
 }
 

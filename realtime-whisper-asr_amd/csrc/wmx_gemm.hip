@@ -55,6 +55,60 @@ __device__ inline void epi_store(const Epi& e, int m, int n, float v) {
   }
 }
 
+// four consecutive columns n..n+3 (n % 4 == 0, n + 3 < N): vectorised loads / stores
+template <DT T>
+__device__ inline void epi_store4(const Epi& e, int m, int n, float4 v) {
+  if (e.bias) {
+    const float4 b = *reinterpret_cast<const float4*>(e.bias + n);
+    v.x += b.x;
+    v.y += b.y;
+    v.z += b.z;
+    v.w += b.w;
+  }
+  switch (e.kind) {
+    case EPI_GELU16:
+      v = make_float4(gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w));
+      [[fallthrough]];
+    case EPI_STORE16: {
+      u16x4 h = {from_f32<T>(v.x), from_f32<T>(v.y), from_f32<T>(v.z), from_f32<T>(v.w)};
+      *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
+      break;
+    }
+    case EPI_RESID32: {
+      float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n);
+      float4 x = *o;
+      *o = make_float4(x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w);
+      break;
+    }
+    case EPI_GELU_POS32: {
+      const float4 p = *reinterpret_cast<const float4*>(e.pos + (long)(m % e.posT) * e.ldc + n);
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n) =
+          make_float4(gelu_erf(v.x) + p.x, gelu_erf(v.y) + p.y, gelu_erf(v.z) + p.z, gelu_erf(v.w) + p.w);
+      break;
+    }
+    case EPI_STORE32:
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n) = v;
+      break;
+    case EPI_QKV_CACHE: {
+      const int d = e.d;
+      u16x4 h = {from_f32<T>(v.x), from_f32<T>(v.y), from_f32<T>(v.z), from_f32<T>(v.w)};
+      uint16_t* dst;
+      if (n < d) {
+        dst = reinterpret_cast<uint16_t*>(e.out) + (long)m * d + n;
+      } else {
+        const int r = m / e.Tn, i = m - r * e.Tn;
+        const long slot = (long)(*e.slot0) + i;
+        uint16_t* cache = n < 2 * d ? e.kc : e.vc;
+        dst = cache + (slot * e.R + (long)r * e.rmul) * d + (n % d);
+      }
+      *reinterpret_cast<u16x4*>(dst) = h;
+      break;
+    }
+    default:
+      break;
+  }
+}
+
 template <DT T, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __restrict__ A, long lda,
                                                            const uint16_t* __restrict__ W, long ldw, int M, int N,
@@ -150,24 +204,43 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
     __syncthreads();
   }
 
-  // epilogue: lane holds rows fq*4 + r, col fr of each 16x16 tile
+  // epilogue through LDS, WM row rounds: the waves of row group `rd` park their fp32 accumulators in a
+  // [BM/WM][BN+4] image, then all threads apply the epilogue 4 columns at a time with vector stores.
+  constexpr int RR = BM / WM, LDT = BN + 4;
+  static_assert(RR * LDT * 4 <= 2 * TILE_BYTES, "epilogue image exceeds the staging LDS");
+  float* img = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
+  for (int rd = 0; rd < WM; ++rd) {
+    if (wm == rd) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * (BN / WN) + j * 16 + fr;
-      if (n >= N) continue;
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / WM) + i * 16 + fq * 4 + r;
-        if (m >= M) continue;
-        if (ws) {
-          ws[((long)blockIdx.y * M + m) * N + n] = acc[i][j][r];
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) img[(i * 16 + fq * 4 + r) * LDT + wn * (BN / WN) + j * 16 + fr] = acc[i][j][r];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < RR * BN / 4; idx += NW * 64) {
+      const int row = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
+      const int m = m0 + rd * RR + row, n = n0 + c4;
+      if (m >= M || n >= N) continue;
+      const float4 v = *reinterpret_cast<const float4*>(img + row * LDT + c4);
+      if (ws) {
+        float* w = ws + ((long)blockIdx.y * M + m) * N + n;
+        if (n + 3 < N && (N & 3) == 0) {
+          *reinterpret_cast<float4*>(w) = v;
         } else {
-          epi_store<T>(e, m, n, acc[i][j][r]);
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+          for (int q = 0; q < 4 && n + q < N; ++q) w[q] = vv[q];
         }
+      } else if (n + 3 < N && (e.ldc & 3) == 0) {
+        epi_store4<T>(e, m, n, v);
+      } else {
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        for (int q = 0; q < 4 && n + q < N; ++q) epi_store<T>(e, m, n + q, vv[q]);
       }
     }
+    __syncthreads();
   }
 }
 
@@ -180,6 +253,130 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restric
     for (int s = 0; s < splits; ++s) v += ws[s * total + i];
     epi_store<T>(e, (int)(i / N), (int)(i % N), v);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// skinny GEMM for decode steps (M <= 256 rows = streams x beams): one workgroup = all M rows x 16 output
+// columns; the 4 waves split K and their partial tiles are summed in LDS (deterministic, no split-K launch).
+// Weights (the only large operand) stream once with 16-B loads, KU k-steps in flight per wave; activations are
+// L2-resident and read as MFMA fragments directly.  N/16 workgroups (80-320 for Whisper widths).
+// ------------------------------------------------------------------------------------------------
+template <DT T, int MT, int NW>
+__global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(const uint16_t* __restrict__ A, long lda,
+                                                              const uint16_t* __restrict__ W, long ldw, int M, int N,
+                                                              int K, Epi e) {
+  // NW waves split K; each wave issues KU k-steps of loads (KU weight + KU*MT activation fragments) before any MFMA
+  constexpr int KU = MT <= 2 ? 8 : (MT <= 4 ? 4 : (MT <= 8 ? 2 : 1));
+  constexpr int LDR = 17;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [NW][MT*16][LDR]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int n = min(n0 + fr, N - 1);
+  const int ksteps = K / 32;
+  const int per = (ksteps + NW - 1) / NW;
+  const int ks0 = wave * per, ks1 = min(ksteps, ks0 + per);
+  f32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0, 0, 0, 0};
+  const uint16_t* wrow = W + (long)n * ldw + 8 * fq;
+  // rows >= M are clamped to M-1: they only feed output rows that are never stored
+  const uint16_t* arow[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) arow[i] = A + (long)min(i * 16 + fr, M - 1) * lda + 8 * fq;
+  for (int kk = ks0; kk < ks1; kk += KU) {
+    u16x8 b[KU], av[KU][MT];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int k = min(kk + u, ks1 - 1) * 32;
+      b[u] = *reinterpret_cast<const u16x8*>(wrow + k);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(arow[i] + k);
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      if (kk + u < ks1) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i] = mfma16<T>(av[u][i], b[u], acc[i]);
+      }
+    }
+  }
+  // every wave parks its partial tile (lane: rows i*16 + fq*4 + r, column fr); then all threads sum over waves
+  float* mine = red + (long)wave * MT * 16 * LDR;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mine[(i * 16 + fq * 4 + r) * LDR + fr] = acc[i][r];
+  __syncthreads();
+  // epilogue: 4 columns per thread
+  for (int idx = tid; idx < MT * 16 * 4; idx += NW * 64) {
+    const int row = idx >> 2, c4 = (idx & 3) * 4;
+    const int m = row, nn = n0 + c4;
+    if (m >= M || nn >= N) continue;
+    float v4[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < NW; ++w) {
+      const float* p = red + ((long)w * MT * 16 + row) * LDR + c4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v4[q] += p[q];
+    }
+    const float4 v = make_float4(v4[0], v4[1], v4[2], v4[3]);
+    if (nn + 3 < N && (e.ldc & 3) == 0) {
+      epi_store4<T>(e, m, nn, v);
+    } else {
+      for (int q = 0; q < 4 && nn + q < N; ++q) epi_store<T>(e, m, nn + q, v4[q]);
+    }
+  }
+}
+
+template <DT T, int MT, int NW>
+static void launch_skinny_cfg(const GemmCall& g, hipStream_t st) {
+  const size_t smem = (size_t)NW * MT * 16 * 17 * sizeof(float);
+  hipLaunchKernelGGL((gemm_skinny_kernel<T, MT, NW>), dim3((g.N + 15) / 16), dim3(NW * 64), smem, st, g.A, g.lda, g.W,
+                     g.ldw, g.M, g.N, g.K, g.epi);
+}
+
+template <DT T, int MT, int NW>
+static void skinny_attr() {
+  const size_t smem = (size_t)NW * MT * 16 * 17 * sizeof(float);
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm_skinny_kernel<T, MT, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)smem));
+}
+
+// set every kernel attribute up front (never inside a stream capture)
+void gemm_init_attributes() {
+  static bool done = false;
+  if (done) return;
+  skinny_attr<DT::BF16, 1, 16>();
+  skinny_attr<DT::BF16, 2, 16>();
+  skinny_attr<DT::BF16, 4, 16>();
+  skinny_attr<DT::BF16, 8, 8>();
+  skinny_attr<DT::BF16, 12, 4>();
+  skinny_attr<DT::BF16, 16, 4>();
+  skinny_attr<DT::F16, 1, 16>();
+  skinny_attr<DT::F16, 2, 16>();
+  skinny_attr<DT::F16, 4, 16>();
+  skinny_attr<DT::F16, 8, 8>();
+  skinny_attr<DT::F16, 12, 4>();
+  skinny_attr<DT::F16, 16, 4>();
+  done = true;
+}
+
+template <DT T>
+static void launch_skinny(const GemmCall& g, hipStream_t st) {
+  WMX_CHECK(g.K % 32 == 0 && g.M <= 256, "skinny gemm: shape");
+  const int mt = (g.M + 15) / 16;
+  if (mt <= 1)
+    launch_skinny_cfg<T, 1, 16>(g, st);
+  else if (mt <= 2)
+    launch_skinny_cfg<T, 2, 16>(g, st);
+  else if (mt <= 4)
+    launch_skinny_cfg<T, 4, 16>(g, st);
+  else if (mt <= 8)
+    launch_skinny_cfg<T, 8, 8>(g, st);
+  else if (mt <= 12)
+    launch_skinny_cfg<T, 12, 4>(g, st);
+  else
+    launch_skinny_cfg<T, 16, 4>(g, st);
 }
 
 template <DT T, int BM, int BN, int WM, int WN>
@@ -203,6 +400,10 @@ static void launch_cfg(const GemmCall& g, hipStream_t st) {
 
 template <DT T>
 static void launch_t(const GemmCall& g, hipStream_t st) {
+  if (g.tile == TILE_SKINNY) {
+    launch_skinny<T>(g, st);
+    return;
+  }
   WMX_CHECK(g.K % 64 == 0, "gemm: K must be a multiple of 64");
   switch (g.tile) {
     case TILE_128x128:

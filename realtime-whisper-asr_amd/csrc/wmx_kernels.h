@@ -27,7 +27,7 @@ struct Epi {
   uint16_t* vc = nullptr;
 };
 
-enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2 };
+enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3 };
 
 struct GemmCall {
   const uint16_t* A;
@@ -43,6 +43,7 @@ struct GemmCall {
 };
 
 void launch_gemm(DT dt, const GemmCall& g, hipStream_t st);
+void gemm_init_attributes();
 
 // log-mel
 size_t logmel_smem_bytes();
@@ -104,7 +105,9 @@ struct DecAttnArgs {
   int win_of_row_div;  // row -> window = row / rows_per_win
 };
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);
-void launch_cross_attn(DT dt, const DecAttnArgs& a, hipStream_t st);
+// ws: cross_attn_ws_floats(H, nwin) floats for the key-split partials (nullptr = no split)
+size_t cross_attn_ws_floats(int H, int nwin);
+void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st);
 // raw cross-attention scores of selected heads (alignment): out [nh][R*Tn][Tk] f32
 void launch_cross_scores(DT dt, const DecAttnArgs& a, const int* heads_layer_local, int nh, float* out, hipStream_t st);
 

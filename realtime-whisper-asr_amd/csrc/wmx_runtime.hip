@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -376,6 +377,8 @@ struct Ctx {
   int max_cand = 1;
   int *ctok = nullptr;
   float* clp = nullptr;
+  float* sel_ws = nullptr;
+  float* xa_ws = nullptr;
   uint32_t* mask = nullptr;
   // alignment
   float *scores = nullptr, *align_scratch = nullptr, *align_out = nullptr, *tprob = nullptr;
@@ -469,6 +472,8 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.bs.new_score, R);
   P.add(&c.ctok, (size_t)R * 9);
   P.add(&c.clp, (size_t)R * 9);
+  P.add(&c.sel_ws, logits_select_ws_floats(R, 9));
+  P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B));
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
   P.add(&c.align_scratch, (size_t)B * T * 1500);
@@ -505,6 +510,11 @@ static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ld
   g.K = K;
   g.epi = e;
   int bm, bn;
+  if (M <= 256 && K % 32 == 0 && N >= 1024) {
+    g.tile = TILE_SKINNY;
+    launch_gemm(c.dt, g, c.st);
+    return;
+  }
   if (M >= 1024) {
     g.tile = TILE_128x128;
     bm = 128;
@@ -693,7 +703,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.ck_ld = ck_ld;
       a.Tk = 1500;
       a.rows_per_win = c.K;
-      launch_cross_attn(c.dt, a, c.st);
+      launch_cross_attn(c.dt, a, c.xa_ws, c.st);
     }
     if (f.align) {
       // alignment heads of this layer
@@ -830,7 +840,8 @@ static void run_step(Ctx& c, int B) {
   dec_logits(c, nullptr, f.rows);
   RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
               c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
-  launch_logits_select(c.logits, m.d.n_vocab, ro, c.rp, f.rows, c.K + (c.K > 1 ? 1 : 0), c.ctok, c.clp, nullptr, c.st);
+  launch_logits_select(c.logits, m.d.n_vocab, ro, c.rp, f.rows, c.K + (c.K > 1 ? 1 : 0), c.ctok, c.clp, nullptr,
+                       c.sel_ws, c.st);
   if (c.K == 1)
     launch_greedy_update(c.rp, c.ctok, c.clp, f.rows, c.sp.timestamp_begin, c.sp.eot, c.hist, c.Tctx, c.slot, c.n_done,
                          c.st);
@@ -961,7 +972,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   if (max_new > 0) {
     RuleOpts ro{V, sp.eot, sp.timestamp_begin, sp.no_timestamps, sp.blank, c.o.suppress_blank,
                 c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
-    launch_logits_select(c.logits, V, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, c.row_map, c.st);
+    launch_logits_select(c.logits, V, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, c.row_map, c.sel_ws, c.st);
     if (K == 1)
       launch_greedy_update(c.rp, c.ctok, c.clp, R, sp.timestamp_begin, sp.eot, c.hist, T, c.slot, c.n_done, c.st);
     else
@@ -1421,6 +1432,7 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       c.o.suppress_tokens = nullptr;
       c.o.alignment_heads = nullptr;
       WMX_HIP(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
+      gemm_init_attributes();
       alloc_ctx(c);
     } catch (...) {
       if (c.buf) (void)hipFree(c.buf);
@@ -1579,5 +1591,108 @@ wmx_status wmx_ctx_stage_ms(wmx_ctx* x, float* out7) {
 }
 
 int wmx_ctx_last_steps(wmx_ctx* x) { return x->c.last_steps; }
+
+wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float* avg_ms, double* bytes, double* flops) {
+  return guard([&] {
+    Ctx& c = x->c;
+    Model& m = *c.m;
+    WMX_CHECK(B >= 1 && B <= c.maxB && iters >= 1, "bench_kernel: args");
+    WMX_HIP(hipSetDevice(m.device));
+    const int da = m.d.n_audio_state, dt = m.d.n_text_state, Lt = m.d.n_text_layer, H = m.d.n_text_head;
+    const long ck_ld = (long)Lt * 2 * dt;
+    const int R = c.K * B;
+    double by = 0, fl = 0;
+    std::function<void()> fn;
+    if (kernel == 0) {
+      DecAttnArgs a{};
+      a.q = c.dcq;
+      a.q_ld = dt;
+      a.o = c.dao;
+      a.R = R;
+      a.Tn = 1;
+      a.H = H;
+      a.d = dt;
+      a.ck = c.ckv;
+      a.ck_ld = ck_ld;
+      a.Tk = 1500;
+      a.rows_per_win = c.K;
+      by = (double)B * 1500 * 2 * dt * 2 + 2.0 * R * dt * 2;
+      fl = 4.0 * R * 1500 * dt;
+      fn = [&c, a] { launch_cross_attn(c.dt, a, c.xa_ws, c.st); };
+    } else if (kernel == 1) {
+      const long rows = (long)B * 1500;
+      by = (double)rows * da * 2 + 4.0 * da * da * 2 + (double)rows * 4 * da * 2;
+      fl = 2.0 * rows * 4 * da * da;
+      fn = [&c, &m, rows, da] {
+        gemm(c, c.ehb, da, m.enc[0].wfc1, da, (int)rows, 4 * da, da, epi(EPI_GELU16, m.enc[0].bfc1, c.ef1, 4 * da));
+      };
+    } else if (kernel == 2) {
+      AttnArgs a{};
+      a.q = c.eqkv;
+      a.k = c.eqkv + da;
+      a.v = c.eqkv + 2 * da;
+      a.q_ld = a.k_ld = a.v_ld = 3 * da;
+      a.q_bstride = a.k_bstride = a.v_bstride = 1500L * 3 * da;
+      a.o = c.eao;
+      a.o_ld = da;
+      a.o_bstride = 1500L * da;
+      a.B = B;
+      a.H = m.d.n_audio_head;
+      a.Tq = a.Tk = 1500;
+      a.head_stride = 64;
+      by = (double)B * 1500 * 4 * da * 2;
+      fl = 4.0 * B * m.d.n_audio_head * 1500.0 * 1500.0 * 64;
+      fn = [&c, a] { launch_attn_encoder(c.dt, a, c.st); };
+    } else if (kernel == 3) {
+      std::vector<long> lens(B, std::min<long>(480000, c.max_samples));
+      WMX_HIP(hipMemcpy(c.lens, lens.data(), B * sizeof(long), hipMemcpyHostToDevice));
+      WMX_HIP(hipMemset(c.seek, 0, B * 4));
+      by = (double)B * (480000.0 * 4 + m.d.n_mels * 3000.0 * 4);
+      fl = (double)B * 3001 * (400.0 * 416 * 2);
+      fn = [&c, &m, B] {
+        launch_logmel(c.pcm, std::min<long>(480000, c.max_samples), c.lens, c.seek, B, 3001, m.mel_basis, m.mel_first,
+                      m.mel_count, m.mel_off, m.mel_w, m.d.n_mels, c.mel_raw, c.fcap, c.wmax, c.mel, c.st);
+      };
+    } else if (kernel == 4) {
+      by = 4.0 * dt * dt * 2 + (double)R * dt * 2 + (double)R * 4 * dt * 2;
+      fl = 2.0 * R * 4 * dt * dt;
+      fn = [&c, &m, R, dt] {
+        gemm(c, c.dhb, dt, m.dec[0].wfc1, dt, R, 4 * dt, dt, epi(EPI_GELU16, m.dec[0].bfc1, c.df1, 4 * dt));
+      };
+    } else if (kernel == 5) {
+      DecAttnArgs a{};
+      a.q = c.dq;
+      a.q_ld = dt;
+      a.o = c.dao;
+      a.R = R;
+      a.Tn = 1;
+      a.H = H;
+      a.d = dt;
+      a.kc = c.kc;
+      a.vc = c.vc;
+      a.anc = c.K > 1 ? c.anc : nullptr;
+      a.anc_ld = c.Tctx;
+      a.pad = c.pad_row;
+      a.slot0 = c.slot;
+      int s = 0;
+      WMX_HIP(hipMemcpy(&s, c.slot, 4, hipMemcpyDeviceToHost));
+      by = (double)R * (s + 1) * dt * 2 * 2;
+      fl = 4.0 * R * (s + 1) * dt;
+      fn = [&c, a] { launch_self_attn(c.dt, a, c.st); };
+    } else {
+      WMX_CHECK(false, "bench_kernel: unknown kernel");
+    }
+    fn();  // warm
+    WMX_HIP(hipEventRecord(c.ev[0], c.st));
+    for (int i = 0; i < iters; ++i) fn();
+    WMX_HIP(hipEventRecord(c.ev[1], c.st));
+    WMX_HIP(hipEventSynchronize(c.ev[1]));
+    float ms = 0;
+    WMX_HIP(hipEventElapsedTime(&ms, c.ev[0], c.ev[1]));
+    *avg_ms = ms / iters;
+    *bytes = by;
+    *flops = fl;
+  });
+}
 
 }  // extern "C"

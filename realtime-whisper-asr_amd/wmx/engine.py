@@ -42,7 +42,8 @@ MODEL_DIMS["tiny.en"] = MODEL_DIMS["tiny"]
 MODEL_DIMS["base.en"] = MODEL_DIMS["base"]
 MODEL_DIMS["large"] = MODEL_DIMS["large-v3"]
 
-# real alignment heads of released checkpoints (openai whisper/__init__.py _ALIGNMENT_HEADS, as (layer, head))
+# alignment heads of released checkpoints as (layer, head): the generation_config.json "alignment_heads" of the
+# HF openai/whisper-large-v3 repo (not reachable offline; only used as the head set, any set is valid)
 ALIGNMENT_HEADS = {
     "large-v3": [(7, 0), (10, 17), (12, 18), (13, 12), (16, 1), (17, 14), (19, 11), (21, 4), (24, 1), (25, 6)],
 }
@@ -266,6 +267,16 @@ class Context:
 
     def last_steps(self) -> int:
         return int(lib.wmx_ctx_last_steps(self._h))
+
+    KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5}
+
+    def bench_kernel(self, kernel: str, batch: int, iters: int = 50):
+        """Average launch duration (ms) of one hot-path kernel replayed on the context stream (HIP events),
+        with its algorithmic bytes and flops per launch."""
+        ms, by, fl = C.c_float(), C.c_double(), C.c_double()
+        check(lib.wmx_ctx_bench_kernel(self._h, self.KERNELS[kernel], batch, iters, C.byref(ms), C.byref(by),
+                                       C.byref(fl)))
+        return float(ms.value), float(by.value), float(fl.value)
 
     def close(self):
         if getattr(self, "_h", None):
