@@ -1,0 +1,61 @@
+"""C-ABI boundary checks that need no GPU: libwmx.so loads, exports every entry point include/wmx.h declares,
+and the ctypes struct layouts match the header's field lists."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "wmx.h")
+LIB = os.path.join(ROOT, "realtime-whisper-asr_amd", "wmx", "libwmx.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(wmx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for must in ("wmx_model_create", "wmx_ctx_create", "wmx_logmel", "wmx_transcribe", "wmx_result_free",
+                 "wmx_last_error", "wmx_model_arena"):
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "build libwmx.so first (make -C realtime-whisper-asr_amd)"
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [f for f in declared_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_ctypes_binding_loads_and_matches():
+    from wmx import _lib
+    assert _lib.lib.wmx_version().decode().startswith("wmx")
+    assert sorted(_lib.EXPORTS) == declared_functions()
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+
+    def fields(struct):
+        body = re.search(r"typedef struct \{([^}]*)\}\s*" + struct + ";", src).group(1)
+        return [re.findall(r"(\w+)\s*;", ln)[0] for ln in body.split("\n") if ";" in ln]
+
+    assert [f[0] for f in _lib.Dims._fields_] == fields("wmx_dims")
+    assert [f[0] for f in _lib.Opts._fields_] == fields("wmx_opts")
+    assert [f[0] for f in _lib.WindowResult._fields_] == fields("wmx_window_result")
+
+
+def test_no_gpu_calls_fail_cleanly():
+    """Without a GPU the library must report an error (no silent CPU fallback)."""
+    import ctypes as C
+
+    from wmx import _lib
+    if _lib.lib.wmx_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    d = _lib.Dims(80, 51865, 1500, 128, 2, 2, 448, 128, 2, 2)
+    h = C.c_void_p()
+    st = _lib.lib.wmx_model_create(C.byref(d), 0, 0, C.byref(h))
+    assert st != 0
+    assert len(_lib.lib.wmx_last_error()) > 0

@@ -1,0 +1,63 @@
+"""GPU end-to-end: the drop-in MI355XWhisperASR (reference CustomFasterWhisperASR surface) driven by the
+streaming processors, single stream and batched multi-stream, on a small synthetic model."""
+import numpy as np
+import pytest
+
+from wmx import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def asr():
+    from wmx.asr import MI355XWhisperASR
+    return MI355XWhisperASR(lan="auto", modelsize="micro", device="cuda", compute_type="float16",
+                            transcribe_kwargs={"beam_size": 5}, max_new_tokens=24)
+
+
+def test_asr_surface(asr):
+    audio = synth.speech_like(3, 16000 * 6)
+    segs = asr.transcribe(audio, init_prompt="t12 t99")
+    words = asr.ts_words(segs)
+    ends = asr.segments_end_ts(segs)
+    assert asr.sep == ""
+    assert len(ends) == len(segs)
+    for s, e, w in words:
+        assert 0.0 <= s <= e <= 6.5 and isinstance(w, str)
+    for seg in segs:
+        assert seg.start <= seg.end and 0.0 <= seg.no_speech_prob <= 1.0
+    asr.set_translate_task()
+    assert asr.transcribe_kargs["task"] == "translate"
+    segs2 = asr.transcribe(audio)
+    assert isinstance(segs2, list)
+    del asr.transcribe_kargs["task"]
+
+
+def test_streaming_processor_on_gpu(asr):
+    from wmx.online import EnhancedOnlineASRProcessor
+    p = EnhancedOnlineASRProcessor(asr, buffer_trimming=("segment", 15), agreement_n=2)
+    audio = synth.speech_like(4, 16000 * 8)
+    outs = []
+    for i in range(0, len(audio), 8000):  # 0.5 s cadence (reference 一键.py:1510)
+        p.insert_audio_chunk(audio[i: i + 8000])
+        outs.append(p.process_iter())
+    outs.append(p.finish())
+    for beg, end, text in outs:
+        if beg is not None:
+            assert beg <= end
+
+
+def test_stream_batcher_matches_single_stream_calls(asr):
+    """B streams through one batched launch give the same words as B separate calls."""
+    from wmx.online import StreamBatcher
+    model = asr.model
+    audios = [synth.speech_like(20 + i, 16000 * (4 + i)) for i in range(3)]
+    model.max_batch = 3
+    model._ctx.clear()
+    batched = model.transcribe_batch(audios, ["", "t5 t6", ""])
+    model.max_batch = 1
+    model._ctx.clear()
+    single = [model.transcribe_batch([a], [p])[0] for a, p in zip(audios, ["", "t5 t6", ""])]
+    for b, s in zip(batched, single):
+        assert [seg.tokens for seg in b] == [seg.tokens for seg in s]
+    assert StreamBatcher(model, asr) is not None
