@@ -9,6 +9,8 @@
 //   (row whose cache slot holds the history of row r), so beam reordering never copies the KV cache.
 // dec_cross_attn: one workgroup per (window, head): all beams of a window share one streamed read of the
 //   window's cross K/V (the dominant HBM stream of the decode loop).
+#include <cstdlib>
+
 #include "wmx_common.h"
 #include "wmx_kernels.h"
 
@@ -37,8 +39,9 @@ __global__ __launch_bounds__(256) void attn_flash_kernel(FlashArgs fa) {
   __shared__ __attribute__((aligned(16))) uint16_t Vt[64 * VTLD];
 
   const uint16_t* qb = a.q + (long)b * a.q_bstride + (long)h * a.head_stride;
-  const uint16_t* kbp = a.k + (long)b * a.k_bstride + (long)h * a.head_stride;
-  const uint16_t* vbp = a.v + (long)b * a.v_bstride + (long)h * a.head_stride;
+  const long kvh = a.kv_head_stride ? a.kv_head_stride : a.head_stride;
+  const uint16_t* kbp = a.k + (long)b * a.k_bstride + (long)h * kvh;
+  const uint16_t* vbp = a.v + (long)b * a.v_bstride + (long)h * kvh;
   const int q0 = blockIdx.x * 128 + wave * 32;
   const int kbeg = fa.kbegin ? fa.kbegin[b] : 0;
 
@@ -200,8 +203,36 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
   const int slot_q = *a.slot0 + i;
   const int beg = a.pad ? a.pad[r] : 0;
   const int gi = lane >> 3, j = lane & 7;  // 8 key groups x 8 dim chunks per wave
+  const long kvR = a.kv_R;
   float q[8];
-  {
+  if (a.qS > 0) {
+    // decode step fed by QKV split-K partials: reduce q/k/v of (row m, head h) in slice order, round to the model
+    // dtype (as the stored path does), put k/v into the cache slot, keep q in LDS
+    __shared__ float qs[64];
+    if (tid < 192) {
+      const int part = tid >> 6, e = tid & 63;
+      const int col = part * a.d + h * 64 + e;
+      float p = 0.f;
+      const float* src = a.qpart + (long)m * a.qpart_ld + col;
+      for (int s0 = 0; s0 < a.qS; s0 += 8) {  // all loads of a batch in flight, slice order kept
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = s0 + u < a.qS ? src[(s0 + u) * a.qpart_stride] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) p += t[u];
+      }
+      const uint16_t hv = from_f32<T>(p + (a.qbias ? a.qbias[col] : 0.f));
+      if (part == 0)
+        qs[e] = to_f32<T>(hv);
+      else
+        const_cast<uint16_t*>(part == 1 ? a.kc : a.vc)[((long)slot_q * kvR + r) * a.d + h * 64 + e] = hv;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = qs[j * 8 + e] * 0.125f;
+  } else {
     const u16x8 qv = *reinterpret_cast<const u16x8*>(a.q + (long)m * a.q_ld + h * 64 + j * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) q[e] = to_f32<T>(qv[e]) * 0.125f;
@@ -215,7 +246,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
     for (int u = 0; u < U; ++u) {
       const int key = min(s0 + 8 * u + gi, slot_q);
       const int row = anc ? anc[key] : r;
-      kv[u] = *reinterpret_cast<const u16x8*>(a.kc + ((long)key * a.R + row) * a.d + h * 64 + j * 8);
+      kv[u] = *reinterpret_cast<const u16x8*>(a.kc + ((long)key * kvR + row) * a.d + h * 64 + j * 8);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -253,7 +284,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
     for (int u = 0; u < U; ++u) {
       const int key = min(s0 + 8 * u + gi, slot_q);
       const int row = anc ? anc[key] : r;
-      vv[u] = *reinterpret_cast<const u16x8*>(a.vc + ((long)key * a.R + row) * a.d + h * 64 + j * 8);
+      vv[u] = *reinterpret_cast<const u16x8*>(a.vc + ((long)key * kvR + row) * a.d + h * 64 + j * 8);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -291,57 +322,82 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// decoder cross attention for a decode step: one workgroup per (window, head); nq = rows_per_win*Tn <= 8
+// decoder cross attention for a decode step: workgroup = (head, window, key chunk of CHUNK keys); the nq =
+// rows_per_win * Tn <= 8 query rows of a window share the window's K/V stream, which is read exactly once.
 // ------------------------------------------------------------------------------------------------
-constexpr int kMaxQ = 8, kMaxTk = 1536;
-constexpr int kChunk = 384, kVPre = kChunk / 32;  // keys per workgroup, V rows prefetched per thread
+constexpr int kMaxQ = 8, kMaxTk = 1536, kMaxSplits = 16;
 
 // Q.K^T on MFMA: A = Q (16 query rows, nq valid) from registers, B = K^T straight from HBM (lane: key l&15,
-// 16 B of head dims) — the dominant stream is read exactly once with 16-B loads, 8 key blocks in flight per
-// wave.  Softmax in LDS, P.V on VALU (thread = 8 keys-apart group x 8 dims, 16-B V loads).  KS key splits per
-// (window, head) keep all CUs streaming at small batch; partial (m, l, o) are merged by dec_cross_combine.
-template <DT T>
-__global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int KS, float* __restrict__ part,
-                                                             int* __restrict__ cnt) {
+// 16 B of head dims, contiguous in the head-major cross-K/V layout).  Every K and V load of the chunk is issued
+// before any arithmetic.  Softmax in LDS, P.V on VALU (thread = key group x 8 dims, 16-B V loads).
+// KS > 1: each chunk writes its (max, sum, o[64]) record per query row; dec_cross_combine merges them in chunk
+// order (no atomics, no cross-workgroup fences inside the kernel).
+template <DT T, int CHUNK>
+__global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int KS, float* __restrict__ part) {
+  constexpr int VPRE = CHUNK / 32;      // V rows per thread (32 key groups x 8 dim chunks)
+  constexpr int NB = CHUNK / 16 / 4;    // 16-key blocks per wave
   const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nq = a.rows_per_win * a.Tn;
   const int m0 = w * nq;
-  const int chunk = ((a.Tk + KS - 1) / KS + 15) / 16 * 16;  // <= kChunk
-  const int k0 = ks * chunk, k1 = min(a.Tk, k0 + chunk);
+  const int k0 = ks * CHUNK, k1 = min(a.Tk, k0 + CHUNK);
   const int nk = max(0, k1 - k0);
-  __shared__ float sc[kMaxQ][kChunk + 4];
+  __shared__ float sc[kMaxQ][CHUNK + 4];
   __shared__ float red[kMaxQ][4];
   __shared__ float fin[4][kMaxQ][64];
-  const uint16_t* kbase = a.ck + (long)w * a.Tk * a.ck_ld + h * 64;
-  const uint16_t* vbase = kbase + a.d;
-  // P.V mapping: thread = (key group kg = tid >> 3 of 32, dims c*8 .. c*8+7); prefetch all its V rows now
+  const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
+  const uint16_t* vbase = a.cv + (long)w * a.x_wstride + (long)h * a.x_hstride;
   const int kg = tid >> 3, c = tid & 7;
-  u16x8 vpre[kVPre];
-#pragma unroll
-  for (int i = 0; i < kVPre; ++i) {
-    const int t = min(kg + 32 * i, nk - 1);
-    vpre[i] = *reinterpret_cast<const u16x8*>(vbase + (long)(k0 + max(t, 0)) * a.ck_ld + c * 8);
-  }
-  // Q fragments: lane row q = lane & 15, dims 32s + 8(lane>>4) .. +8
   const int fr = lane & 15, g = lane >> 4;
-  u16x8 qa[2];
+  u16x8 vpre[VPRE];
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    u16x8 z = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (fr < nq) z = *reinterpret_cast<const u16x8*>(a.q + (long)(m0 + fr) * a.q_ld + h * 64 + 32 * s2 + 8 * g);
-    qa[s2] = z;
+  for (int i = 0; i < VPRE; ++i) {
+    const int t = min(kg + 32 * i, nk - 1);
+    vpre[i] = *reinterpret_cast<const u16x8*>(vbase + (long)(k0 + max(t, 0)) * 64 + c * 8);
   }
-  // ---- scores: wave handles key blocks wave, wave+4, ... (<= 6 per wave), all loads issued first ----
   const int nblk = (nk + 15) / 16;
-  constexpr int NB = kChunk / 16 / 4;  // 6
   u16x8 kb[NB][2];
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     const int key = min(k0 + (wave + 4 * u) * 16 + fr, a.Tk - 1);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) kb[u][s2] = *reinterpret_cast<const u16x8*>(kbase + (long)key * a.ck_ld + 32 * s2 + 8 * g);
+    for (int s2 = 0; s2 < 2; ++s2) kb[u][s2] = *reinterpret_cast<const u16x8*>(kbase + (long)key * 64 + 32 * s2 + 8 * g);
   }
+  // Q fragments: lane row q = lane & 15, dims 32s + 8(lane>>4) .. +8
+  u16x8 qa[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    u16x8 z = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (fr < nq) {
+      const int col = h * 64 + 32 * s2 + 8 * g;
+      if (a.qS > 0) {
+        // q = bias + sum of the split-K partials (slice order), rounded to the model dtype like the stored path
+        float p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const float* src = a.qpart + (long)(m0 + fr) * a.qpart_ld + col;
+        for (int q0 = 0; q0 < a.qS; q0 += 4) {  // all loads of a batch in flight, slice order kept
+          float4 x0[4], x1[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool ok = q0 + u < a.qS;
+            const float* sp = src + (long)(ok ? q0 + u : 0) * a.qpart_stride;
+            x0[u] = ok ? *reinterpret_cast<const float4*>(sp) : make_float4(0, 0, 0, 0);
+            x1[u] = ok ? *reinterpret_cast<const float4*>(sp + 4) : make_float4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            p[0] += x0[u].x; p[1] += x0[u].y; p[2] += x0[u].z; p[3] += x0[u].w;
+            p[4] += x1[u].x; p[5] += x1[u].y; p[6] += x1[u].z; p[7] += x1[u].w;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = from_f32<T>(p[e] + (a.qbias ? a.qbias[col + e] : 0.f));
+      } else {
+        z = *reinterpret_cast<const u16x8*>(a.q + (long)(m0 + fr) * a.q_ld + col);
+      }
+    }
+    qa[s2] = z;
+  }
+  // ---- scores ----
 #pragma unroll
   for (int u = 0; u < NB; ++u) {
     const int blk = wave + 4 * u;
@@ -357,7 +413,7 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int 
     }
   }
   __syncthreads();
-  // ---- softmax (partial over this key range) ----
+  // ---- softmax over this chunk ----
   float mx[kMaxQ];
 #pragma unroll
   for (int q = 0; q < kMaxQ; ++q) {
@@ -391,7 +447,7 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int 
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[q][e] = 0.f;
 #pragma unroll
-  for (int i = 0; i < kVPre; ++i) {
+  for (int i = 0; i < VPRE; ++i) {
     const int t = kg + 32 * i;
     if (t < nk) {
       float vf[8];
@@ -435,7 +491,7 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int 
     if (KS == 1) {
       a.o[(long)(m0 + q) * a.d + h * 64 + e] = from_f32<T>(o / tot);
     } else {
-      // partial record per (window, head, split, q): [m, l, o[64]]
+      // record per (window, head, chunk, q): [max, sum, o[64]]
       float* pr = part + ((((long)w * a.H + h) * KS + ks) * kMaxQ + q) * 66;
       if (e == 0) {
         pr[0] = mx[q];
@@ -444,59 +500,83 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int 
       pr[2 + e] = o;
     }
   }
-  if (KS == 1) return;
-  // ---- the last of the KS workgroups of (window, head) merges the partials (cdna_hip_programming.md
-  //      Guideline 16: drained plain stores -> agent release -> counter; last arriver: agent acquire -> loads) ----
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(cnt + w * a.H + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == KS - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  for (int t = tid; t < nq * 64; t += 256) {
-    const int q = t >> 6, e = t & 63;
-    const float* pr = part + (((long)w * a.H + h) * KS * kMaxQ + q) * 66;
-    float M = -INFINITY;
-    for (int k = 0; k < KS; ++k) M = fmaxf(M, pr[(long)k * kMaxQ * 66]);
-    float l = 0.f, o = 0.f;
-    for (int k = 0; k < KS; ++k) {
-      const float* x = pr + (long)k * kMaxQ * 66;
-      const float sc2 = __expf(x[0] - M);
-      l += x[1] * sc2;
-      o += x[2 + e] * sc2;
-    }
-    a.o[(long)(m0 + q) * a.d + h * 64 + e] = from_f32<T>(o / l);
-  }
-  if (tid == 0) __hip_atomic_store(cnt + w * a.H + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-int cross_attn_splits(int Tk) { return (Tk + kChunk - 1) / kChunk; }
+// merge the KS chunk records of every (window, head, q) in chunk order: o = sum_k o_k e^{m_k - M} / sum_k l_k e^{m_k - M}
+template <DT T>
+__global__ __launch_bounds__(256) void dec_cross_combine_kernel(const float* __restrict__ part, int KS, int H, int nq,
+                                                                int d, uint16_t* __restrict__ out) {
+  const int w = blockIdx.x, h = blockIdx.y;
+  for (int t = threadIdx.x; t < nq * 64; t += 256) {
+    const int q = t >> 6, e = t & 63;
+    const float* pr = part + (((long)w * H + h) * KS * kMaxQ + q) * 66;
+    float rec[kMaxSplits][3];
+#pragma unroll
+    for (int k = 0; k < kMaxSplits; ++k) {
+      if (k < KS) {
+        const float* x = pr + (long)k * kMaxQ * 66;
+        rec[k][0] = x[0];
+        rec[k][1] = x[1];
+        rec[k][2] = x[2 + e];
+      }
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kMaxSplits; ++k)
+      if (k < KS) M = fmaxf(M, rec[k][0]);
+    float l = 0.f, o = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxSplits; ++k) {
+      if (k < KS) {
+        const float sc2 = __expf(rec[k][0] - M);
+        l += rec[k][1] * sc2;
+        o += rec[k][2] * sc2;
+      }
+    }
+    out[(long)(w * nq + q) * d + h * 64 + e] = from_f32<T>(o / l);
+  }
+}
 
-// partial records + one arrival counter per (window, head) (the counters must start at 0; the last arriver resets)
-size_t cross_attn_ws_floats(int H, int nwin) { return (size_t)nwin * H * 8 * kMaxQ * 66 + (size_t)nwin * H; }
+// keys per workgroup; WMX_CROSS_CHUNK (128 / 256 / 384) overrides the default for tuning runs
+static int cross_chunk(int Tk) {
+  static const int env = [] {
+    const char* v = getenv("WMX_CROSS_CHUNK");
+    return v ? atoi(v) : 0;
+  }();
+  if (env) return env;
+  return Tk > 768 ? 256 : 128;
+}
+
+int cross_attn_splits(int Tk) { return (Tk + cross_chunk(Tk) - 1) / cross_chunk(Tk); }
+
+size_t cross_attn_ws_floats(int H, int nwin) { return (size_t)nwin * H * kMaxSplits * kMaxQ * 66; }
+
+template <DT T>
+static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
+  const int nq = a.rows_per_win * a.Tn;
+  const int nwin = a.R / a.rows_per_win;
+  const int chunk = cross_chunk(a.Tk);
+  const int KS = (a.Tk + chunk - 1) / chunk;
+  WMX_CHECK(KS <= kMaxSplits, "cross attn: too many key chunks");
+  WMX_CHECK(KS == 1 || ws != nullptr, "cross attn: split workspace required");
+  dim3 grid(a.H, nwin, KS);
+  switch (chunk) {
+    case 128: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 128>), grid, dim3(256), 0, st, a, KS, ws); break;
+    case 256: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 256>), grid, dim3(256), 0, st, a, KS, ws); break;
+    case 384: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 384>), grid, dim3(256), 0, st, a, KS, ws); break;
+    default: WMX_CHECK(false, "cross attn: unsupported key chunk");
+  }
+  if (KS > 1)
+    hipLaunchKernelGGL(dec_cross_combine_kernel<T>, dim3(nwin, a.H), dim3(256), 0, st, ws, KS, a.H, nq, a.d, a.o);
+}
 
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {
   const int nq = a.rows_per_win * a.Tn;
   WMX_CHECK(nq <= kMaxQ && a.Tk <= kMaxTk, "cross attn: too many queries per window");
-  const int nwin = a.R / a.rows_per_win;
-  const int KS = cross_attn_splits(a.Tk);
-  WMX_CHECK(KS == 1 || ws != nullptr, "cross attn: split workspace required");
-  dim3 grid(a.H, nwin, KS);
-  int* cnt = ws ? reinterpret_cast<int*>(ws + (size_t)nwin * a.H * 8 * kMaxQ * 66) : nullptr;
   if (dt == DT::BF16)
-    hipLaunchKernelGGL(dec_cross_attn_kernel<DT::BF16>, grid, dim3(256), 0, st, a, KS, ws, cnt);
+    launch_cross_t<DT::BF16>(a, ws, st);
   else
-    hipLaunchKernelGGL(dec_cross_attn_kernel<DT::F16>, grid, dim3(256), 0, st, a, KS, ws, cnt);
+    launch_cross_t<DT::F16>(a, ws, st);
   WMX_HIP(hipGetLastError());
 }
 
@@ -512,9 +592,9 @@ __global__ __launch_bounds__(256) void cross_scores_kernel(DecAttnArgs a, const 
   __shared__ float qs[64];
   if (threadIdx.x < 64) qs[threadIdx.x] = to_f32<T>(a.q[(long)m * a.q_ld + h * 64 + threadIdx.x]) * 0.125f;
   __syncthreads();
-  const uint16_t* kbase = a.ck + (long)w * a.Tk * a.ck_ld + h * 64;
+  const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
   for (int s = threadIdx.x; s < a.Tk; s += 256) {
-    const uint16_t* kp = kbase + (long)s * a.ck_ld;
+    const uint16_t* kp = kbase + (long)s * 64;
     float acc = 0.f;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {

@@ -15,6 +15,14 @@
 
 namespace wmx {
 
+// [L][K|V][xw][H][xt][64]: each (window, head) key range is one contiguous stream for the decode step
+__device__ inline long crosskv_index(const Epi& e, int m, int n) {
+  const int w = m / e.xt, t = m - w * e.xt;
+  const int lk = n / e.d, c = n - lk * e.d;
+  const int h = c >> 6;
+  return ((((long)lk * e.xw + w) * (e.d >> 6) + h) * e.xt + t) * 64 + (c & 63);
+}
+
 template <DT T>
 __device__ inline void epi_store(const Epi& e, int m, int n, float v) {
   if (e.bias) v += e.bias[n];
@@ -50,6 +58,9 @@ __device__ inline void epi_store(const Epi& e, int m, int n, float v) {
       }
       break;
     }
+    case EPI_CROSSKV:
+      reinterpret_cast<uint16_t*>(e.out)[crosskv_index(e, m, n)] = from_f32<T>(v);
+      break;
     default:
       break;
   }
@@ -102,6 +113,11 @@ __device__ inline void epi_store4(const Epi& e, int m, int n, float4 v) {
         dst = cache + (slot * e.R + (long)r * e.rmul) * d + (n % d);
       }
       *reinterpret_cast<u16x4*>(dst) = h;
+      break;
+    }
+    case EPI_CROSSKV: {
+      u16x4 h = {from_f32<T>(v.x), from_f32<T>(v.y), from_f32<T>(v.z), from_f32<T>(v.w)};
+      *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)) = h;
       break;
     }
     default:
@@ -377,6 +393,149 @@ static void launch_skinny(const GemmCall& g, hipStream_t st) {
     launch_skinny_cfg<T, 12, 4>(g, st);
   else
     launch_skinny_cfg<T, 16, 4>(g, st);
+}
+
+// ------------------------------------------------------------------------------------------------
+// decode GEMM on packed weights (skinny M): workgroup = NCT 16-column tiles x one K slice x one 16*MT row chunk;
+// its 4 waves split the slice's k-steps, every wave issues KU k-steps of loads (NCT contiguous 1 KiB weight
+// fragments + MT activation fragments) before their MFMAs, partial tiles are summed through LDS.
+// Grid (col groups, S, row chunks).  S == 1: epilogue; S > 1: raw fp32 partials part[s][M][N].
+// ------------------------------------------------------------------------------------------------
+template <DT T, int MT, int NCT>
+__global__ __launch_bounds__(256) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
+                                                          const uint16_t* __restrict__ Wp, int M, int N, int K, int S,
+                                                          Epi e, float* __restrict__ part) {
+  constexpr int KU = (MT + NCT) <= 8 ? 2 : 1;
+  constexpr int LDR = 16 * NCT + 1;
+  __shared__ float red[4][MT * 16][LDR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ntiles = (N + 15) >> 4;
+  const int t0 = blockIdx.x * NCT;
+  const int sp = blockIdx.y;
+  const int m0 = blockIdx.z * MT * 16;
+  const int ksteps = K >> 5;
+  const int kps = (ksteps + S - 1) / S;
+  const int kb = sp * kps, ke = min(ksteps, kb + kps);
+  const int per = (max(0, ke - kb) + 3) >> 2;
+  const int ks0 = kb + wave * per, ks1 = min(ke, ks0 + per);
+  f32x4 acc[MT][NCT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+  const uint16_t* wt[NCT];
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) wt[j] = Wp + ((long)min(t0 + j, ntiles - 1) * ksteps << 9) + lane * 8;
+  // rows >= M are clamped to M-1: they only feed output rows that are never stored
+  const uint16_t* ar[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) ar[i] = A + (long)min(m0 + i * 16 + fr, M - 1) * lda + 8 * fq;
+  for (int kk = ks0; kk < ks1; kk += KU) {
+    u16x8 b[KU][NCT], av[KU][MT];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      if (kk + u < ks1) {
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) b[u][j] = *reinterpret_cast<const u16x8*>(wt[j] + ((long)(kk + u) << 9));
+#pragma unroll
+        for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + (kk + u) * 32);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u)
+      if (kk + u < ks1)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NCT; ++j) acc[i][j] = mfma16<T>(av[u][i], b[u][j], acc[i][j]);
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NCT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][i * 16 + fq * 4 + r][j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  // 4 consecutive columns per thread
+  constexpr int C4 = 4 * NCT;  // column quads per row
+  for (int idx = tid; idx < MT * 16 * C4; idx += 256) {
+    const int row = idx / C4, c = (idx - row * C4) * 4;
+    const int m = m0 + row, n = t0 * 16 + c;
+    if (m >= M || n >= N) continue;
+    float v4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v4[q] = red[0][row][c + q] + red[1][row][c + q] + red[2][row][c + q] + red[3][row][c + q];
+    if (S > 1) {
+      float* dst = part + ((long)sp * M + m) * N + n;
+      if (n + 3 < N && (N & 3) == 0) {
+        *reinterpret_cast<float4*>(dst) = make_float4(v4[0], v4[1], v4[2], v4[3]);
+      } else {
+        for (int q = 0; q < 4 && n + q < N; ++q) dst[q] = v4[q];
+      }
+    } else if (n + 3 < N && (e.ldc & 3) == 0) {
+      epi_store4<T>(e, m, n, make_float4(v4[0], v4[1], v4[2], v4[3]));
+    } else {
+      for (int q = 0; q < 4 && n + q < N; ++q) epi_store<T>(e, m, n + q, v4[q]);
+    }
+  }
+}
+
+static int packed_mt(int M) {
+  const int mt = (std::min(M, 128) + 15) / 16;
+  return mt <= 4 ? mt : (mt <= 6 ? 6 : 4);
+}
+
+int packed_nct(int M, int N, int K) {
+  const int mt = packed_mt(M);
+  if (mt > 4) return 2;
+  return (N >= 16384 || K >= 4096) ? 4 : 2;
+}
+
+int packed_splits(int M, int N, int K, long cap_elems) {
+  const int mt = packed_mt(M);
+  const int chunks = (M + mt * 16 - 1) / (mt * 16);
+  const int nct = packed_nct(M, N, K);
+  const long wgs = (long)((N + 16 * nct - 1) / (16 * nct)) * chunks;
+  long S = (480 + wgs - 1) / wgs;
+  S = std::min<long>(S, std::max(1, (K / 32) / 4));
+  S = std::min<long>(S, K / (2L * std::max(M, 1)));
+  while (S > 1 && S * M * (long)N > cap_elems) --S;
+  return (int)std::max<long>(1, S);
+}
+
+template <DT T, int MT, int NCT>
+static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
+  const int ntiles = (g.N + 15) / 16;
+  dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
+  hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT>), grid, dim3(256), 0, st, g.A, g.lda, g.W, g.M, g.N, g.K, g.S,
+                     g.epi, g.part);
+}
+
+template <DT T, int NCT>
+static void launch_packed_mt(const PackedCall& g, hipStream_t st) {
+  const int mt = (std::min(g.M, 128) + 15) / 16;
+  switch (mt) {
+    case 1: launch_packed_cfg<T, 1, NCT>(g, st); break;
+    case 2: launch_packed_cfg<T, 2, NCT>(g, st); break;
+    case 3: launch_packed_cfg<T, 3, NCT>(g, st); break;
+    case 4: launch_packed_cfg<T, 4, NCT>(g, st); break;
+    case 5:
+    case 6: launch_packed_cfg<T, 6, 2>(g, st); break;
+    default: launch_packed_cfg<T, 4, 2>(g, st); break;  // 7..8 row tiles: 64-row chunks (LDS budget)
+  }
+}
+
+void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
+  WMX_CHECK(g.M >= 1 && g.K % 32 == 0 && g.S >= 1, "packed gemm: shape");
+  WMX_CHECK(g.S == 1 || g.part != nullptr, "packed gemm: partial buffer required for S > 1");
+  const int nct = packed_nct(g.M, g.N, g.K);
+  if (dt == DT::BF16) {
+    if (nct == 4) launch_packed_mt<DT::BF16, 4>(g, st); else launch_packed_mt<DT::BF16, 2>(g, st);
+  } else {
+    if (nct == 4) launch_packed_mt<DT::F16, 4>(g, st); else launch_packed_mt<DT::F16, 2>(g, st);
+  }
+  WMX_HIP(hipGetLastError());
 }
 
 template <DT T, int BM, int BN, int WM, int WN>

@@ -11,6 +11,7 @@ enum EpiKind {
   EPI_GELU_POS32 = 3,  // out32 = gelu(acc + bias) + pos[m % posT]   (encoder conv2)
   EPI_STORE32 = 4,     // out32 = acc (+ bias)          (logits)
   EPI_QKV_CACHE = 5,   // decoder self-attn: q -> out16, k/v -> KV cache at slot *slot0 + (m % Tn)
+  EPI_CROSSKV = 6,     // cross K/V of all decoder layers -> head-major [L][K|V][xw][H][xt][64] (16-bit)
 };
 
 struct Epi {
@@ -25,6 +26,8 @@ struct Epi {
   const int* slot0 = nullptr;
   uint16_t* kc = nullptr;
   uint16_t* vc = nullptr;
+  // EPI_CROSSKV: row m = w * xt + t, column n = (l * 2 + kv) * d + h * 64 + e
+  int xw = 1, xt = 1500;
 };
 
 enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3 };
@@ -43,6 +46,35 @@ struct GemmCall {
 };
 
 void launch_gemm(DT dt, const GemmCall& g, hipStream_t st);
+
+// ---- decoder weights in MFMA-fragment-major ("packed") layout ----
+// A [N][K] weight is stored as tiles of 16 rows x 32 k (1 KiB); tile (n/16, k/32) at ((n/16)*(K/32) + k/32)*512,
+// inside a tile lane l = (n%16) + 16*((k%32)/8) holds k%8 = 0..7 contiguously.  One wave's B-fragment load of a
+// k-step is then a single contiguous, lane-linear 1 KiB read.  Sub-matrices starting at a row multiple of 16
+// (the fused QKV parts) keep the same formula with base + row0*K.  N is padded to a multiple of 16.
+__host__ __device__ inline long packed_index(long n, long k, long K) {
+  return (((n >> 4) * (K >> 5) + (k >> 5)) << 9) + (((n & 15) + 16 * ((k & 31) >> 3)) << 3) + (k & 7);
+}
+
+// C[M][N] = A[M][K] . Wp^T.  S == 1: epilogue applied in-kernel.  S > 1: K is split over S workgroup slices and
+// each writes raw fp32 partials part[s][M][N] (no bias); the consumer sums them in slice order (deterministic).
+struct PackedCall {
+  const uint16_t* A;
+  long lda;
+  const uint16_t* W;  // packed
+  int M, N, K;
+  int S = 1;
+  Epi epi;
+  float* part = nullptr;
+};
+void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st);
+int packed_nct(int M, int N, int K);
+// split count for a partial-output launch (<= cap_elems / (M*N) partial slices)
+int packed_splits(int M, int N, int K, long cap_elems);
+
+// x[m] += bias + sum_s part[s][m]; optionally out16[m] = LayerNorm(x[m]) (g == nullptr: no LN)
+void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float* x, const float* g, const float* b,
+                      uint16_t* out16, int rows, int d, hipStream_t st);
 void gemm_init_attributes();
 
 // log-mel
@@ -60,6 +92,7 @@ void launch_im2col_conv1(DT dt, const float* mel, int B, int n_mels, int Kp, uin
 void launch_im2col_conv2(DT dt, const uint16_t* h1, int B, int d, uint16_t* out, hipStream_t st);
 void launch_cvt16_to_f32(DT dt, const uint16_t* in, float* out, long n, hipStream_t st);
 // x[r*Tn+i] = tok_emb[hist[r*hist_ld + slot]] + pos_emb[slot - pad[r]],  slot = *slot0 + i
+// tok_emb is packed (packed_index), pos_emb row-major
 void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R, int Tn,
                   const int* pad, const int* slot0, int d, float* x, hipStream_t st);
 
@@ -79,6 +112,7 @@ struct AttnArgs {
   long o_bstride;
   int B, H, Tq, Tk;
   int head_stride;     // elements between heads (64 for [t][h*64] layouts)
+  long kv_head_stride = 0;  // K/V head stride when it differs from head_stride (0: same)
 };
 void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st);
 // flash attention with optional causal mask (key <= query + causal_off) and per-entry first valid key
@@ -97,11 +131,20 @@ struct DecAttnArgs {
   int anc_ld;
   const int* pad;      // [R] first valid slot
   const int* slot0;    // device scalar: slot of the first new token
+  int kv_R;            // row stride of the KV cache ([slot][kv_R][d]); >= R
   // cross
-  const uint16_t* ck;  // [W][Tk][ck_ld] (k at +0, v at +d)
-  long ck_ld;
+  // cross K/V of one layer, head-major: key t of (window w, head h) at ck + w*x_wstride + h*x_hstride + t*64
+  const uint16_t* ck;
+  const uint16_t* cv;
+  long x_wstride, x_hstride;
   int Tk;
   int rows_per_win;    // rows sharing one encoder window (beam)
+  // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
+  // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
+  const float* qpart = nullptr;
+  int qS = 0;
+  long qpart_stride = 0, qpart_ld = 0;
+  const float* qbias = nullptr;
   int win_of_row_div;  // row -> window = row / rows_per_win
 };
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);
@@ -116,8 +159,8 @@ struct InitSpec {
   int tid;
   float scale, offset;
   long n;          // logical elements
-  int kind;        // 0 plain copy order, 1 conv permute ([O][C][3] -> [O][3*C padded Kp]), 2 f32 store
-  int O, C, Kp;    // conv permute
+  int kind;        // 0 plain copy order, 1 conv permute ([O][C][3] -> [O][3*C padded Kp]), 2 packed [O][Kp]
+  int O, C, Kp;    // conv permute / packed (Kp = K)
   void* dst;
   int store_f32;   // store as f32 (biases / LN) instead of 16-bit
 };

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const uint16_t* __restrict__
   int pos = slot - (pad ? pad[r] : 0);
   pos = max(pos, 0);
   for (int c = threadIdx.x; c < d; c += 256)
-    x[(long)m * d + c] = to_f32<T>(tok_emb[(long)tok * d + c]) + to_f32<T>(pos_emb[(long)pos * d + c]);
+    x[(long)m * d + c] = to_f32<T>(tok_emb[packed_index(tok, c, d)]) + to_f32<T>(pos_emb[(long)pos * d + c]);
 }
 
 void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R, int Tn,
@@ -170,6 +170,82 @@ void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const
   else
     hipLaunchKernelGGL(embed_kernel<DT::F16>, dim3(R * Tn), dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, Tn, pad,
                        slot0, d, x);
+  WMX_HIP(hipGetLastError());
+}
+
+// ---------------- split-K reduction + residual + LayerNorm (decode step) ----------------
+// one workgroup per row: v = x + bias + sum_s part[s] (slice order fixed), x = v, out16 = LN(v) * g + b
+template <DT T>
+__global__ __launch_bounds__(256) void reduce_ln_kernel(const float* __restrict__ part, int S, long pstride,
+                                                        const float* __restrict__ bias, float* __restrict__ x,
+                                                        const float* __restrict__ g, const float* __restrict__ b,
+                                                        uint16_t* __restrict__ out, int d) {
+  constexpr int MAXV = 8;  // d <= 2048
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float red[2][4];
+  float v[MAXV], p[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) p[i] = 0.f;
+  // partial slices in batches of 4 with every load of a batch issued before the adds (slice order kept)
+  for (int s0 = 0; s0 < S; s0 += 4) {
+    float t[MAXV][4];
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = tid + i * 256;
+        t[i][u] = (c < d && s0 + u < S) ? part[(s0 + u) * pstride + (long)m * d + c] : 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p[i] += t[i][u];
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = tid + i * 256;
+    v[i] = 0.f;
+    if (c < d) {
+      const float a = x[(long)m * d + c] + (bias ? bias[c] : 0.f) + p[i];
+      x[(long)m * d + c] = a;
+      v[i] = a;
+      sum += a;
+    }
+  }
+  if (!g) return;
+  sum = wave_sum(sum);
+  if (lane == 0) red[0][wave] = sum;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / d;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = tid + i * 256;
+    if (c < d) {
+      const float t = v[i] - mean;
+      sq += t * t;
+    }
+  }
+  sq = wave_sum(sq);
+  if (lane == 0) red[1][wave] = sq;
+  __syncthreads();
+  const float rstd = 1.0f / sqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / d + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = tid + i * 256;
+    if (c < d) out[(long)m * d + c] = from_f32<T>((v[i] - mean) * rstd * g[c] + b[c]);
+  }
+}
+
+void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float* x, const float* g, const float* b,
+                      uint16_t* out16, int rows, int d, hipStream_t st) {
+  WMX_CHECK(d <= 2048, "reduce_ln: width");
+  const long pstride = (long)rows * d;
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(reduce_ln_kernel<DT::BF16>, dim3(rows), dim3(256), 0, st, part, S, pstride, bias, x, g, b, out16, d);
+  else
+    hipLaunchKernelGGL(reduce_ln_kernel<DT::F16>, dim3(rows), dim3(256), 0, st, part, S, pstride, bias, x, g, b, out16, d);
   WMX_HIP(hipGetLastError());
 }
 
@@ -195,6 +271,8 @@ __global__ void init_kernel(uint64_t key, InitSpec s) {
       const int c = (int)(oc % s.C);
       const long o = oc / s.C;
       di = o * s.Kp + (long)kk * s.C + c;
+    } else if (s.kind == 2) {
+      di = packed_index(i / s.Kp, i % s.Kp, s.Kp);
     }
     if (s.store_f32) {
       // f32 storage of a 16-bit parameter: keep the value the 16-bit storage would hold

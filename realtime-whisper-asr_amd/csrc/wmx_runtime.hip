@@ -187,7 +187,7 @@ static void build_model(Model& m) {
   }
   P.add(&m.lnpg, da);
   P.add(&m.lnpb, da);
-  P.add(&m.tok_emb, (size_t)V * dt);
+  P.add(&m.tok_emb, (size_t)(V + 15) / 16 * 16 * dt);  // packed: rows padded to a 16-row tile
   P.add(&m.dec_pos, (size_t)d.n_text_ctx * dt);
   m.dec.resize(d.n_text_layer);
   for (auto& L : m.dec) {
@@ -246,8 +246,10 @@ static void build_model(Model& m) {
     m.by_name[name] = (int)m.entries.size();
     m.entries.push_back(e);
   };
-  auto lin = [&](const std::string& p, long n_out, long n_in, uint16_t* w, float* b) {
-    add(p + ".weight", {n_out, n_in}, f32s(1.0 / std::sqrt((double)n_in)), 0.f, w, 0);
+  auto lin = [&](const std::string& p, long n_out, long n_in, uint16_t* w, float* b, bool packed = false) {
+    // decoder projections are stored packed (MFMA-fragment-major, see packed_index)
+    add(p + ".weight", {n_out, n_in}, f32s(1.0 / std::sqrt((double)n_in)), 0.f, w, 0, packed ? 2 : 0, 0,
+        packed ? (int)n_in : 0);
     if (b) add(p + ".bias", {n_out}, 0.02f, 0.f, b, 1);
   };
   auto ln = [&](const std::string& p, long n, float* g, float* b) {
@@ -271,24 +273,24 @@ static void build_model(Model& m) {
     lin(p + ".fc2", da, 4 * da, L.wfc2, L.bfc2);
   }
   ln("encoder.layer_norm", da, m.lnpg, m.lnpb);
-  add("decoder.embed_tokens.weight", {V, dt}, f32s(6.0 / std::sqrt((double)dt)), 0.f, m.tok_emb, 0);
+  add("decoder.embed_tokens.weight", {V, dt}, f32s(6.0 / std::sqrt((double)dt)), 0.f, m.tok_emb, 0, 2, 0, dt);
   add("decoder.embed_positions.weight", {d.n_text_ctx, dt}, 0.05f, 0.f, m.dec_pos, 0);
   for (int i = 0; i < d.n_text_layer; ++i) {
     DecLayer& L = m.dec[i];
     const std::string p = "decoder.layers." + std::to_string(i);
     ln(p + ".self_attn_layer_norm", dt, L.ln1g, L.ln1b);
-    lin(p + ".self_attn.q_proj", dt, dt, L.wqkv, L.bqkv);
-    lin(p + ".self_attn.k_proj", dt, dt, L.wqkv + (size_t)dt * dt, nullptr);
-    lin(p + ".self_attn.v_proj", dt, dt, L.wqkv + (size_t)2 * dt * dt, L.bqkv + 2 * dt);
-    lin(p + ".self_attn.out_proj", dt, dt, L.wo, L.bo);
+    lin(p + ".self_attn.q_proj", dt, dt, L.wqkv, L.bqkv, true);
+    lin(p + ".self_attn.k_proj", dt, dt, L.wqkv + (size_t)dt * dt, nullptr, true);
+    lin(p + ".self_attn.v_proj", dt, dt, L.wqkv + (size_t)2 * dt * dt, L.bqkv + 2 * dt, true);
+    lin(p + ".self_attn.out_proj", dt, dt, L.wo, L.bo, true);
     ln(p + ".encoder_attn_layer_norm", dt, L.ln2g, L.ln2b);
-    lin(p + ".encoder_attn.q_proj", dt, dt, L.wcq, L.bcq);
+    lin(p + ".encoder_attn.q_proj", dt, dt, L.wcq, L.bcq, true);
     lin(p + ".encoder_attn.k_proj", dt, dt, m.wckv + (size_t)i * 2 * dt * dt, nullptr);
     lin(p + ".encoder_attn.v_proj", dt, dt, m.wckv + ((size_t)i * 2 * dt + dt) * dt, m.bckv + (size_t)i * 2 * dt + dt);
-    lin(p + ".encoder_attn.out_proj", dt, dt, L.wco, L.bco);
+    lin(p + ".encoder_attn.out_proj", dt, dt, L.wco, L.bco, true);
     ln(p + ".final_layer_norm", dt, L.ln3g, L.ln3b);
-    lin(p + ".fc1", 4 * dt, dt, L.wfc1, L.bfc1);
-    lin(p + ".fc2", dt, 4 * dt, L.wfc2, L.bfc2);
+    lin(p + ".fc1", 4 * dt, dt, L.wfc1, L.bfc1, true);
+    lin(p + ".fc2", dt, 4 * dt, L.wfc2, L.bfc2, true);
   }
   ln("decoder.layer_norm", dt, m.lng, m.lnb);
 
@@ -369,6 +371,8 @@ struct Ctx {
   int logits_rows = 0;
   float* ws = nullptr;
   long ws_elems = 0;
+  float* part = nullptr;  // split-K partials of the packed decode GEMMs [S][rows][N]
+  long part_elems = 0;
   int *hist = nullptr, *hist_tmp = nullptr, *anc = nullptr, *anc_tmp = nullptr, *pad_row = nullptr, *pad_win = nullptr;
   int *slot = nullptr, *n_done = nullptr, *lang_slot = nullptr, *lang_tok = nullptr, *row_map = nullptr, *gather = nullptr;
   float *lang_prob = nullptr, *nospeech = nullptr;
@@ -436,6 +440,8 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.vc, (size_t)Lt * T * R * dt);
   P.add(&c.logits, (size_t)c.logits_rows * V);
   P.add(&c.ws, (size_t)c.ws_elems);
+  c.part_elems = (long)R * dt * 48;
+  P.add(&c.part, (size_t)c.part_elems);
   P.add(&c.hist, (size_t)R * T);
   P.add(&c.hist_tmp, (size_t)R * T);
   P.add(&c.anc, (size_t)R * T);
@@ -549,6 +555,39 @@ static Epi epi(int kind, const float* bias, void* out, long ldc) {
   return e;
 }
 
+// decoder projection on packed weights, epilogue in-kernel (any M: row chunks on the grid's z axis)
+static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, const Epi& e) {
+  PackedCall g;
+  g.A = A;
+  g.lda = lda;
+  g.W = Wp;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.S = 1;
+  g.epi = e;
+  launch_gemm_packed(c.dt, g, c.st);
+}
+
+// decoder projection on packed weights, split-K raw partials into c.part; returns the split count
+static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K) {
+  PackedCall g;
+  g.A = A;
+  g.lda = lda;
+  g.W = Wp;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.S = packed_splits(M, N, K, c.part_elems);
+  g.part = c.part;
+  if (g.S == 1) {  // nothing to split: a single slice is still written as raw partials
+    g.S = 2;
+    WMX_CHECK(2L * M * N <= c.part_elems, "decode gemm: partial buffer too small");
+  }
+  launch_gemm_packed(c.dt, g, c.st);
+  return g.S;
+}
+
 // ------------------------------------------------------------------------------------------------
 // encoder
 // ------------------------------------------------------------------------------------------------
@@ -588,11 +627,23 @@ static void encode(Ctx& c, int B) {
   launch_layernorm(c.dt, c.ex, m.lnpg, m.lnpb, c.enc_out, (int)rows, da, c.st);
 }
 
+// layer l's cross K / V in the head-major layout written by EPI_CROSSKV
+static const uint16_t* cross_k(const Ctx& c, int l) {
+  return c.ckv + (size_t)(2 * l) * c.maxB * 1500 * c.m->d.n_text_state;
+}
+static const uint16_t* cross_v(const Ctx& c, int l) {
+  return c.ckv + (size_t)(2 * l + 1) * c.maxB * 1500 * c.m->d.n_text_state;
+}
+
 static void cross_kv(Ctx& c, int B) {
   Model& m = *c.m;
   const int dt = m.d.n_text_state, Lt = m.d.n_text_layer;
   WMX_CHECK(m.d.n_audio_state == dt, "cross K/V: audio and text widths differ");
-  gemm(c, c.enc_out, dt, m.wckv, dt, B * 1500, Lt * 2 * dt, dt, epi(EPI_STORE16, m.bckv, c.ckv, (long)Lt * 2 * dt));
+  Epi e = epi(EPI_CROSSKV, m.bckv, c.ckv, 0);
+  e.d = dt;
+  e.xw = c.maxB;
+  e.xt = 1500;
+  gemm(c, c.enc_out, dt, m.wckv, dt, B * 1500, Lt * 2 * dt, dt, e);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -611,13 +662,79 @@ struct FwdArgs {
   bool align = false;
 };
 
+// Decode step (Tn == 1): every projection runs on packed weights with split-K partials, and the reductions are
+// fused into the consumers -- q/k/v into self attention (which also writes the KV cache), cross q into cross
+// attention, out-proj / fc2 into reduce_ln (residual add + the next LayerNorm).  10 launches per layer.
+// Leaves LN_final(x) of every row in c.dhb.
+static void dec_step_fast(Ctx& c, const FwdArgs& f) {
+  Model& m = *c.m;
+  const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
+  const int R = f.rows;
+  const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
+  launch_embed(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, 1, f.pad_seq, c.slot, dt, c.dx, c.st);
+  launch_layernorm(c.dt, c.dx, m.dec[0].ln1g, m.dec[0].ln1b, c.dhb, R, dt, c.st);
+  for (int l = 0; l < Lt; ++l) {
+    DecLayer& L = m.dec[l];
+    const bool last = l + 1 == Lt;
+    // self attention: QKV partials -> (reduce, cache write, attention) -> out-proj partials -> +x, LN2
+    int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt);
+    DecAttnArgs a{};
+    a.o = c.dao;
+    a.R = R;
+    a.Tn = 1;
+    a.H = H;
+    a.d = dt;
+    a.kc = c.kc + l * cache_layer;
+    a.vc = c.vc + l * cache_layer;
+    a.kv_R = c.R;
+    a.anc = f.anc;
+    a.anc_ld = c.Tctx;
+    a.pad = f.pad_seq;
+    a.slot0 = c.slot;
+    a.qpart = c.part;
+    a.qS = S;
+    a.qpart_stride = (long)R * 3 * dt;
+    a.qpart_ld = 3 * dt;
+    a.qbias = L.bqkv;
+    launch_self_attn(c.dt, a, c.st);
+    S = gemm_p_part(c, c.dao, dt, L.wo, R, dt, dt);
+    launch_reduce_ln(c.dt, c.part, S, L.bo, c.dx, L.ln2g, L.ln2b, c.dhb, R, dt, c.st);
+    // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3
+    S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
+    DecAttnArgs x{};
+    x.o = c.dao;
+    x.R = R;
+    x.Tn = 1;
+    x.H = H;
+    x.d = dt;
+    x.ck = cross_k(c, l);
+    x.cv = cross_v(c, l);
+    x.x_wstride = 1500L * dt;
+    x.x_hstride = 1500L * 64;
+    x.Tk = 1500;
+    x.rows_per_win = c.K;
+    x.qpart = c.part;
+    x.qS = S;
+    x.qpart_stride = (long)R * dt;
+    x.qpart_ld = dt;
+    x.qbias = L.bcq;
+    launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    S = gemm_p_part(c, c.dao, dt, L.wco, R, dt, dt);
+    launch_reduce_ln(c.dt, c.part, S, L.bco, c.dx, L.ln3g, L.ln3b, c.dhb, R, dt, c.st);
+    // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
+    gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
+    S = gemm_p_part(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt);
+    launch_reduce_ln(c.dt, c.part, S, L.bfc2, c.dx, last ? m.lng : m.dec[l + 1].ln1g, last ? m.lnb : m.dec[l + 1].ln1b,
+                     c.dhb, R, dt, c.st);
+  }
+}
+
 static void dec_forward(Ctx& c, const FwdArgs& f) {
   Model& m = *c.m;
   const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
   const int rowsT = f.rows * f.Tn;
   WMX_CHECK(rowsT <= c.dec_rows_max, "decoder: too many rows");
   launch_embed(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, f.rows, f.Tn, f.pad_seq, c.slot, dt, c.dx, c.st);
-  const long ck_ld = (long)Lt * 2 * dt;
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
@@ -632,7 +749,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
     eq.slot0 = c.slot;
     eq.kc = kcl;
     eq.vc = vcl;
-    gemm(c, c.dhb, dt, L.wqkv, dt, rowsT, 3 * dt, dt, eq);
+    gemm_p(c, c.dhb, dt, L.wqkv, rowsT, 3 * dt, dt, eq);
     if (f.prefill) {
       AttnArgs a{};
       a.q = c.dq;
@@ -662,25 +779,28 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.d = dt;
       a.kc = kcl;
       a.vc = vcl;
+      a.kv_R = c.R;
       a.anc = f.anc;
       a.anc_ld = c.Tctx;
       a.pad = f.pad_seq;
       a.slot0 = c.slot;
       launch_self_attn(c.dt, a, c.st);
     }
-    gemm(c, c.dao, dt, L.wo, dt, rowsT, dt, dt, epi(EPI_RESID32, L.bo, c.dx, dt));
+    gemm_p(c, c.dao, dt, L.wo, rowsT, dt, dt, epi(EPI_RESID32, L.bo, c.dx, dt));
     launch_layernorm(c.dt, c.dx, L.ln2g, L.ln2b, c.dhb, rowsT, dt, c.st);
-    gemm(c, c.dhb, dt, L.wcq, dt, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt));
-    const uint16_t* ckl = c.ckv + (size_t)l * 2 * dt;
+    gemm_p(c, c.dhb, dt, L.wcq, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt));
+    const uint16_t* ckl = cross_k(c, l);
+    const uint16_t* cvl = cross_v(c, l);
     if (f.prefill) {
       AttnArgs a{};
       a.q = c.dcq;
       a.q_ld = dt;
       a.q_bstride = (long)f.Tn * dt;
       a.k = ckl;
-      a.v = ckl + dt;
-      a.k_ld = a.v_ld = ck_ld;
-      a.k_bstride = a.v_bstride = 1500L * ck_ld;
+      a.v = cvl;
+      a.k_ld = a.v_ld = 64;
+      a.k_bstride = a.v_bstride = 1500L * dt;
+      a.kv_head_stride = 1500L * 64;
       a.o = c.dao;
       a.o_ld = dt;
       a.o_bstride = (long)f.Tn * dt;
@@ -700,7 +820,9 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.H = H;
       a.d = dt;
       a.ck = ckl;
-      a.ck_ld = ck_ld;
+      a.cv = cvl;
+      a.x_wstride = 1500L * dt;
+      a.x_hstride = 1500L * 64;
       a.Tk = 1500;
       a.rows_per_win = c.K;
       launch_cross_attn(c.dt, a, c.xa_ws, c.st);
@@ -720,7 +842,9 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         a.H = H;
         a.d = dt;
         a.ck = ckl;
-        a.ck_ld = ck_ld;
+        a.cv = cvl;
+        a.x_wstride = 1500L * dt;
+        a.x_hstride = 1500L * 64;
         a.Tk = 1500;
         a.rows_per_win = 1;
         launch_cross_scores(c.dt, a, c.a_heads, (int)hs.size(), c.scores, c.st);
@@ -730,20 +854,21 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         sync(c);
       }
     }
-    gemm(c, c.dao, dt, L.wco, dt, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt));
+    gemm_p(c, c.dao, dt, L.wco, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt));
     launch_layernorm(c.dt, c.dx, L.ln3g, L.ln3b, c.dhb, rowsT, dt, c.st);
-    gemm(c, c.dhb, dt, L.wfc1, dt, rowsT, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
-    gemm(c, c.df1, 4 * dt, L.wfc2, 4 * dt, rowsT, dt, 4 * dt, epi(EPI_RESID32, L.bfc2, c.dx, dt));
+    gemm_p(c, c.dhb, dt, L.wfc1, rowsT, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
+    gemm_p(c, c.df1, 4 * dt, L.wfc2, rowsT, dt, 4 * dt, epi(EPI_RESID32, L.bfc2, c.dx, dt));
   }
 }
 
 // final LN of selected rows + logits GEMM into c.logits [n][V]
-static void dec_logits(Ctx& c, const int* rows_idx, int n) {
+// (ln_done: c.dhb already holds LN_final of rows 0..n-1, as dec_step_fast leaves it)
+static void dec_logits(Ctx& c, const int* rows_idx, int n, bool ln_done = false) {
   Model& m = *c.m;
   const int dt = m.d.n_text_state, V = m.d.n_vocab;
   WMX_CHECK(n <= c.logits_rows, "logits: too many rows");
-  launch_layernorm_rows(c.dt, c.dx, rows_idx, m.lng, m.lnb, c.dhb, n, dt, c.st);
-  gemm(c, c.dhb, dt, m.tok_emb, dt, n, V, dt, epi(EPI_STORE32, nullptr, c.logits, V));
+  if (!ln_done) launch_layernorm_rows(c.dt, c.dx, rows_idx, m.lng, m.lnb, c.dhb, n, dt, c.st);
+  gemm_p(c, c.dhb, dt, m.tok_emb, n, V, dt, epi(EPI_STORE32, nullptr, c.logits, V));
 }
 
 static void set_slot(Ctx& c, int v) {
@@ -836,8 +961,8 @@ static void run_step(Ctx& c, int B) {
   f.pad_seq = c.pad_row;
   f.prefill = false;
   f.anc = c.K > 1 ? c.anc : nullptr;
-  dec_forward(c, f);
-  dec_logits(c, nullptr, f.rows);
+  dec_step_fast(c, f);
+  dec_logits(c, nullptr, f.rows, true);
   RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
               c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
   launch_logits_select(c.logits, m.d.n_vocab, ro, c.rp, f.rows, c.K + (c.K > 1 ? 1 : 0), c.ctok, c.clp, nullptr,
@@ -1320,6 +1445,13 @@ wmx_status wmx_model_set_tensor(wmx_model* w, const char* name, const float* dat
         h[o * e.Kp + (long)kk * e.C + c] = m.dt == DT::BF16 ? host_f32_to_bf16(data[i]) : host_f32_to_f16(data[i]);
       }
       WMX_HIP(hipMemcpy(e.dst, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    } else if (e.kind == 2) {
+      std::vector<uint16_t> h((size_t)(e.O + 15) / 16 * 16 * e.Kp, 0);
+      for (long i = 0; i < n; ++i)
+        h[packed_index(i / e.Kp, i % e.Kp, e.Kp)] =
+            m.dt == DT::BF16 ? host_f32_to_bf16(data[i]) : host_f32_to_f16(data[i]);
+      // sub-matrices of fused weights have row counts that are multiples of 16, so h covers exactly their rows
+      WMX_HIP(hipMemcpy(e.dst, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     } else {
       std::vector<uint16_t> h(n);
       for (long i = 0; i < n; ++i) h[i] = m.dt == DT::BF16 ? host_f32_to_bf16(data[i]) : host_f32_to_f16(data[i]);
@@ -1343,7 +1475,7 @@ wmx_status wmx_model_get_tensor(wmx_model* w, const char* name, float* out, int6
       WMX_HIP(hipMemcpy(out, e.dst, n * 4, hipMemcpyDeviceToHost));
       return;
     }
-    const long dn = e.kind == 1 ? (long)e.O * e.Kp : n;
+    const long dn = e.kind == 1 ? (long)e.O * e.Kp : (e.kind == 2 ? (long)(e.O + 15) / 16 * 16 * e.Kp : n);
     std::vector<uint16_t> h(dn);
     WMX_HIP(hipMemcpy(h.data(), e.dst, dn * 2, hipMemcpyDeviceToHost));
     for (long i = 0; i < n; ++i) {
@@ -1352,6 +1484,8 @@ wmx_status wmx_model_get_tensor(wmx_model* w, const char* name, float* out, int6
         const int kk = (int)(i % 3), c = (int)((i / 3) % e.C);
         const long o = i / 3 / e.C;
         di = o * e.Kp + (long)kk * e.C + c;
+      } else if (e.kind == 2) {
+        di = packed_index(i / e.Kp, i % e.Kp, e.Kp);
       }
       out[i] = m.dt == DT::BF16 ? host_bf16_to_f32(h[di]) : host_f16_to_f32(h[di]);
     }
@@ -1599,7 +1733,6 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
     WMX_CHECK(B >= 1 && B <= c.maxB && iters >= 1, "bench_kernel: args");
     WMX_HIP(hipSetDevice(m.device));
     const int da = m.d.n_audio_state, dt = m.d.n_text_state, Lt = m.d.n_text_layer, H = m.d.n_text_head;
-    const long ck_ld = (long)Lt * 2 * dt;
     const int R = c.K * B;
     double by = 0, fl = 0;
     std::function<void()> fn;
@@ -1612,8 +1745,10 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.Tn = 1;
       a.H = H;
       a.d = dt;
-      a.ck = c.ckv;
-      a.ck_ld = ck_ld;
+      a.ck = cross_k(c, 0);
+      a.cv = cross_v(c, 0);
+      a.x_wstride = 1500L * dt;
+      a.x_hstride = 1500L * 64;
       a.Tk = 1500;
       a.rows_per_win = c.K;
       by = (double)B * 1500 * 2 * dt * 2 + 2.0 * R * dt * 2;
@@ -1657,7 +1792,7 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       by = 4.0 * dt * dt * 2 + (double)R * dt * 2 + (double)R * 4 * dt * 2;
       fl = 2.0 * R * 4 * dt * dt;
       fn = [&c, &m, R, dt] {
-        gemm(c, c.dhb, dt, m.dec[0].wfc1, dt, R, 4 * dt, dt, epi(EPI_GELU16, m.dec[0].bfc1, c.df1, 4 * dt));
+        gemm_p(c, c.dhb, dt, m.dec[0].wfc1, R, 4 * dt, dt, epi(EPI_GELU16, m.dec[0].bfc1, c.df1, 4 * dt));
       };
     } else if (kernel == 5) {
       DecAttnArgs a{};
@@ -1670,6 +1805,7 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.d = dt;
       a.kc = c.kc;
       a.vc = c.vc;
+      a.kv_R = c.R;
       a.anc = c.K > 1 ? c.anc : nullptr;
       a.anc_ld = c.Tctx;
       a.pad = c.pad_row;

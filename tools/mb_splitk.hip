@@ -7,7 +7,7 @@
 using namespace wmx;
 
 // KSPLIT: the 4 waves of a workgroup split its K chunk (LDS reduce); otherwise they own 4 different column groups.
-template <int MT, int NCT, int KU, bool KSPLIT>
+template <int MT, int NCT, int KU, bool KSPLIT, int VAR = 0>
 __global__ __launch_bounds__(256) void part(const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ W,
                                             int ldw, int M, int N, int K, int S, float* __restrict__ P) {
   __shared__ float red[KSPLIT ? 4 : 1][KSPLIT ? MT * 16 : 1][KSPLIT ? 16 * NCT + 1 : 1];
@@ -31,9 +31,15 @@ __global__ __launch_bounds__(256) void part(const uint16_t* __restrict__ A, int 
   const uint16_t* wrow[NCT];
 #pragma unroll
   for (int j = 0; j < NCT; ++j) wrow[j] = W + (long)min(n0 + j * 16 + fr, N - 1) * ldw + 8 * fq;
-  const uint16_t* arow[MT];
+  // VAR 1: fragment-major W: tile (n/16, k/32) is one contiguous 1 KiB, lane-linear
+  const int ksteps_all = K / 32;
+  const uint16_t* wtile[NCT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) arow[i] = A + (long)min(i * 16 + fr, M - 1) * lda + 8 * fq;
+  for (int j = 0; j < NCT; ++j) wtile[j] = W + ((long)min((n0 + j * 16) / 16, (N - 1) / 16) * ksteps_all) * 512 + lane * 8;
+  const uint16_t* arow[MT];
+  const uint16_t* Ab = VAR == 2 ? A + (long)(blockIdx.x % 64) * 64 * lda : A;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) arow[i] = Ab + (long)min(i * 16 + fr, M - 1) * lda + 8 * fq;
   for (int kk = ks0; kk < ks1; kk += KU) {
     u16x8 b[KU][NCT], av[KU][MT];
 #pragma unroll
@@ -41,9 +47,12 @@ __global__ __launch_bounds__(256) void part(const uint16_t* __restrict__ A, int 
       if (kk + u < ks1) {
         const int k = (kk + u) * 32;
 #pragma unroll
-        for (int j = 0; j < NCT; ++j) b[u][j] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wrow[j] + k));
+        for (int j = 0; j < NCT; ++j)
+          b[u][j] = VAR == 1 ? *reinterpret_cast<const u16x8*>(wtile[j] + (long)(kk + u) * 512)
+                             : *reinterpret_cast<const u16x8*>(wrow[j] + k);
 #pragma unroll
-        for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(arow[i] + k);
+        for (int i = 0; i < MT; ++i)
+          av[u][i] = VAR == 3 ? u16x8{(uint16_t)k, 1, 2, 3, 4, 5, 6, (uint16_t)i} : *reinterpret_cast<const u16x8*>(arow[i] + k);
       }
     }
 #pragma unroll
@@ -53,6 +62,15 @@ __global__ __launch_bounds__(256) void part(const uint16_t* __restrict__ A, int 
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int j = 0; j < NCT; ++j) acc[i][j] = mfma16<DT::BF16>(av[u][i], b[u][j], acc[i][j]);
+  }
+  if (VAR == 4) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == 1234.5f) P[tid] = t;
+    return;
   }
   if (KSPLIT) {
 #pragma unroll
@@ -119,49 +137,44 @@ float* P;
 hipStream_t st;
 long wstride = 0;
 
-template <int MT, int NCT, int KU, bool KSPLIT>
+template <int MT, int NCT, int KU, bool KSPLIT, int VAR = 0>
 void run(int M, int N, int K, int S) {
   int it = 0;
   const int cols = KSPLIT ? 16 * NCT : 64 * NCT;
   const int tiles = (N + cols - 1) / cols;
   float us_p = timeit([&] {
     const uint16_t* w = W + (it++ % 8) * wstride;
-    hipLaunchKernelGGL((part<MT, NCT, KU, KSPLIT>), dim3(tiles, S), dim3(256), 0, st, A, K, w, K, M, N, K, S, P);
+    hipLaunchKernelGGL((part<MT, NCT, KU, KSPLIT, VAR>), dim3(tiles, S), dim3(256), 0, st, A, K, w, K, M, N, K, S, P);
   }, st);
-  const int rb = (int)(((long)M * N / 4 + 255) / 256);
-  float us_r = timeit([&] { hipLaunchKernelGGL(reduce, dim3(rb), dim3(256), 0, st, P, S, M, N, O); }, st);
-  printf("M=%3d N=%5d K=%4d MT=%2d NCT=%d KU=%d %s S=%3d WG=%6d: part %7.2f us (%6.0f GB/s) reduce %6.2f us\n", M,
-         N, K, MT, NCT, KU, KSPLIT ? "ksplit" : "nsplit", S, tiles * S, us_p, 2.0 * N * K / us_p / 1e3, us_r);
+  printf("M=%3d N=%5d K=%4d MT=%2d NCT=%d KU=%d %s S=%3d WG=%6d VAR=%d: part %7.2f us (%6.0f GB/s)\n", M, N, K, MT,
+         NCT, KU, KSPLIT ? "ksplit" : "nsplit", S, tiles * S, VAR, us_p, 2.0 * N * K / us_p / 1e3);
 }
 
 int main() {
   hipStreamCreate(&st);
   wstride = 51866L * 1280 + 4096;
-  hipMalloc(&A, 256L * 5120 * 2);
+  hipMalloc(&A, 64L * 64 * 5120 * 2);
   hipMalloc(&W, 8 * wstride * 2);
   hipMalloc(&O, 256L * 51866 * 2);
   hipMalloc(&P, 64L * 256 * 5120 * 4);
-  hipMemset(A, 0, 256L * 5120 * 2);
+  hipMemset(A, 0, 64L * 64 * 5120 * 2);
   hipMemset(W, 0x11, 8 * wstride * 2);
-  const int shapes[5][2] = {{1280, 1280}, {3840, 1280}, {5120, 1280}, {1280, 5120}, {51866, 1280}};
-  for (auto& sh : shapes) {
-    const int N = sh[0], K = sh[1];
-    for (int S : {1, 2, 4, 8, 10, 20}) {
-      if (K / 32 < S * 2) continue;
-      if ((long)S * 40 * N > 64L * 256 * 5120) continue;
-      if (N > 6000 && S > 2) continue;
-      run<3, 1, 2, true>(40, N, K, S);
-      run<3, 2, 2, true>(40, N, K, S);
-      run<3, 4, 2, true>(40, N, K, S);
-      run<3, 1, 4, false>(40, N, K, S);
-      run<3, 2, 4, false>(40, N, K, S);
-      run<3, 4, 2, false>(40, N, K, S);
-    }
-  }
-  for (int S : {1, 4, 10}) run<10, 2, 1, false>(160, 1280, 1280, S);
-  for (int S : {1, 4, 10}) run<10, 2, 1, false>(160, 1280, 5120, S * 2);
-  for (int S : {1, 4, 10}) run<10, 1, 1, true>(160, 1280, 5120, S * 2);
-  for (int S : {1, 2}) run<10, 2, 1, false>(160, 51866, 1280, S);
-  for (int S : {1, 2}) run<10, 4, 1, false>(160, 51866, 1280, S);
+#define SWEEP(MT, NCT, KU, M, N, K, S) \
+  run<MT, NCT, KU, true, 0>(M, N, K, S);  \
+  run<MT, NCT, KU, true, 1>(M, N, K, S);  \
+  run<MT, NCT, KU, true, 2>(M, N, K, S);  \
+  run<MT, NCT, KU, true, 3>(M, N, K, S);  \
+  run<MT, NCT, KU, true, 4>(M, N, K, S);
+  SWEEP(3, 2, 2, 40, 1280, 1280, 10)
+  SWEEP(3, 1, 2, 40, 1280, 1280, 10)
+  SWEEP(3, 2, 2, 40, 3840, 1280, 4)
+  SWEEP(3, 2, 2, 40, 5120, 1280, 4)
+  SWEEP(3, 2, 2, 40, 5120, 1280, 1)
+  SWEEP(3, 4, 2, 40, 1280, 5120, 10)
+  SWEEP(3, 2, 2, 40, 1280, 5120, 20)
+  SWEEP(3, 4, 2, 40, 51866, 1280, 1)
+  SWEEP(3, 8, 1, 40, 51866, 1280, 1)
+  SWEEP(1, 4, 4, 8, 1280, 1280, 10)
+  SWEEP(1, 8, 2, 8, 51866, 1280, 1)
   return 0;
 }
