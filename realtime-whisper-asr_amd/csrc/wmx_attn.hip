@@ -322,59 +322,70 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// decoder cross attention for a decode step: workgroup = (head, window, key chunk of CHUNK keys); the nq =
-// rows_per_win * Tn <= 8 query rows of a window share the window's K/V stream, which is read exactly once.
+// decoder cross attention (decode step and prefill): workgroup = (head, window, key chunk x 16-query tile).
+// The nq = rows_per_win * Tn query rows of a window share its K / V^T stream.
+//
+// Per wave, per 32-key block kb: S^T = K.Q^T on MFMA with the block's keys permuted so that lane (q = l&15,
+// g = l>>4) ends up holding the scores of keys kb + 8g + 0..7 for query q -- exactly the A-operand layout of
+// the following P.V MFMA (A = P[16 q][32 keys]).  B of P.V is V^T[dim][kb + 8g .. +8]: one contiguous 16-B
+// load per lane from the transposed V image.  Softmax statistics are per lane (q = l&15) plus two xor
+// shuffles across the four 16-lane groups; P goes to the MFMA as bf16/f16 hi + lo halves (two MFMAs), so
+// the probabilities keep ~16 mantissa bits.  No LDS until the 4-wave combine at the end.
+// KS > 1: each chunk writes a (max, sum, o[64]) record per query; dec_cross_combine merges them in order.
 // ------------------------------------------------------------------------------------------------
-constexpr int kMaxQ = 8, kMaxTk = 1536, kMaxSplits = 16;
+constexpr int kMaxTk = kXS, kMaxSplits = 16;
 
-// Q.K^T on MFMA: A = Q (16 query rows, nq valid) from registers, B = K^T straight from HBM (lane: key l&15,
-// 16 B of head dims, contiguous in the head-major cross-K/V layout).  Every K and V load of the chunk is issued
-// before any arithmetic.  Softmax in LDS, P.V on VALU (thread = key group x 8 dims, 16-B V loads).
-// KS > 1: each chunk writes its (max, sum, o[64]) record per query row; dec_cross_combine merges them in chunk
-// order (no atomics, no cross-workgroup fences inside the kernel).
-template <DT T, int CHUNK>
-__global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int KS, float* __restrict__ part) {
-  constexpr int VPRE = CHUNK / 32;      // V rows per thread (32 key groups x 8 dim chunks)
-  constexpr int NB = CHUNK / 16 / 4;    // 16-key blocks per wave
-  const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z;
+template <DT T, int KPW>
+__global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
+  const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z % KS, qt = blockIdx.z / KS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4;
   const int nq = a.rows_per_win * a.Tn;
-  const int m0 = w * nq;
-  const int k0 = ks * CHUNK, k1 = min(a.Tk, k0 + CHUNK);
-  const int nk = max(0, k1 - k0);
-  __shared__ float sc[kMaxQ][CHUNK + 4];
-  __shared__ float red[kMaxQ][4];
-  __shared__ float fin[4][kMaxQ][64];
+  const int i0 = qt * 16;  // first query (within the window) of this tile
+  const int nqt = min(16, nq - i0);
+  const int kc0 = ks * chunk, kc1 = min(a.Tk, kc0 + chunk);
+  const int per = ((kc1 - kc0 + 3) / 4 + 31) / 32 * 32;  // keys per wave, whole 32-key blocks
+  const int kw0 = kc0 + wave * per, kw1 = min(kc1, kw0 + per);
   const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
   const uint16_t* vbase = a.cv + (long)w * a.x_wstride + (long)h * a.x_hstride;
-  const int kg = tid >> 3, c = tid & 7;
-  const int fr = lane & 15, g = lane >> 4;
-  u16x8 vpre[VPRE];
+  const long m_row = (long)w * nq + i0 + fr;  // query row held by this lane's column
+  const bool q_ok = fr < nqt;
+
+  // ---- first batch of K / V^T loads (issued before the q reduction so their latency overlaps it) ----
+  // K A-fragment of block b, pair u, dim half hh: key kb + 8*(fr>>2) + 4u + (fr&3), dims 32hh + 8g .. +8
+  // V^T B-fragment of block b, dim block db: V^T[16db + fr][kb + 8g .. +8]
+  u16x8 kf[KPW][2][2], vf[KPW][4];
+  auto load_batch = [&](int kb0) {
 #pragma unroll
-  for (int i = 0; i < VPRE; ++i) {
-    const int t = min(kg + 32 * i, nk - 1);
-    vpre[i] = *reinterpret_cast<const u16x8*>(vbase + (long)(k0 + max(t, 0)) * 64 + c * 8);
-  }
-  const int nblk = (nk + 15) / 16;
-  u16x8 kb[NB][2];
+    for (int b = 0; b < KPW; ++b) {
+      const int kb = kb0 + 32 * b;
 #pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    const int key = min(k0 + (wave + 4 * u) * 16 + fr, a.Tk - 1);
+      for (int u = 0; u < 2; ++u) {
+        const int key = min(kb + 8 * (fr >> 2) + 4 * u + (fr & 3), kXS - 1);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) kb[u][s2] = *reinterpret_cast<const u16x8*>(kbase + (long)key * 64 + 32 * s2 + 8 * g);
-  }
-  // Q fragments: lane row q = lane & 15, dims 32s + 8(lane>>4) .. +8
-  u16x8 qa[2];
+        for (int hh = 0; hh < 2; ++hh)
+          kf[b][u][hh] = *reinterpret_cast<const u16x8*>(kbase + (long)key * 64 + 32 * hh + 8 * g);
+      }
+      const int kk = min(kb + 8 * g, kXS - 8);
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
+      for (int db = 0; db < 4; ++db)
+        vf[b][db] = *reinterpret_cast<const u16x8*>(vbase + (long)(16 * db + fr) * kXS + kk);
+    }
+  };
+  if (kw0 < kw1) load_batch(kw0);
+
+  // ---- Q^T B-fragments: lane (col q = fr, g): dims 32hh + 8g .. +8 ----
+  u16x8 qb[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
     u16x8 z = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (fr < nq) {
-      const int col = h * 64 + 32 * s2 + 8 * g;
+    if (q_ok) {
+      const int col = h * 64 + 32 * hh + 8 * g;
       if (a.qS > 0) {
         // q = bias + sum of the split-K partials (slice order), rounded to the model dtype like the stored path
         float p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        const float* src = a.qpart + (long)(m0 + fr) * a.qpart_ld + col;
-        for (int q0 = 0; q0 < a.qS; q0 += 4) {  // all loads of a batch in flight, slice order kept
+        const float* src = a.qpart + m_row * a.qpart_ld + col;
+        for (int q0 = 0; q0 < a.qS; q0 += 4) {
           float4 x0[4], x1[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -392,129 +403,129 @@ __global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int 
 #pragma unroll
         for (int e = 0; e < 8; ++e) z[e] = from_f32<T>(p[e] + (a.qbias ? a.qbias[col + e] : 0.f));
       } else {
-        z = *reinterpret_cast<const u16x8*>(a.q + (long)(m0 + fr) * a.q_ld + col);
+        z = *reinterpret_cast<const u16x8*>(a.q + m_row * a.q_ld + col);
       }
     }
-    qa[s2] = z;
+    qb[hh] = z;
   }
-  // ---- scores ----
+
+  // ---- online softmax over the wave's key range, P.V on MFMA ----
+  float m_run = -INFINITY, l_run = 0.f;  // statistics of query fr (replicated over g)
+  f32x4 o[4];
 #pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    const int blk = wave + 4 * u;
-    if (blk >= nblk) break;
-    f32x4 acc = f32x4{0, 0, 0, 0};
-    acc = mfma16<T>(qa[0], kb[u][0], acc);
-    acc = mfma16<T>(qa[1], kb[u][1], acc);
-    const int kl = blk * 16 + fr;  // lane holds S[q = 4g + r][key kl]
+  for (int db = 0; db < 4; ++db) o[db] = f32x4{0, 0, 0, 0};
+  for (int kb0 = kw0; kb0 < kw1; kb0 += 32 * KPW) {
+    if (kb0 != kw0) load_batch(kb0);  // (prefill only: decode chunks are one batch, loaded above)
+    float sv[KPW][8];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = 4 * g + r;
-      if (q < nq && kl < nk) sc[q][kl] = acc[r] * 0.125f;
-    }
-  }
-  __syncthreads();
-  // ---- softmax over this chunk ----
-  float mx[kMaxQ];
+    for (int b = 0; b < KPW; ++b) {
 #pragma unroll
-  for (int q = 0; q < kMaxQ; ++q) {
-    float v = -INFINITY;
-    if (q < nq)
-      for (int t = tid; t < nk; t += 256) v = fmaxf(v, sc[q][t]);
-    v = wave_max(v);
-    if (lane == 0) red[q][wave] = v;
-  }
-  __syncthreads();
+      for (int u = 0; u < 2; ++u) {
+        f32x4 acc = f32x4{0, 0, 0, 0};
+        acc = mfma16<T>(kf[b][u][0], qb[0], acc);
+        acc = mfma16<T>(kf[b][u][1], qb[1], acc);
 #pragma unroll
-  for (int q = 0; q < kMaxQ; ++q) mx[q] = fmaxf(fmaxf(red[q][0], red[q][1]), fmaxf(red[q][2], red[q][3]));
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < kMaxQ; ++q) {
-    float sum = 0.f;
-    if (q < nq)
-      for (int t = tid; t < nk; t += 256) {
-        const float e = __expf(sc[q][t] - mx[q]);
-        sc[q][t] = e;
-        sum += e;
-      }
-    sum = wave_sum(sum);
-    if (lane == 0) red[q][wave] = sum;
-  }
-  __syncthreads();
-  // ---- P.V from the prefetched V rows ----
-  float acc[kMaxQ][8];
-#pragma unroll
-  for (int q = 0; q < kMaxQ; ++q)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[q][e] = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPRE; ++i) {
-    const int t = kg + 32 * i;
-    if (t < nk) {
-      float vf[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) vf[e] = to_f32<T>(vpre[i][e]);
-#pragma unroll
-      for (int q = 0; q < kMaxQ; ++q) {
-        if (q < nq) {
-          const float p = sc[q][t];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[q][e] += p * vf[e];
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb0 + 32 * b + 8 * g + 4 * u + r;
+          sv[b][4 * u + r] = key < kw1 ? acc[r] * 0.125f : -INFINITY;
         }
       }
     }
-  }
+    float mx = -INFINITY;
 #pragma unroll
-  for (int q = 0; q < kMaxQ; ++q) {
-    if (q < nq) {
+    for (int b = 0; b < KPW; ++b)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = acc[q][e];
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        acc[q][e] = v;
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, sv[b][j]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __expf(m_run - m_new);  // 0 on the first batch (m_run = -inf)
+    float ls = 0.f;
+#pragma unroll
+    for (int b = 0; b < KPW; ++b)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = __expf(sv[b][j] - m_new);
+        sv[b][j] = e;
+        ls += e;
+      }
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+    // o rows are queries 4g + r: their alpha lives in lane (4g + r) of any group
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ar = __shfl(alpha, 4 * g + r);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db][r] *= ar;
+    }
+#pragma unroll
+    for (int b = 0; b < KPW; ++b) {
+      u16x8 phi, plo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint16_t hi = from_f32<T>(sv[b][j]);
+        phi[j] = hi;
+        plo[j] = from_f32<T>(sv[b][j] - to_f32<T>(hi));
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        o[db] = mfma16<T>(phi, vf[b][db], o[db]);
+        o[db] = mfma16<T>(plo, vf[b][db], o[db]);
       }
     }
   }
-  if (lane < 8) {
-#pragma unroll
-    for (int q = 0; q < kMaxQ; ++q)
-      if (q < nq)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) fin[wave][q][c * 8 + e] = acc[q][e];
+
+  // ---- combine the 4 waves (LDS), then output or a chunk record ----
+  __shared__ float sm[4][16], sl[4][16];
+  __shared__ float so[4][16][65];
+  if (g == 0) {
+    sm[wave][fr] = m_run;
+    sl[wave][fr] = l_run;
   }
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) so[wave][4 * g + r][16 * db + fr] = o[db][r];
   __syncthreads();
-  for (int t = tid; t < nq * 64; t += 256) {
+  for (int t = tid; t < nqt * 64; t += 256) {
     const int q = t >> 6, e = t & 63;
-    const float tot = red[q][0] + red[q][1] + red[q][2] + red[q][3];
-    const float o = fin[0][q][e] + fin[1][q][e] + fin[2][q][e] + fin[3][q][e];
+    float M = fmaxf(fmaxf(sm[0][q], sm[1][q]), fmaxf(sm[2][q], sm[3][q]));
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) {
+      const float f = sm[wv][q] == -INFINITY ? 0.f : __expf(sm[wv][q] - M);
+      L += sl[wv][q] * f;
+      O += so[wv][q][e] * f;
+    }
+    const long row = (long)w * nq + i0 + q;
     if (KS == 1) {
-      a.o[(long)(m0 + q) * a.d + h * 64 + e] = from_f32<T>(o / tot);
+      a.o[row * a.d + h * 64 + e] = from_f32<T>(O / L);
     } else {
-      // record per (window, head, chunk, q): [max, sum, o[64]]
-      float* pr = part + ((((long)w * a.H + h) * KS + ks) * kMaxQ + q) * 66;
+      float* pr = part + (((long)(w * a.H + h) * KS + ks) * nq + i0 + q) * 66;
       if (e == 0) {
-        pr[0] = mx[q];
-        pr[1] = tot;
+        pr[0] = M;
+        pr[1] = L;
       }
-      pr[2 + e] = o;
+      pr[2 + e] = O;
     }
   }
 }
 
-// merge the KS chunk records of every (window, head, q) in chunk order: o = sum_k o_k e^{m_k - M} / sum_k l_k e^{m_k - M}
+// merge the KS chunk records of every (window, head, q) in chunk order (records: cross_attn_ws_floats(H, nwin, 16))
 template <DT T>
 __global__ __launch_bounds__(256) void dec_cross_combine_kernel(const float* __restrict__ part, int KS, int H, int nq,
                                                                 int d, uint16_t* __restrict__ out) {
   const int w = blockIdx.x, h = blockIdx.y;
   for (int t = threadIdx.x; t < nq * 64; t += 256) {
     const int q = t >> 6, e = t & 63;
-    const float* pr = part + (((long)w * H + h) * KS * kMaxQ + q) * 66;
+    const float* pr = part + ((long)(w * H + h) * KS * nq + q) * 66;
     float rec[kMaxSplits][3];
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
-        const float* x = pr + (long)k * kMaxQ * 66;
+        const float* x = pr + (long)k * nq * 66;
         rec[k][0] = x[0];
         rec[k][1] = x[1];
         rec[k][2] = x[2 + e];
@@ -528,7 +539,7 @@ __global__ __launch_bounds__(256) void dec_cross_combine_kernel(const float* __r
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
-        const float sc2 = __expf(rec[k][0] - M);
+        const float sc2 = rec[k][0] == -INFINITY ? 0.f : __expf(rec[k][0] - M);
         l += rec[k][1] * sc2;
         o += rec[k][2] * sc2;
       }
@@ -537,42 +548,42 @@ __global__ __launch_bounds__(256) void dec_cross_combine_kernel(const float* __r
   }
 }
 
-// keys per workgroup; WMX_CROSS_CHUNK (128 / 256 / 384) overrides the default for tuning runs
-static int cross_chunk(int Tk) {
+// key chunk per workgroup; WMX_CROSS_CHUNK overrides the default for tuning runs
+static int cross_chunk(int Tk, int nq) {
   static const int env = [] {
     const char* v = getenv("WMX_CROSS_CHUNK");
     return v ? atoi(v) : 0;
   }();
+  if (nq > 16) return Tk;  // prefill: many query tiles already fill the chip
   if (env) return env;
-  return Tk > 768 ? 256 : 128;
+  return 256;
 }
 
-int cross_attn_splits(int Tk) { return (Tk + cross_chunk(Tk) - 1) / cross_chunk(Tk); }
-
-size_t cross_attn_ws_floats(int H, int nwin) { return (size_t)nwin * H * kMaxSplits * kMaxQ * 66; }
+size_t cross_attn_ws_floats(int H, int nwin, int nq_max) { return (size_t)nwin * H * kMaxSplits * nq_max * 66; }
 
 template <DT T>
 static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
   const int nq = a.rows_per_win * a.Tn;
   const int nwin = a.R / a.rows_per_win;
-  const int chunk = cross_chunk(a.Tk);
+  const int chunk = std::min(cross_chunk(a.Tk, nq), a.Tk);
   const int KS = (a.Tk + chunk - 1) / chunk;
+  const int QT = (nq + 15) / 16;
   WMX_CHECK(KS <= kMaxSplits, "cross attn: too many key chunks");
-  WMX_CHECK(KS == 1 || ws != nullptr, "cross attn: split workspace required");
-  dim3 grid(a.H, nwin, KS);
-  switch (chunk) {
-    case 128: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 128>), grid, dim3(256), 0, st, a, KS, ws); break;
-    case 256: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 256>), grid, dim3(256), 0, st, a, KS, ws); break;
-    case 384: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 384>), grid, dim3(256), 0, st, a, KS, ws); break;
-    default: WMX_CHECK(false, "cross attn: unsupported key chunk");
+  WMX_CHECK(KS == 1 || (ws != nullptr && nq <= 16), "cross attn: split workspace required");
+  dim3 grid(a.H, nwin, KS * QT);
+  const int per_wave = ((chunk + 3) / 4 + 31) / 32;  // 32-key blocks per wave
+  switch (std::min(per_wave, 4)) {
+    case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
   }
   if (KS > 1)
     hipLaunchKernelGGL(dec_cross_combine_kernel<T>, dim3(nwin, a.H), dim3(256), 0, st, ws, KS, a.H, nq, a.d, a.o);
 }
 
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {
-  const int nq = a.rows_per_win * a.Tn;
-  WMX_CHECK(nq <= kMaxQ && a.Tk <= kMaxTk, "cross attn: too many queries per window");
+  WMX_CHECK(a.Tk <= 1500 && a.d == a.H * 64, "cross attn: shape");
   if (dt == DT::BF16)
     launch_cross_t<DT::BF16>(a, ws, st);
   else

@@ -15,12 +15,13 @@
 
 namespace wmx {
 
-// [L][K|V][xw][H][xt][64]: each (window, head) key range is one contiguous stream for the decode step
+// K: [L][xw][H][kXS][64] (key rows), V: [L][xw][H][64][kXS] (V^T, key-contiguous): each (window, head) is one
+// contiguous stream for the decode step, and V^T rows are the MFMA B operand of P.V without a transpose
 __device__ inline long crosskv_index(const Epi& e, int m, int n) {
   const int w = m / e.xt, t = m - w * e.xt;
   const int lk = n / e.d, c = n - lk * e.d;
-  const int h = c >> 6;
-  return ((((long)lk * e.xw + w) * (e.d >> 6) + h) * e.xt + t) * 64 + (c & 63);
+  const long base = (((long)lk * e.xw + w) * (e.d >> 6) + (c >> 6)) * 64 * kXS;
+  return (lk & 1) ? base + (long)(c & 63) * kXS + t : base + (long)t * 64 + (c & 63);
 }
 
 template <DT T>
@@ -116,8 +117,16 @@ __device__ inline void epi_store4(const Epi& e, int m, int n, float4 v) {
       break;
     }
     case EPI_CROSSKV: {
-      u16x4 h = {from_f32<T>(v.x), from_f32<T>(v.y), from_f32<T>(v.z), from_f32<T>(v.w)};
-      *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)) = h;
+      uint16_t* o = reinterpret_cast<uint16_t*>(e.out);
+      if (((n / e.d) & 1) == 0) {
+        u16x4 h = {from_f32<T>(v.x), from_f32<T>(v.y), from_f32<T>(v.z), from_f32<T>(v.w)};
+        *reinterpret_cast<u16x4*>(o + crosskv_index(e, m, n)) = h;
+      } else {  // V^T: the 4 columns are 4 rows of the transposed image
+        o[crosskv_index(e, m, n)] = from_f32<T>(v.x);
+        o[crosskv_index(e, m, n + 1)] = from_f32<T>(v.y);
+        o[crosskv_index(e, m, n + 2)] = from_f32<T>(v.z);
+        o[crosskv_index(e, m, n + 3)] = from_f32<T>(v.w);
+      }
       break;
     }
     default:
@@ -236,6 +245,21 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
           for (int r = 0; r < 4; ++r) img[(i * 16 + fq * 4 + r) * LDT + wn * (BN / WN) + j * 16 + fr] = acc[i][j][r];
     }
     __syncthreads();
+    if (e.kind == EPI_CROSSKV && !ws && ((n0 / e.d) & 1)) {
+      // V^T tile (the host checks d % BN == 0, xt % 4 == 0): 4 consecutive keys of one column per 8-byte store
+      for (int idx = tid; idx < RR / 4 * BN; idx += NW * 64) {
+        const int col = idx % BN, r4 = (idx / BN) * 4;
+        const int m = m0 + rd * RR + r4, n = n0 + col;
+        if (m >= M || n >= N) continue;
+        const float b = e.bias ? e.bias[n] : 0.f;
+        u16x4 h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) h[q] = from_f32<T>(img[(r4 + q) * LDT + col] + b);
+        *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)) = h;
+      }
+      __syncthreads();
+      continue;
+    }
     for (int idx = tid; idx < RR * BN / 4; idx += NW * 64) {
       const int row = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
       const int m = m0 + rd * RR + row, n = n0 + c4;

@@ -11,7 +11,7 @@ enum EpiKind {
   EPI_GELU_POS32 = 3,  // out32 = gelu(acc + bias) + pos[m % posT]   (encoder conv2)
   EPI_STORE32 = 4,     // out32 = acc (+ bias)          (logits)
   EPI_QKV_CACHE = 5,   // decoder self-attn: q -> out16, k/v -> KV cache at slot *slot0 + (m % Tn)
-  EPI_CROSSKV = 6,     // cross K/V of all decoder layers -> head-major [L][K|V][xw][H][xt][64] (16-bit)
+  EPI_CROSSKV = 6,     // cross K/V of all decoder layers, head-major: K [L][xw][H][kXS][64], V^T [L][xw][H][64][kXS]
 };
 
 struct Epi {
@@ -29,6 +29,9 @@ struct Epi {
   // EPI_CROSSKV: row m = w * xt + t, column n = (l * 2 + kv) * d + h * 64 + e
   int xw = 1, xt = 1500;
 };
+
+// padded key stride of the cross K/V images (a multiple of 32 keys; the pad stays zero)
+constexpr int kXS = 1504;
 
 enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3 };
 
@@ -133,7 +136,8 @@ struct DecAttnArgs {
   const int* slot0;    // device scalar: slot of the first new token
   int kv_R;            // row stride of the KV cache ([slot][kv_R][d]); >= R
   // cross
-  // cross K/V of one layer, head-major: key t of (window w, head h) at ck + w*x_wstride + h*x_hstride + t*64
+  // cross K/V of one layer, head-major: K[t][e] of (window w, head h) at ck + w*x_wstride + h*x_hstride + t*64,
+  // V^T[e][t] at cv + w*x_wstride + h*x_hstride + e*kXS + t
   const uint16_t* ck;
   const uint16_t* cv;
   long x_wstride, x_hstride;
@@ -148,8 +152,8 @@ struct DecAttnArgs {
   int win_of_row_div;  // row -> window = row / rows_per_win
 };
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);
-// ws: cross_attn_ws_floats(H, nwin) floats for the key-split partials (nullptr = no split)
-size_t cross_attn_ws_floats(int H, int nwin);
+// ws: cross_attn_ws_floats(H, nwin, nq_max) floats for the key-chunk records (decode steps)
+size_t cross_attn_ws_floats(int H, int nwin, int nq_max);
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st);
 // raw cross-attention scores of selected heads (alignment): out [nh][R*Tn][Tk] f32
 void launch_cross_scores(DT dt, const DecAttnArgs& a, const int* heads_layer_local, int nh, float* out, hipStream_t st);

@@ -428,7 +428,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.eao, (size_t)B * 1500 * da);
   P.add(&c.ef1, (size_t)B * 1500 * 4 * da);
   P.add(&c.enc_out, (size_t)B * 1500 * da);
-  P.add(&c.ckv, (size_t)B * 1500 * Lt * 2 * dt);
+  P.add(&c.ckv, (size_t)B * kXS * Lt * 2 * dt);  // K and V^T images, key stride kXS (pad stays zero)
   const int DR = c.dec_rows_max;
   P.add(&c.dx, (size_t)DR * dt);
   P.add(&c.dhb, (size_t)DR * dt);
@@ -479,7 +479,8 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.ctok, (size_t)R * 9);
   P.add(&c.clp, (size_t)R * 9);
   P.add(&c.sel_ws, logits_select_ws_floats(R, 9));
-  P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B));
+  // key-chunk records: chunked launches have <= 16 queries per window (more use one chunk, no records)
+  P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
   P.add(&c.align_scratch, (size_t)B * T * 1500);
@@ -629,10 +630,10 @@ static void encode(Ctx& c, int B) {
 
 // layer l's cross K / V in the head-major layout written by EPI_CROSSKV
 static const uint16_t* cross_k(const Ctx& c, int l) {
-  return c.ckv + (size_t)(2 * l) * c.maxB * 1500 * c.m->d.n_text_state;
+  return c.ckv + (size_t)(2 * l) * c.maxB * kXS * c.m->d.n_text_state;
 }
 static const uint16_t* cross_v(const Ctx& c, int l) {
-  return c.ckv + (size_t)(2 * l + 1) * c.maxB * 1500 * c.m->d.n_text_state;
+  return c.ckv + (size_t)(2 * l + 1) * c.maxB * kXS * c.m->d.n_text_state;
 }
 
 static void cross_kv(Ctx& c, int B) {
@@ -709,8 +710,8 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.d = dt;
     x.ck = cross_k(c, l);
     x.cv = cross_v(c, l);
-    x.x_wstride = 1500L * dt;
-    x.x_hstride = 1500L * 64;
+    x.x_wstride = (long)kXS * dt;
+    x.x_hstride = (long)kXS * 64;
     x.Tk = 1500;
     x.rows_per_win = c.K;
     x.qpart = c.part;
@@ -791,40 +792,22 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
     gemm_p(c, c.dhb, dt, L.wcq, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt));
     const uint16_t* ckl = cross_k(c, l);
     const uint16_t* cvl = cross_v(c, l);
-    if (f.prefill) {
-      AttnArgs a{};
-      a.q = c.dcq;
-      a.q_ld = dt;
-      a.q_bstride = (long)f.Tn * dt;
-      a.k = ckl;
-      a.v = cvl;
-      a.k_ld = a.v_ld = 64;
-      a.k_bstride = a.v_bstride = 1500L * dt;
-      a.kv_head_stride = 1500L * 64;
-      a.o = c.dao;
-      a.o_ld = dt;
-      a.o_bstride = (long)f.Tn * dt;
-      a.B = f.rows;
-      a.H = H;
-      a.Tq = f.Tn;
-      a.Tk = 1500;
-      a.head_stride = 64;
-      launch_attn_flash(c.dt, a, 0, 0, nullptr, c.st);
-    } else {
+    {
       DecAttnArgs a{};
       a.q = c.dcq;
       a.q_ld = dt;
       a.o = c.dao;
       a.R = f.rows;
-      a.Tn = 1;
+      a.Tn = f.Tn;
       a.H = H;
       a.d = dt;
       a.ck = ckl;
       a.cv = cvl;
-      a.x_wstride = 1500L * dt;
-      a.x_hstride = 1500L * 64;
+      a.x_wstride = (long)kXS * dt;
+      a.x_hstride = (long)kXS * 64;
       a.Tk = 1500;
-      a.rows_per_win = c.K;
+      // prefill: one sequence per window; decode through this path: the beams of a window share it
+      a.rows_per_win = f.prefill ? 1 : c.K;
       launch_cross_attn(c.dt, a, c.xa_ws, c.st);
     }
     if (f.align) {
@@ -843,8 +826,8 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         a.d = dt;
         a.ck = ckl;
         a.cv = cvl;
-        a.x_wstride = 1500L * dt;
-        a.x_hstride = 1500L * 64;
+        a.x_wstride = (long)kXS * dt;
+        a.x_hstride = (long)kXS * 64;
         a.Tk = 1500;
         a.rows_per_win = 1;
         launch_cross_scores(c.dt, a, c.a_heads, (int)hs.size(), c.scores, c.st);
@@ -1747,8 +1730,8 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.d = dt;
       a.ck = cross_k(c, 0);
       a.cv = cross_v(c, 0);
-      a.x_wstride = 1500L * dt;
-      a.x_hstride = 1500L * 64;
+      a.x_wstride = (long)kXS * dt;
+      a.x_hstride = (long)kXS * 64;
       a.Tk = 1500;
       a.rows_per_win = c.K;
       by = (double)B * 1500 * 2 * dt * 2 + 2.0 * R * dt * 2;

@@ -151,12 +151,37 @@ def test_decoder_logits_match_oracle(micro_ctx, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
-def test_greedy_transcribe_matches_oracle(micro_ctx, dt):
+def test_decoder_logits_batched_windows(micro_ctx, dt):
+    """Several windows in one launch, short (key-chunked cross attention) and long (> 16 queries per window)
+    token sequences: every window's logits match the oracle run on that window alone."""
+    d = O.DIMS["micro"]
+    W = O.make_weights(d, 1, dt)
+    sp = O.special_tokens(d.n_vocab)
+    mels = np.stack([_mel(61, 480000, 80), _mel(62, 90000, 80), _mel(63, 300000, 80)])
+    ctx = micro_ctx[dt]
+    ctx.encode(mels, want_output=False)
+    encs = [O.encoder(W, d, m) for m in mels]
+    rng = np.random.default_rng(7)
+    for T in (5, 21):
+        toks = np.concatenate([np.full((3, 1), sp.sot, np.int32),
+                               rng.integers(0, 50000, size=(3, T - 1)).astype(np.int32)], axis=1)
+        got = ctx.decoder_logits(toks)
+        for b in range(3):
+            ref = O.decoder_forward(W, d, list(toks[b]), O.DecoderCache(W, d, encs[b]))
+            e = rel_l2(got[b], ref)
+            print(dt, "T", T, "window", b, "rel_l2", e)
+            assert e <= REL[dt], (T, b, e)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("n_audio", [3, 2])
+def test_greedy_transcribe_matches_oracle(micro_ctx, dt, n_audio):
+    """n_audio < max_batch checks that a partial batch addresses the KV cache rows like a full one."""
     d = O.DIMS["micro"]
     W = O.make_weights(d, 1, dt)
     sp = O.special_tokens(d.n_vocab)
     ctx = micro_ctx[dt]
-    audios = [synth.speech_like(41, 116800), synth.speech_like(42, 480000), synth.speech_like(43, 40000)]
+    audios = [synth.speech_like(41, 116800), synth.speech_like(42, 480000), synth.speech_like(43, 40000)][:n_audio]
     res = ctx.transcribe(audios)
     n_cmp = 0
     for a, r in zip(audios, res):

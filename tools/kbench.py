@@ -1,0 +1,32 @@
+"""Replay one hot-path kernel of the large-v3 decode step (wmx_ctx_bench_kernel) so a profiler can look at it
+alone, e.g.  rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES -- python tools/kbench.py cross_attn
+Weights are left uninitialised (timing only)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "realtime-whisper-asr_amd"))
+
+import torch  # noqa: E402  (one HIP runtime per process: torch initialises it first)
+
+torch.cuda.init()
+from wmx.engine import Context, Model  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kernel")
+    ap.add_argument("--model", default="large-v3")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--beam", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    m = Model(args.model)
+    ctx = Context(m, max_batch=args.batch, beam_size=args.beam)
+    ms, by, fl = ctx.bench_kernel(args.kernel, args.batch, iters=args.iters)
+    print(f"{args.kernel}: {ms * 1e3:.2f} us/launch, {by / ms / 1e6:.1f} GB/s, {fl / ms / 1e9:.2f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
