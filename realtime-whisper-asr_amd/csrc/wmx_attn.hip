@@ -336,7 +336,7 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 constexpr int kMaxTk = kXS, kMaxSplits = 16;
 
 template <DT T, int KPW>
-__global__ __launch_bounds__(256) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
+__global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z % KS, qt = blockIdx.z / KS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;

@@ -524,6 +524,7 @@ int packed_splits(int M, int N, int K, long cap_elems) {
   long S = (480 + wgs - 1) / wgs;
   S = std::min<long>(S, std::max(1, (K / 32) / 4));
   S = std::min<long>(S, K / (2L * std::max(M, 1)));
+  S = std::min<long>(S, 8);  // the consumers load every slice of a value in one batch (reduce_ln: kRedMaxS)
   while (S > 1 && S * M * (long)N > cap_elems) --S;
   return (int)std::max<long>(1, S);
 }

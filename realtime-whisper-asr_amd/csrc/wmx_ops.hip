@@ -174,78 +174,84 @@ void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const
 }
 
 // ---------------- split-K reduction + residual + LayerNorm (decode step) ----------------
-// one workgroup per row: v = x + bias + sum_s part[s] (slice order fixed), x = v, out16 = LN(v) * g + b
+// one 1024-thread workgroup per row: every partial slice of the thread's columns is loaded in one batch (slice
+// order kept in the sum), v = x + bias + sum_s part[s], x = v, out16 = LN(v) * g + b
+constexpr int kRedThreads = 1024, kRedMaxS = 8;
 template <DT T>
-__global__ __launch_bounds__(256) void reduce_ln_kernel(const float* __restrict__ part, int S, long pstride,
-                                                        const float* __restrict__ bias, float* __restrict__ x,
-                                                        const float* __restrict__ g, const float* __restrict__ b,
-                                                        uint16_t* __restrict__ out, int d) {
-  constexpr int MAXV = 8;  // d <= 2048
+__global__ __launch_bounds__(kRedThreads) void reduce_ln_kernel(const float* __restrict__ part, int S, long pstride,
+                                                                const float* __restrict__ bias, float* __restrict__ x,
+                                                                const float* __restrict__ g, const float* __restrict__ b,
+                                                                uint16_t* __restrict__ out, int d) {
+  constexpr int MAXV = 2;  // d <= 2048
+  constexpr int NW = kRedThreads / 64;
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ float red[2][4];
-  float v[MAXV], p[MAXV];
+  __shared__ float red[2][NW];
+  float t[MAXV][kRedMaxS], xv[MAXV], bv[MAXV];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) p[i] = 0.f;
-  // partial slices in batches of 4 with every load of a batch issued before the adds (slice order kept)
-  for (int s0 = 0; s0 < S; s0 += 4) {
-    float t[MAXV][4];
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = tid + i * kRedThreads;
+    const bool ok = c < d;
+    xv[i] = ok ? x[(long)m * d + c] : 0.f;
+    bv[i] = ok && bias ? bias[c] : 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = tid + i * 256;
-        t[i][u] = (c < d && s0 + u < S) ? part[(s0 + u) * pstride + (long)m * d + c] : 0.f;
-      }
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) p[i] += t[i][u];
+    for (int u = 0; u < kRedMaxS; ++u) t[i][u] = (ok && u < S) ? part[u * pstride + (long)m * d + c] : 0.f;
   }
+  float v[MAXV];
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int c = tid + i * 256;
+    float p = 0.f;
+#pragma unroll
+    for (int u = 0; u < kRedMaxS; ++u) p += t[i][u];
+    const int c = tid + i * kRedThreads;
     v[i] = 0.f;
     if (c < d) {
-      const float a = x[(long)m * d + c] + (bias ? bias[c] : 0.f) + p[i];
-      x[(long)m * d + c] = a;
-      v[i] = a;
-      sum += a;
+      v[i] = xv[i] + bv[i] + p;
+      x[(long)m * d + c] = v[i];
+      sum += v[i];
     }
   }
   if (!g) return;
   sum = wave_sum(sum);
   if (lane == 0) red[0][wave] = sum;
   __syncthreads();
-  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / d;
+  float tot = 0.f;
+#pragma unroll
+  for (int w2 = 0; w2 < NW; ++w2) tot += red[0][w2];
+  const float mean = tot / d;
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int c = tid + i * 256;
+    const int c = tid + i * kRedThreads;
     if (c < d) {
-      const float t = v[i] - mean;
-      sq += t * t;
+      const float q = v[i] - mean;
+      sq += q * q;
     }
   }
   sq = wave_sum(sq);
   if (lane == 0) red[1][wave] = sq;
   __syncthreads();
-  const float rstd = 1.0f / sqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / d + 1e-5f);
+  float tq = 0.f;
+#pragma unroll
+  for (int w2 = 0; w2 < NW; ++w2) tq += red[1][w2];
+  const float rstd = 1.0f / sqrtf(tq / d + 1e-5f);
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
-    const int c = tid + i * 256;
+    const int c = tid + i * kRedThreads;
     if (c < d) out[(long)m * d + c] = from_f32<T>((v[i] - mean) * rstd * g[c] + b[c]);
   }
 }
 
 void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float* x, const float* g, const float* b,
                       uint16_t* out16, int rows, int d, hipStream_t st) {
-  WMX_CHECK(d <= 2048, "reduce_ln: width");
+  WMX_CHECK(d <= 2 * kRedThreads && S >= 1 && S <= kRedMaxS, "reduce_ln: width / split count");
   const long pstride = (long)rows * d;
   if (dt == DT::BF16)
-    hipLaunchKernelGGL(reduce_ln_kernel<DT::BF16>, dim3(rows), dim3(256), 0, st, part, S, pstride, bias, x, g, b, out16, d);
+    hipLaunchKernelGGL(reduce_ln_kernel<DT::BF16>, dim3(rows), dim3(kRedThreads), 0, st, part, S, pstride, bias, x, g,
+                       b, out16, d);
   else
-    hipLaunchKernelGGL(reduce_ln_kernel<DT::F16>, dim3(rows), dim3(256), 0, st, part, S, pstride, bias, x, g, b, out16, d);
+    hipLaunchKernelGGL(reduce_ln_kernel<DT::F16>, dim3(rows), dim3(kRedThreads), 0, st, part, S, pstride, bias, x, g,
+                       b, out16, d);
   WMX_HIP(hipGetLastError());
 }
 
