@@ -50,8 +50,9 @@ void launch_text_prob(const float* logits, int ldl, int eot, const int* target, 
 // alignment matrix [nwin][Tn][Tk]: zero, accumulate heads (softmax over nframes/2, normalise over tokens, median
 // filter), scale by 1/n_heads
 void launch_align_matrix_zero(float* out, int nwin, int Tn, int Tk, hipStream_t st);
-void launch_align_matrix_acc(const float* scores, int nh, int rows_total, int Tk, int Tn, const int* ntok,
-                             const int* nframes, int width, int nwin, float* scratch, float* out, hipStream_t st);
+// (scores [nh][rows_total][Tk] are normalised in place)
+void launch_align_matrix_acc(float* scores, int nh, int rows_total, int Tk, int Tn, const int* ntok,
+                             const int* nframes, int width, int nwin, hipStream_t st, float* out);
 void launch_align_matrix_scale(float* out, int nwin, int Tn, int Tk, const int* ntok, const int* nframes, float scale,
                                hipStream_t st);
 

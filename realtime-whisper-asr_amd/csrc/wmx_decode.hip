@@ -532,61 +532,98 @@ __device__ inline float median7(float* v, int n) {
   return v[n / 2];
 }
 
-__global__ __launch_bounds__(256) void align_acc_kernel(const float* __restrict__ scores, int nh, int rows_total, int Tk,
-                                                        int Tn, const int* __restrict__ ntok,
-                                                        const int* __restrict__ nframes, int width,
-                                                        float* __restrict__ scratch, float* __restrict__ out) {
-  const int w = blockIdx.x;
-  const int T = ntok[w];
+// alignment matrix of one decoder layer's alignment heads (faster-whisper/openai find_alignment), in three
+// grid-wide passes over scores[hh][row][Tk] (rows = window * Tn + token), in place:
+//   softmax over the window's nf = nframes/2 frames (one workgroup per (token, head, window)),
+//   per-frame standardisation over the T tokens (one thread per frame),
+//   median filter along frames, accumulated into out over the heads in head order.
+__global__ __launch_bounds__(256) void align_softmax_kernel(float* __restrict__ scores, int rows_total, int Tk, int Tn,
+                                                            const int* __restrict__ ntok,
+                                                            const int* __restrict__ nframes) {
+  const int t = blockIdx.x, hh = blockIdx.y, w = blockIdx.z;
+  if (t >= ntok[w]) return;
   const int nf = nframes[w] / 2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* sc = scratch + (long)w * Tn * Tk;
-  float* o = out + (long)w * Tn * Tk;
-  const int pad = width / 2;
-  for (int hh = 0; hh < nh; ++hh) {
-    const float* s = scores + ((long)hh * rows_total + (long)w * Tn) * Tk;
-    for (int t = wave; t < T; t += 4) {
-      float mx = -INFINITY;
-      for (int f = lane; f < nf; f += 64) mx = fmaxf(mx, s[(long)t * Tk + f]);
-      mx = wave_max(mx);
-      float sum = 0.f;
-      for (int f = lane; f < nf; f += 64) sum += __expf(s[(long)t * Tk + f] - mx);
-      sum = wave_sum(sum);
-      const float inv = 1.0f / sum;
-      for (int f = lane; f < nf; f += 64) sc[(long)t * Tk + f] = __expf(s[(long)t * Tk + f] - mx) * inv;
-    }
-    __syncthreads();
-    for (int f = tid; f < nf; f += 256) {
-      float mean = 0.f;
-      for (int t = 0; t < T; ++t) mean += sc[(long)t * Tk + f];
-      mean /= T;
-      float var = 0.f;
-      for (int t = 0; t < T; ++t) {
-        const float dlt = sc[(long)t * Tk + f] - mean;
-        var += dlt * dlt;
-      }
-      const float inv = 1.0f / sqrtf(var / T);
-      for (int t = 0; t < T; ++t) sc[(long)t * Tk + f] = (sc[(long)t * Tk + f] - mean) * inv;
-    }
-    __syncthreads();
-    for (int i = tid; i < T * nf; i += 256) {
-      const int t = i / nf, f = i % nf;
+  __shared__ float red[4];
+  float* s = scores + ((long)hh * rows_total + (long)w * Tn + t) * Tk;
+  float v[6];  // Tk <= 1536
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int f = tid + 256 * i;
+    v[i] = f < nf ? s[f] : -INFINITY;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int f = tid + 256 * i;
+    v[i] = f < nf ? __expf(v[i] - mx) : 0.f;
+    sum += v[i];
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  const float inv = 1.0f / (red[0] + red[1] + red[2] + red[3]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int f = tid + 256 * i;
+    if (f < nf) s[f] = v[i] * inv;
+  }
+}
+
+__global__ __launch_bounds__(256) void align_colnorm_kernel(float* __restrict__ scores, int rows_total, int Tk, int Tn,
+                                                            const int* __restrict__ ntok,
+                                                            const int* __restrict__ nframes) {
+  const int f = blockIdx.x * 256 + threadIdx.x, hh = blockIdx.y, w = blockIdx.z;
+  const int T = ntok[w], nf = nframes[w] / 2;
+  if (f >= nf || T <= 0) return;
+  float* s = scores + ((long)hh * rows_total + (long)w * Tn) * Tk + f;
+  float mean = 0.f;
+  for (int t = 0; t < T; ++t) mean += s[(long)t * Tk];
+  mean /= T;
+  float var = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float dlt = s[(long)t * Tk] - mean;
+    var += dlt * dlt;
+  }
+  const float inv = 1.0f / sqrtf(var / T);
+  for (int t = 0; t < T; ++t) s[(long)t * Tk] = (s[(long)t * Tk] - mean) * inv;
+}
+
+__global__ __launch_bounds__(256) void align_median_acc_kernel(const float* __restrict__ scores, int nh, int rows_total,
+                                                               int Tk, int Tn, const int* __restrict__ ntok,
+                                                               const int* __restrict__ nframes, int width,
+                                                               float* __restrict__ out) {
+  const int t = blockIdx.x, w = blockIdx.y;
+  if (t >= ntok[w]) return;
+  const int nf = nframes[w] / 2, pad = width / 2;
+  float* o = out + ((long)w * Tn + t) * Tk;
+  for (int f = threadIdx.x; f < nf; f += 256) {
+    float acc = o[f];
+    for (int hh = 0; hh < nh; ++hh) {
+      const float* sc = scores + ((long)hh * rows_total + (long)w * Tn + t) * Tk;
       float v;
       if (nf <= pad) {
-        v = sc[(long)t * Tk + f];
+        v = sc[f];
       } else {
         float win[15];
         for (int k = 0; k < width; ++k) {
           int j = f - pad + k;
           if (j < 0) j = -j;
           if (j >= nf) j = 2 * (nf - 1) - j;
-          win[k] = sc[(long)t * Tk + j];
+          win[k] = sc[j];
         }
         v = median7(win, width);
       }
-      o[(long)t * Tk + f] += v;
+      acc += v;
     }
-    __syncthreads();
+    o[f] = acc;
   }
 }
 
@@ -655,11 +692,15 @@ void launch_align_matrix_zero(float* out, int nwin, int Tn, int Tk, hipStream_t 
   WMX_HIP(hipMemsetAsync(out, 0, (size_t)nwin * Tn * Tk * sizeof(float), st));
 }
 
-void launch_align_matrix_acc(const float* scores, int nh, int rows_total, int Tk, int Tn, const int* ntok,
-                             const int* nframes, int width, int nwin, float* scratch, float* out, hipStream_t st) {
-  WMX_CHECK(width <= 15 && width % 2 == 1, "median filter width");
-  hipLaunchKernelGGL(align_acc_kernel, dim3(nwin), dim3(256), 0, st, scores, nh, rows_total, Tk, Tn, ntok, nframes, width,
-                     scratch, out);
+void launch_align_matrix_acc(float* scores, int nh, int rows_total, int Tk, int Tn, const int* ntok,
+                             const int* nframes, int width, int nwin, hipStream_t st, float* out) {
+  WMX_CHECK(width <= 15 && width % 2 == 1 && Tk <= 1536, "alignment: median filter width / frames");
+  hipLaunchKernelGGL(align_softmax_kernel, dim3(Tn, nh, nwin), dim3(256), 0, st, scores, rows_total, Tk, Tn, ntok,
+                     nframes);
+  hipLaunchKernelGGL(align_colnorm_kernel, dim3((Tk + 255) / 256, nh, nwin), dim3(256), 0, st, scores, rows_total, Tk,
+                     Tn, ntok, nframes);
+  hipLaunchKernelGGL(align_median_acc_kernel, dim3(Tn, nwin), dim3(256), 0, st, scores, nh, rows_total, Tk, Tn, ntok,
+                     nframes, width, out);
   WMX_HIP(hipGetLastError());
 }
 

@@ -385,7 +385,7 @@ struct Ctx {
   float* xa_ws = nullptr;
   uint32_t* mask = nullptr;
   // alignment
-  float *scores = nullptr, *align_scratch = nullptr, *align_out = nullptr, *tprob = nullptr;
+  float *scores = nullptr, *align_out = nullptr, *tprob = nullptr;
   int *a_ntok = nullptr, *a_nframes = nullptr, *a_target = nullptr, *a_heads = nullptr;
   int a_heads_cap = 0;
   int* pinned_i = nullptr;
@@ -483,7 +483,6 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
-  P.add(&c.align_scratch, (size_t)B * T * 1500);
   P.add(&c.align_out, (size_t)B * T * 1500);
   P.add(&c.tprob, (size_t)B * T);
   P.add(&c.a_ntok, B);
@@ -832,7 +831,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         a.rows_per_win = 1;
         launch_cross_scores(c.dt, a, c.a_heads, (int)hs.size(), c.scores, c.st);
         launch_align_matrix_acc(c.scores, (int)hs.size(), rowsT, 1500, f.Tn, c.a_ntok, c.a_nframes,
-                                c.o.median_filter_width, f.rows, c.align_scratch, c.align_out, c.st);
+                                c.o.median_filter_width, f.rows, c.st, c.align_out);
         // hipMemcpyAsync of a host vector: make sure it completed before hs goes out of scope
         sync(c);
       }
