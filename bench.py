@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--model", default="large-v3")
     p.add_argument("--batch", type=int, default=8, help="concurrent 30 s streams per GPU")
+    p.add_argument("--groups", type=int, default=2, help="concurrent decoding contexts the streams are split over")
     p.add_argument("--beam", type=int, default=5)
     p.add_argument("--max-new-tokens", type=int, default=224)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
@@ -138,17 +139,35 @@ def main():
     log(f"[rank {rank}] weights ready in {time.time() - t:.2f}s ({model.n_params() / 1e9:.2f} B params)")
 
     B = args.batch
+    G = args.groups
+    assert B % G == 0, "--batch must be a multiple of --groups"
+    Bg = B // G
     heads = engine.ALIGNMENT_HEADS.get(args.model)
-    ctx = engine.Context(model, max_batch=B, beam_size=args.beam, max_new_tokens=args.max_new_tokens,
-                         language=None, word_timestamps=True, alignment_heads=heads, use_graph=not args.no_graph)
+    # G decoding contexts (each its own HIP stream and captured decode graph) share the weights; their window
+    # groups run concurrently, so one group's kernel boundaries and latency-bound phases overlap the other's work
+    ctxs = [engine.Context(model, max_batch=Bg, beam_size=args.beam, max_new_tokens=args.max_new_tokens,
+                           language=None, word_timestamps=True, alignment_heads=heads, use_graph=not args.no_graph)
+            for _ in range(G)]
+    ctx = ctxs[0]
     # synthetic 30 s streams, resident in HBM before the timed region
     audio = np.stack([synth.speech_like(rank * B + i, 480000) for i in range(B)])
     pcm = torch.from_numpy(audio).to(f"cuda:{local}")
-    lens = np.full(B, 480000, np.int64)
+    lens = np.full(Bg, 480000, np.int64)
     torch.cuda.synchronize()
+    pool = None
+    if G > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=G)  # ctypes drops the GIL inside libwmx calls
 
     def step():
-        return ctx.transcribe_device(pcm.data_ptr(), 480000, lens)
+        if G == 1:
+            return ctx.transcribe_device(pcm.data_ptr(), 480000, lens)
+        futs = [pool.submit(c.transcribe_device, pcm.data_ptr() + g * Bg * 480000 * 4, 480000, lens)
+                for g, c in enumerate(ctxs)]
+        out = []
+        for f in futs:
+            out.extend(f.result())
+        return out
 
     for _ in range(args.warmup):
         step()
@@ -185,17 +204,17 @@ def main():
     per_step_ms = {}
     kern_stats = {}
     R = B * args.beam
-    counts = {  # launches per transcribe step
-        "cross_attn": steps_done * model.dims.n_text_layer,
-        "self_attn": steps_done * model.dims.n_text_layer,
-        "dec_fc1": steps_done * model.dims.n_text_layer,
-        "enc_fc1": model.dims.n_audio_layer,
-        "enc_attn": model.dims.n_audio_layer,
-        "logmel": 1,
+    counts = {  # launches per transcribe step (each context group launches its own, over Bg windows)
+        "cross_attn": G * steps_done * model.dims.n_text_layer,
+        "self_attn": G * steps_done * model.dims.n_text_layer,
+        "dec_fc1": G * steps_done * model.dims.n_text_layer,
+        "enc_fc1": G * model.dims.n_audio_layer,
+        "enc_attn": G * model.dims.n_audio_layer,
+        "logmel": G,
     }
     for k in counts:
         log(f"[rank {rank}] timing kernel {k}")
-        ms, by, fl = ctx.bench_kernel(k, B, iters=20)
+        ms, by, fl = ctx.bench_kernel(k, Bg, iters=20)
         kern_stats[k] = (ms, by, fl)
         per_step_ms[k] = ms * counts[k]
     dom = max(per_step_ms, key=per_step_ms.get) if args.roofline_kernel == "auto" else args.roofline_kernel
@@ -208,6 +227,15 @@ def main():
         ach = by / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py), if present
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(pmc):
+        rec = json.load(open(pmc)).get(dom)
+        if rec:
+            roof["traffic"] = round(rec["traffic_bytes"] / (1e9 if roof["unit"] == "GB/s" else 1.0) / (ms * 1e-3), 1) \
+                if roof["unit"] == "GB/s" else rec["traffic_bytes"]
+            roof["traffic_bytes_per_launch"] = rec["traffic_bytes"]
+            roof["traffic_source"] = "profiles/r01_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
     roof["kernel"] = dom
     roof["launch_ms"] = round(ms, 4)
     roof["algorithmic_per_launch"] = {"bytes": by, "flops": fl}
@@ -234,7 +262,7 @@ def main():
                                f"word_timestamps, language auto-detect, max_new_tokens {args.max_new_tokens}",
                    "model": f"whisper-{args.model}", "global_batch": B * world, "seq_len": 480000,
                    "parallelism": f"dp{world} (independent streams)", "decode_steps": steps_done,
-                   "use_graph": not args.no_graph},
+                   "use_graph": not args.no_graph, "context_groups": G},
         "stage_ms": [round(s, 2) for s in stages],
         "roofline": roof,
     }

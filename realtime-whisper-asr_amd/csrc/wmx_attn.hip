@@ -189,124 +189,141 @@ void launch_attn_flash(DT dt, const AttnArgs& a, int causal, int causal_off, con
 void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) { launch_attn_flash(dt, a, 0, 0, nullptr, st); }
 
 // ------------------------------------------------------------------------------------------------
-// decoder self attention (decode step or small Tn), keys through the ancestry table
+// decoder self attention for decode steps: workgroup = (head, row); the row's keys are its ancestry
+// (anc[r][slot] = the cache row holding slot `slot` of row r's hypothesis; identity without beams).
+// Thread = (key group kg = tid >> 3 of 32, 8-dim chunk c = tid & 7); per batch of 256 keys each thread
+// holds 8 keys' K and V chunks in registers, all their loads issued before any arithmetic (ancestry ->
+// K/V is the only dependent round trip).  Online softmax across batches; block-wide reductions via LDS.
 // ------------------------------------------------------------------------------------------------
 template <DT T>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
+  constexpr int J = 8;  // keys per thread per batch (32 key groups x 8 = 256 keys)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = blockIdx.x;
   const int m = blockIdx.y;  // r * Tn + i
-  __shared__ float s[512];
-  __shared__ float red[4];
-  __shared__ float fin[4][64];
   const int r = m / a.Tn, i = m - r * a.Tn;
   const int slot_q = *a.slot0 + i;
   const int beg = a.pad ? a.pad[r] : 0;
-  const int gi = lane >> 3, j = lane & 7;  // 8 key groups x 8 dim chunks per wave
+  const int kg = tid >> 3, c = tid & 7;
   const long kvR = a.kv_R;
-  float q[8];
+  __shared__ float qs[64], kcur[64], vcur[64];
+  __shared__ float red[2][4];
+  __shared__ float fin[4][64];
+  const int* anc = a.anc ? a.anc + (long)r * a.anc_ld : nullptr;
+
+  // ---- this step's q / k / v of (row, head): from the QKV split-K partials or the stored q + cache slot ----
   if (a.qS > 0) {
-    // decode step fed by QKV split-K partials: reduce q/k/v of (row m, head h) in slice order, round to the model
-    // dtype (as the stored path does), put k/v into the cache slot, keep q in LDS
-    __shared__ float qs[64];
     if (tid < 192) {
       const int part = tid >> 6, e = tid & 63;
       const int col = part * a.d + h * 64 + e;
-      float p = 0.f;
       const float* src = a.qpart + (long)m * a.qpart_ld + col;
-      for (int s0 = 0; s0 < a.qS; s0 += 8) {  // all loads of a batch in flight, slice order kept
-        float t[8];
+      float t[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = s0 + u < a.qS ? src[(s0 + u) * a.qpart_stride] : 0.f;
+      for (int u = 0; u < 8; ++u) t[u] = u < a.qS ? src[u * a.qpart_stride] : 0.f;  // qS <= 8: one batch
+      float p = 0.f;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) p += t[u];
-      }
+      for (int u = 0; u < 8; ++u) p += t[u];
       const uint16_t hv = from_f32<T>(p + (a.qbias ? a.qbias[col] : 0.f));
-      if (part == 0)
-        qs[e] = to_f32<T>(hv);
-      else
+      const float f = to_f32<T>(hv);
+      if (part == 0) {
+        qs[e] = f * 0.125f;
+      } else {
+        (part == 1 ? kcur : vcur)[e] = f;
         const_cast<uint16_t*>(part == 1 ? a.kc : a.vc)[((long)slot_q * kvR + r) * a.d + h * 64 + e] = hv;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = qs[j * 8 + e] * 0.125f;
-  } else {
-    const u16x8 qv = *reinterpret_cast<const u16x8*>(a.q + (long)m * a.q_ld + h * 64 + j * 8);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = to_f32<T>(qv[e]) * 0.125f;
-  }
-  const int* anc = a.anc ? a.anc + (long)r * a.anc_ld : nullptr;
-  constexpr int U = 4;  // per wave per iteration: 32 keys, 4 independent 16-B loads per lane
-  float mx = -INFINITY;
-  for (int s0 = beg + wave * 8 * U; s0 <= slot_q; s0 += 4 * 8 * U) {
-    u16x8 kv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int key = min(s0 + 8 * u + gi, slot_q);
-      const int row = anc ? anc[key] : r;
-      kv[u] = *reinterpret_cast<const u16x8*>(a.kc + ((long)key * kvR + row) * a.d + h * 64 + j * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int key = s0 + 8 * u + gi;
-      float part = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) part += q[e] * to_f32<T>(kv[u][e]);
-      part += __shfl_xor(part, 1);
-      part += __shfl_xor(part, 2);
-      part += __shfl_xor(part, 4);
-      if (key <= slot_q) {
-        if (j == 0) s[key - beg] = part;
-        mx = fmaxf(mx, part);
       }
     }
+  } else if (tid < 192) {
+    const int part = tid >> 6, e = tid & 63;
+    if (part == 0)
+      qs[e] = to_f32<T>(a.q[(long)m * a.q_ld + h * 64 + e]) * 0.125f;
+    else
+      (part == 1 ? kcur : vcur)[e] = to_f32<T>((part == 1 ? a.kc : a.vc)[((long)slot_q * kvR + r) * a.d + h * 64 + e]);
   }
-  mx = wave_max(mx);
-  if (lane == 0) red[wave] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  const int n = slot_q - beg + 1;
-  float sum = 0.f;
-  for (int t = tid; t < n; t += 256) {
-    const float e = __expf(s[t] - mx);
-    s[t] = e;
-    sum += e;
-  }
-  sum = wave_sum(sum);
-  __syncthreads();
-  if (lane == 0) red[wave] = sum;
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int s0 = beg + wave * 8 * U; s0 <= slot_q; s0 += 4 * 8 * U) {
-    u16x8 vv[U];
+
+  float m_run = -INFINITY, l_run = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool first = true;
+  for (int b0 = beg; b0 <= slot_q; b0 += 32 * J) {
+    // ancestry, then every K / V load of the batch (keys < slot_q come from the cache)
+    int row[J];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int key = min(s0 + 8 * u + gi, slot_q);
-      const int row = anc ? anc[key] : r;
-      vv[u] = *reinterpret_cast<const u16x8*>(a.vc + ((long)key * kvR + row) * a.d + h * 64 + j * 8);
+    for (int j = 0; j < J; ++j) {
+      const int key = b0 + kg + 32 * j;
+      row[j] = (anc && key < slot_q) ? anc[key] : r;
     }
+    u16x8 kv[J], vv[J];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int key = s0 + 8 * u + gi;
-      const float p = key <= slot_q ? s[key - beg] : 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += p * to_f32<T>(vv[u][e]);
+    for (int j = 0; j < J; ++j) {
+      const int key = min(b0 + kg + 32 * j, slot_q);
+      const long off = ((long)key * kvR + row[j]) * a.d + h * 64 + c * 8;
+      kv[j] = *reinterpret_cast<const u16x8*>(a.kc + off);
+      vv[j] = *reinterpret_cast<const u16x8*>(a.vc + off);
     }
+    if (first) {
+      __syncthreads();  // qs / kcur / vcur (and this step's cache slot) complete
+      first = false;
+    }
+    float q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = qs[c * 8 + e];
+    float sc[J];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int key = b0 + kg + 32 * j;
+      float p = 0.f;
+      if (key == slot_q) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) p += q[e] * kcur[c * 8 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) p += q[e] * to_f32<T>(kv[j][e]);
+      }
+      p += __shfl_xor(p, 1);
+      p += __shfl_xor(p, 2);
+      p += __shfl_xor(p, 4);
+      sc[j] = key <= slot_q ? p : -INFINITY;
+      mx = fmaxf(mx, sc[j]);
+    }
+    mx = wave_max(mx);
+    if (lane == 0) red[0][wave] = mx;
+    __syncthreads();
+    const float m_new = fmaxf(m_run, fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3])));
+    __syncthreads();  // red reused by the next batch
+    const float alpha = __expf(m_run - m_new);
+    l_run *= alpha;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= alpha;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int key = b0 + kg + 32 * j;
+      const float p = __expf(sc[j] - m_new);  // 0 for keys past slot_q
+      if (c == 0) l_run += p;
+      if (key == slot_q) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += p * vcur[c * 8 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += p * to_f32<T>(vv[j][e]);
+      }
+    }
+    m_run = m_new;
   }
+  // reduce over the 8 key groups of the wave, then over the 4 waves
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     acc[e] += __shfl_xor(acc[e], 8);
     acc[e] += __shfl_xor(acc[e], 16);
     acc[e] += __shfl_xor(acc[e], 32);
   }
-  if (gi == 0) {
+  const float lw = wave_sum(l_run);
+  if (lane == 0) red[1][wave] = lw;
+  if (lane < 8) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) fin[wave][j * 8 + e] = acc[e];
+    for (int e = 0; e < 8; ++e) fin[wave][c * 8 + e] = acc[e];
   }
   __syncthreads();
   if (tid < 64) {
-    const float tot = red[0] + red[1] + red[2] + red[3];
+    const float tot = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     const float o = (fin[0][tid] + fin[1][tid] + fin[2][tid] + fin[3][tid]) / tot;
     a.o[(long)m * a.d + h * 64 + tid] = from_f32<T>(o);
   }
@@ -334,6 +351,10 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 // KS > 1: each chunk writes a (max, sum, o[64]) record per query; dec_cross_combine merges them in order.
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxTk = kXS, kMaxSplits = 16;
+typedef __attribute__((address_space(1))) float gf32;
+
+// chunk records [nwin][H][KS][nq][66]; one arrival counter per (window, head) in DecAttnArgs::xcnt
+inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long)nwin * H * KS * nq * 66; }
 
 template <DT T, int KPW>
 __global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
@@ -503,49 +524,60 @@ __global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(D
     if (KS == 1) {
       a.o[row * a.d + h * 64 + e] = from_f32<T>(O / L);
     } else {
-      float* pr = part + (((long)(w * a.H + h) * KS + ks) * nq + i0 + q) * 66;
+      // chunk record, stored write-through (sc1) so the last arriver can read it without an L2 release
+      gf32* pr = (gf32*)(part + (((long)(w * a.H + h) * KS + ks) * nq + i0 + q) * 66);
       if (e == 0) {
-        pr[0] = M;
-        pr[1] = L;
+        __hip_atomic_store(pr, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pr + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      pr[2 + e] = O;
+      __hip_atomic_store(pr + 2 + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-}
-
-// merge the KS chunk records of every (window, head, q) in chunk order (records: cross_attn_ws_floats(H, nwin, 16))
-template <DT T>
-__global__ __launch_bounds__(256) void dec_cross_combine_kernel(const float* __restrict__ part, int KS, int H, int nq,
-                                                                int d, uint16_t* __restrict__ out) {
-  const int w = blockIdx.x, h = blockIdx.y;
-  for (int t = threadIdx.x; t < nq * 64; t += 256) {
+  if (KS == 1) return;
+  // ---- in-launch merge (cdna_hip_programming.md Guideline 16, sc1 form): every storing wave drains its
+  //      write-through stores, one lane takes a ticket; the workgroup drawing KS-1 merges the records in chunk
+  //      order with sc1 loads (no acquire fence needed) and re-arms the counter for the next launch ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* cnt = a.xcnt;
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(cnt + w * a.H + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm[0][0] = old == KS - 1 ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (sm[0][0] == 0.f) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // every record load is a buffer load with sc1 (aux 16): it bypasses this CU's L1, so no acquire is needed
+  const float* wh = part + (long)(w * a.H + h) * KS * nq * 66;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)wh, (short)0, KS * nq * 66 * 4, 0x00020000);
+  for (int t = tid; t < nq * 64; t += 256) {
     const int q = t >> 6, e = t & 63;
-    const float* pr = part + ((long)(w * H + h) * KS * nq + q) * 66;
     float rec[kMaxSplits][3];
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
-        const float* x = pr + (long)k * nq * 66;
-        rec[k][0] = x[0];
-        rec[k][1] = x[1];
-        rec[k][2] = x[2 + e];
+        const int off = ((k * nq + q) * 66) * 4;
+        rec[k][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 16));
+        rec[k][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 16));
+        rec[k][2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + (2 + e) * 4, 0, 16));
       }
     }
     float M = -INFINITY;
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k)
       if (k < KS) M = fmaxf(M, rec[k][0]);
-    float l = 0.f, o = 0.f;
+    float l = 0.f, o2 = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
         const float sc2 = rec[k][0] == -INFINITY ? 0.f : __expf(rec[k][0] - M);
         l += rec[k][1] * sc2;
-        o += rec[k][2] * sc2;
+        o2 += rec[k][2] * sc2;
       }
     }
-    out[(long)(w * nq + q) * d + h * 64 + e] = from_f32<T>(o / l);
+    a.o[((long)w * nq + q) * a.d + h * 64 + e] = from_f32<T>(o2 / l);
   }
+  if (tid == 0) __hip_atomic_store(cnt + w * a.H + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // key chunk per workgroup; WMX_CROSS_CHUNK overrides the default for tuning runs
@@ -559,7 +591,9 @@ static int cross_chunk(int Tk, int nq) {
   return 256;
 }
 
-size_t cross_attn_ws_floats(int H, int nwin, int nq_max) { return (size_t)nwin * H * kMaxSplits * nq_max * 66; }
+size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
+  return (size_t)cross_records_floats(H, nwin, nq_max, kMaxSplits);
+}
 
 template <DT T>
 static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
@@ -569,7 +603,7 @@ static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
   const int KS = (a.Tk + chunk - 1) / chunk;
   const int QT = (nq + 15) / 16;
   WMX_CHECK(KS <= kMaxSplits, "cross attn: too many key chunks");
-  WMX_CHECK(KS == 1 || (ws != nullptr && nq <= 16), "cross attn: split workspace required");
+  WMX_CHECK(KS == 1 || (ws != nullptr && a.xcnt != nullptr && nq <= 16), "cross attn: split workspace required");
   dim3 grid(a.H, nwin, KS * QT);
   const int per_wave = ((chunk + 3) / 4 + 31) / 32;  // 32-key blocks per wave
   switch (std::min(per_wave, 4)) {
@@ -578,8 +612,6 @@ static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
     case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
     default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
   }
-  if (KS > 1)
-    hipLaunchKernelGGL(dec_cross_combine_kernel<T>, dim3(nwin, a.H), dim3(256), 0, st, ws, KS, a.H, nq, a.d, a.o);
 }
 
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {

@@ -22,10 +22,10 @@ struct RowState {  // SoA pointers, one entry per row
   float* sum_lp;
 };
 
-__device__ inline bool allowed(const RuleOpts& o, int t, int ns, bool last_ts, bool pen_ts, int lts) {
+// every rule except the suppress bitmask (the caller tests that word)
+__device__ inline bool allowed_rules(const RuleOpts& o, int t, int ns, bool last_ts, bool pen_ts, int lts) {
   if (t == o.no_ts) return false;
   if (o.suppress_blank && ns == 0 && (t == o.blank || t == o.eot)) return false;
-  if ((o.mask[t >> 5] >> (t & 31)) & 1u) return false;
   if (!o.without_ts) {
     if (last_ts) {
       if (pen_ts) {
@@ -44,6 +44,11 @@ __device__ inline bool allowed(const RuleOpts& o, int t, int ns, bool last_ts, b
     }
   }
   return true;
+}
+
+__device__ inline bool allowed(const RuleOpts& o, int t, int ns, bool last_ts, bool pen_ts, int lts) {
+  if ((o.mask[t >> 5] >> (t & 31)) & 1u) return false;
+  return allowed_rules(o, t, ns, last_ts, pen_ts, lts);
 }
 
 struct MS {  // online max/sum
@@ -76,6 +81,8 @@ __device__ inline bool better(float va, int ia, float vb, int ib) { return va > 
 // ---- phase A: one block per (row, vocab slice): masked statistics + top-KP of allowed text and timestamp
 //      tokens, kept separately because whether text is masked depends on the whole row ----
 constexpr int kSlices = 8, kSelA = 256;
+constexpr int kSelPer = 6656;                   // vocab entries per slice (8 x 6656 >= 51866), even
+constexpr int kSelNL = kSelPer / (2 * kSelA);   // 8-byte loads per thread per slice
 
 struct TopK {
   float v[kMaxKP];
@@ -161,24 +168,38 @@ __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict
   const int ns = rs.ns[r], lt = rs.last[r], pt = rs.pen[r], lts = rs.last_ts[r];
   const bool last_ts = ns >= 1 && lt >= o.tb;
   const bool pen_ts = ns < 2 || pt >= o.tb;
-  const int per = (o.V + kSlices - 1) / kSlices;
-  const int t0 = sl * per, t1 = min(o.V, t0 + per);
   const int tid = threadIdx.x;
   MS text{-INFINITY, 0.f}, ts{-INFINITY, 0.f};
   float tmax = -INFINITY;
   TopK ktx, kts;
   topk_init(ktx);
   topk_init(kts);
-  for (int t = t0 + tid; t < t1; t += kSelA) {
-    if (!allowed(o, t, ns, last_ts, pen_ts, lts)) continue;
-    const float v = x[t];
-    if (t < o.tb) {
-      text = ms_add(text, v);
-      tmax = fmaxf(tmax, v);
-      topk_push(ktx, v, t, KP);
-    } else {
-      ts = ms_add(ts, v);
-      topk_push(kts, v, t, KP);
+  // the slice's values (pairs t, t+1 per 8-byte load) and suppress-mask words, all loaded before any use
+  const int t0 = sl * kSelPer;
+  float2 xv[kSelNL];
+  unsigned mw[kSelNL];
+#pragma unroll
+  for (int u = 0; u < kSelNL; ++u) {
+    const int t = t0 + 2 * (tid + u * kSelA);
+    xv[u] = t + 1 < o.V ? *reinterpret_cast<const float2*>(x + t)
+                        : make_float2(t < o.V ? x[min(t, o.V - 1)] : -INFINITY, -INFINITY);
+    mw[u] = t < o.V ? o.mask[t >> 5] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < kSelNL; ++u) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int t = t0 + 2 * (tid + u * kSelA) + hh;
+      if (t >= o.V || ((mw[u] >> (t & 31)) & 1u) || !allowed_rules(o, t, ns, last_ts, pen_ts, lts)) continue;
+      const float v = hh ? xv[u].y : xv[u].x;
+      if (t < o.tb) {
+        text = ms_add(text, v);
+        tmax = fmaxf(tmax, v);
+        topk_push(ktx, v, t, KP);
+      } else {
+        ts = ms_add(ts, v);
+        topk_push(kts, v, t, KP);
+      }
     }
   }
 #pragma unroll
@@ -641,6 +662,7 @@ size_t logits_select_ws_floats(int R, int KP) { return (size_t)R * kSlices * (5 
 void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const RowPtrs& rp, int R, int KP, int* tok,
                           float* lp, const int* row_map, float* ws, hipStream_t st) {
   WMX_CHECK(KP <= kMaxKP, "beam too large");
+  WMX_CHECK(o.V <= kSlices * kSelPer && ldl % 2 == 0, "logits select: vocabulary / row stride");
   RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
   hipLaunchKernelGGL(logits_select_a, dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, KP, row_map, ws);
   hipLaunchKernelGGL(logits_select_b, dim3(R), dim3(64), 0, st, ws, o, KP, tok, lp);

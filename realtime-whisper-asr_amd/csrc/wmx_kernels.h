@@ -143,6 +143,7 @@ struct DecAttnArgs {
   long x_wstride, x_hstride;
   int Tk;
   int rows_per_win;    // rows sharing one encoder window (beam)
+  int* xcnt = nullptr; // key-chunked launches: one arrival counter per (window, head), zero between launches
   // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
   // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
   const float* qpart = nullptr;
@@ -152,7 +153,8 @@ struct DecAttnArgs {
   int win_of_row_div;  // row -> window = row / rows_per_win
 };
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);
-// ws: cross_attn_ws_floats(H, nwin, nq_max) floats for the key-chunk records (decode steps)
+// ws: cross_attn_ws_floats(H, nwin, nq_max) floats for the key-chunk records (decode steps), a.xcnt: nwin*H
+// zero-initialised ints (the merging workgroup re-arms its counter)
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max);
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st);
 // raw cross-attention scores of selected heads (alignment): out [nh][R*Tn][Tk] f32

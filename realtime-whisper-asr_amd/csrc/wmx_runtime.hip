@@ -369,6 +369,7 @@ struct Ctx {
   uint16_t *dhb = nullptr, *dq = nullptr, *dao = nullptr, *dcq = nullptr, *df1 = nullptr, *kc = nullptr, *vc = nullptr;
   float* logits = nullptr;
   int logits_rows = 0;
+  int ldl = 0;  // logits row stride (vocab rounded up to 4 floats: 16-B aligned rows)
   float* ws = nullptr;
   long ws_elems = 0;
   float* part = nullptr;  // split-K partials of the packed decode GEMMs [S][rows][N]
@@ -383,6 +384,7 @@ struct Ctx {
   float* clp = nullptr;
   float* sel_ws = nullptr;
   float* xa_ws = nullptr;
+  int* xa_cnt = nullptr;
   uint32_t* mask = nullptr;
   // alignment
   float *scores = nullptr, *align_out = nullptr, *tprob = nullptr;
@@ -407,6 +409,7 @@ static void alloc_ctx(Ctx& c) {
   c.fcap = (int)(c.max_samples / 160) + 1;
   c.dec_rows_max = std::max(R, B * T);
   c.logits_rows = std::max({R, 2 * B, 256});
+  c.ldl = (V + 3) / 4 * 4;
   int nheads = c.align_heads.empty() ? (Lt - Lt / 2) * d.n_text_head : (int)c.align_heads.size() / 2;
   int heads_per_layer = d.n_text_head;
   c.a_heads_cap = std::max(nheads, heads_per_layer);
@@ -438,7 +441,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.df1, (size_t)DR * 4 * dt);
   P.add(&c.kc, (size_t)Lt * T * R * dt);
   P.add(&c.vc, (size_t)Lt * T * R * dt);
-  P.add(&c.logits, (size_t)c.logits_rows * V);
+  P.add(&c.logits, (size_t)c.logits_rows * c.ldl);
   P.add(&c.ws, (size_t)c.ws_elems);
   c.part_elems = (long)R * dt * 48;
   P.add(&c.part, (size_t)c.part_elems);
@@ -481,6 +484,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.sel_ws, logits_select_ws_floats(R, 9));
   // key-chunk records: chunked launches have <= 16 queries per window (more use one chunk, no records)
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
+  P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
   P.add(&c.align_out, (size_t)B * T * 1500);
@@ -718,6 +722,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.qpart_stride = (long)R * dt;
     x.qpart_ld = dt;
     x.qbias = L.bcq;
+    x.xcnt = c.xa_cnt;
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
     S = gemm_p_part(c, c.dao, dt, L.wco, R, dt, dt);
     launch_reduce_ln(c.dt, c.part, S, L.bco, c.dx, L.ln3g, L.ln3b, c.dhb, R, dt, c.st);
@@ -807,6 +812,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.Tk = 1500;
       // prefill: one sequence per window; decode through this path: the beams of a window share it
       a.rows_per_win = f.prefill ? 1 : c.K;
+      a.xcnt = c.xa_cnt;
       launch_cross_attn(c.dt, a, c.xa_ws, c.st);
     }
     if (f.align) {
@@ -850,7 +856,7 @@ static void dec_logits(Ctx& c, const int* rows_idx, int n, bool ln_done = false)
   const int dt = m.d.n_text_state, V = m.d.n_vocab;
   WMX_CHECK(n <= c.logits_rows, "logits: too many rows");
   if (!ln_done) launch_layernorm_rows(c.dt, c.dx, rows_idx, m.lng, m.lnb, c.dhb, n, dt, c.st);
-  gemm_p(c, c.dhb, dt, m.tok_emb, n, V, dt, epi(EPI_STORE32, nullptr, c.logits, V));
+  gemm_p(c, c.dhb, dt, m.tok_emb, n, V, dt, epi(EPI_STORE32, nullptr, c.logits, c.ldl));
 }
 
 static void set_slot(Ctx& c, int v) {
@@ -947,7 +953,7 @@ static void run_step(Ctx& c, int B) {
   dec_logits(c, nullptr, f.rows, true);
   RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
               c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
-  launch_logits_select(c.logits, m.d.n_vocab, ro, c.rp, f.rows, c.K + (c.K > 1 ? 1 : 0), c.ctok, c.clp, nullptr,
+  launch_logits_select(c.logits, c.ldl, ro, c.rp, f.rows, c.K + (c.K > 1 ? 1 : 0), c.ctok, c.clp, nullptr,
                        c.sel_ws, c.st);
   if (c.K == 1)
     launch_greedy_update(c.rp, c.ctok, c.clp, f.rows, c.sp.timestamp_begin, c.sp.eot, c.hist, c.Tctx, c.slot, c.n_done,
@@ -1045,7 +1051,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     f.anc = nullptr;
     dec_forward(c, f);
     dec_logits(c, nullptr, B);
-    launch_lang_detect(c.logits, V, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st);
+    launch_lang_detect(c.logits, c.ldl, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st);
   }
   rec(c, 4);
 
@@ -1069,7 +1075,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     }
     WMX_HIP(hipMemcpyAsync(c.gather, g.data(), g.size() * 4, hipMemcpyHostToDevice, c.st));
     dec_logits(c, c.gather, 2 * B);
-    launch_token_prob(c.logits + (size_t)B * V, V, V, sp.no_speech, B, c.nospeech, c.st);
+    launch_token_prob(c.logits + (size_t)B * c.ldl, c.ldl, V, sp.no_speech, B, c.nospeech, c.st);
     sync(c);
   }
   // first selection from the prefill logits (rows of a window share their window's logits row)
@@ -1079,7 +1085,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   if (max_new > 0) {
     RuleOpts ro{V, sp.eot, sp.timestamp_begin, sp.no_timestamps, sp.blank, c.o.suppress_blank,
                 c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
-    launch_logits_select(c.logits, V, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, c.row_map, c.sel_ws, c.st);
+    launch_logits_select(c.logits, c.ldl, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, c.row_map, c.sel_ws, c.st);
     if (K == 1)
       launch_greedy_update(c.rp, c.ctok, c.clp, R, sp.timestamp_begin, sp.eot, c.hist, T, c.slot, c.n_done, c.st);
     else
@@ -1255,7 +1261,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
       for (int i = 0; i < n; ++i) g[i] = r0 + i;
       WMX_HIP(hipMemcpyAsync(c.gather, g.data(), n * 4, hipMemcpyHostToDevice, c.st));
       dec_logits(c, c.gather, n);
-      launch_text_prob(c.logits, V, sp.eot, c.a_target + r0, n, c.tprob + r0, c.st);
+      launch_text_prob(c.logits, c.ldl, sp.eot, c.a_target + r0, n, c.tprob + r0, c.st);
       sync(c);
     }
     std::vector<float> mat((size_t)B * Tn * 1500), tp((size_t)B * Tn);
@@ -1661,7 +1667,8 @@ wmx_status wmx_decoder_logits(wmx_ctx* x, const int32_t* tokens, const int32_t* 
       for (int i = 0; i < n; ++i) g[i] = r0 + i;
       WMX_HIP(hipMemcpyAsync(c.gather, g.data(), n * 4, hipMemcpyHostToDevice, c.st));
       dec_logits(c, c.gather, n);
-      WMX_HIP(hipMemcpyAsync(logits_out + (size_t)r0 * V, c.logits, (size_t)n * V * 4, hipMemcpyDeviceToHost, c.st));
+      WMX_HIP(hipMemcpy2DAsync(logits_out + (size_t)r0 * V, (size_t)V * 4, c.logits, (size_t)c.ldl * 4, (size_t)V * 4, n,
+                               hipMemcpyDeviceToHost, c.st));
       sync(c);
     }
     (void)lens;
@@ -1735,6 +1742,7 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.rows_per_win = c.K;
       by = (double)B * 1500 * 2 * dt * 2 + 2.0 * R * dt * 2;
       fl = 4.0 * R * 1500 * dt;
+      a.xcnt = c.xa_cnt;
       fn = [&c, a] { launch_cross_attn(c.dt, a, c.xa_ws, c.st); };
     } else if (kernel == 1) {
       const long rows = (long)B * 1500;

@@ -136,6 +136,7 @@ uint16_t *A, *W, *O;
 float* P;
 hipStream_t st;
 long wstride = 0;
+int g_rot = 8;
 
 template <int MT, int NCT, int KU, bool KSPLIT, int VAR = 0>
 void run(int M, int N, int K, int S) {
@@ -143,11 +144,11 @@ void run(int M, int N, int K, int S) {
   const int cols = KSPLIT ? 16 * NCT : 64 * NCT;
   const int tiles = (N + cols - 1) / cols;
   float us_p = timeit([&] {
-    const uint16_t* w = W + (it++ % 8) * wstride;
+    const uint16_t* w = W + (it++ % g_rot) * wstride;
     hipLaunchKernelGGL((part<MT, NCT, KU, KSPLIT, VAR>), dim3(tiles, S), dim3(256), 0, st, A, K, w, K, M, N, K, S, P);
   }, st);
-  printf("M=%3d N=%5d K=%4d MT=%2d NCT=%d KU=%d %s S=%3d WG=%6d VAR=%d: part %7.2f us (%6.0f GB/s)\n", M, N, K, MT,
-         NCT, KU, KSPLIT ? "ksplit" : "nsplit", S, tiles * S, VAR, us_p, 2.0 * N * K / us_p / 1e3);
+  printf("rot=%d M=%3d N=%5d K=%4d MT=%2d NCT=%d KU=%d %s S=%3d WG=%6d VAR=%d: part %7.2f us (%6.0f GB/s)\n", g_rot, M, N,
+         K, MT, NCT, KU, KSPLIT ? "ksplit" : "nsplit", S, tiles * S, VAR, us_p, 2.0 * N * K / us_p / 1e3);
 }
 
 int main() {
@@ -159,22 +160,14 @@ int main() {
   hipMalloc(&P, 64L * 256 * 5120 * 4);
   hipMemset(A, 0, 64L * 64 * 5120 * 2);
   hipMemset(W, 0x11, 8 * wstride * 2);
-#define SWEEP(MT, NCT, KU, M, N, K, S) \
-  run<MT, NCT, KU, true, 0>(M, N, K, S);  \
-  run<MT, NCT, KU, true, 1>(M, N, K, S);  \
-  run<MT, NCT, KU, true, 2>(M, N, K, S);  \
-  run<MT, NCT, KU, true, 3>(M, N, K, S);  \
-  run<MT, NCT, KU, true, 4>(M, N, K, S);
-  SWEEP(3, 2, 2, 40, 1280, 1280, 10)
-  SWEEP(3, 1, 2, 40, 1280, 1280, 10)
-  SWEEP(3, 2, 2, 40, 3840, 1280, 4)
-  SWEEP(3, 2, 2, 40, 5120, 1280, 4)
-  SWEEP(3, 2, 2, 40, 5120, 1280, 1)
-  SWEEP(3, 4, 2, 40, 1280, 5120, 10)
-  SWEEP(3, 2, 2, 40, 1280, 5120, 20)
-  SWEEP(3, 4, 2, 40, 51866, 1280, 1)
-  SWEEP(3, 8, 1, 40, 51866, 1280, 1)
-  SWEEP(1, 4, 4, 8, 1280, 1280, 10)
-  SWEEP(1, 8, 2, 8, 51866, 1280, 1)
+  for (int rot : {8, 1}) {
+    g_rot = rot;
+    run<3, 2, 2, true, 1>(40, 1280, 1280, 8);
+    run<3, 2, 2, true, 1>(40, 3840, 1280, 4);
+    run<3, 2, 2, true, 1>(40, 5120, 1280, 1);
+    run<3, 2, 2, true, 1>(40, 5120, 1280, 4);
+    run<3, 4, 2, true, 1>(40, 1280, 5120, 8);
+    run<3, 4, 2, true, 1>(40, 51866, 1280, 1);
+  }
   return 0;
 }

@@ -1,0 +1,66 @@
+"""HBM traffic per launch of the hot-path kernels from rocprofv3 PMC counters.
+
+Each counter gets its own rocprofv3 pass (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950), over
+`tools/kbench.py <kernel>` replaying one kernel.  FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: on gfx950 it
+reports half the bytes of a wide coalesced streaming read); WRITE_SIZE is taken as is.  Both are in KB.
+Writes a JSON summary (default profiles/r01_pmc_traffic.json) that bench.py reports as roofline.traffic.
+
+Run on the GPU box:  python tools/pmc_traffic.py cross_attn dec_fc1
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# kernel-name substrings of the timed launch (the helper launches of a replay are excluded)
+MATCH = {
+    "cross_attn": "dec_cross_attn_kernel",
+    "self_attn": "dec_self_attn_kernel",
+    "dec_fc1": "gemm_packed_kernel",
+    "enc_fc1": "gemm_kernel",
+    "enc_attn": "attn_flash_kernel",
+    "logmel": "logmel_raw_kernel",
+}
+
+
+def run_pass(kernel, counter, out_dir):
+    d = os.path.join(out_dir, f"{kernel}_{counter}")
+    cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.join(ROOT, "tools", "kbench.py"), kernel, "--iters", "10"]
+    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300)
+    vals = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if MATCH[kernel] in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]))
+    if not vals:
+        raise RuntimeError(f"no {counter} samples for {kernel}")
+    vals = vals[1:] if len(vals) > 1 else vals  # drop the warm-up launch
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kernels", nargs="+")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc"))
+    args = ap.parse_args()
+    res = {}
+    for k in args.kernels:
+        fetch_kb, n1 = run_pass(k, "FETCH_SIZE", args.work)
+        write_kb, n2 = run_pass(k, "WRITE_SIZE", args.work)
+        res[k] = {"fetch_bytes": 2.0 * fetch_kb * 1024, "write_bytes": write_kb * 1024,
+                  "traffic_bytes": 2.0 * fetch_kb * 1024 + write_kb * 1024,
+                  "launches": min(n1, n2), "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B"}
+        print(k, json.dumps(res[k]))
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
