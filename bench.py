@@ -169,6 +169,10 @@ def main():
             out.extend(f.result())
         return out
 
+    # in-situ probe: HIP events captured into each context's decode-step graph around the cross-attention launch
+    # of the middle decoder layer, sampled once per 8-step replay chunk during the timed decode loops
+    for c in ctxs:
+        c.set_probe("cross_attn", model.dims.n_text_layer // 2)
     for _ in range(args.warmup):
         step()
     if dist is not None:
@@ -219,6 +223,15 @@ def main():
         per_step_ms[k] = ms * counts[k]
     dom = max(per_step_ms, key=per_step_ms.get) if args.roofline_kernel == "auto" else args.roofline_kernel
     ms, by, fl = kern_stats[dom]
+    measured = "isolated replay (wmx_ctx_bench_kernel, HIP events, 20 launches)"
+    if dom == "cross_attn":
+        # the in-situ launches of the timed region (all context groups running concurrently)
+        st = [c.probe_stats() for c in ctxs]
+        n = sum(x[1] for x in st)
+        if n:
+            ms = sum(x[0] * x[1] for x in st) / n
+            by = st[0][2]
+            measured = f"in-situ, timed region: {n} sampled launches (layer {model.dims.n_text_layer // 2})"
     if dom in ("enc_fc1", "enc_attn"):
         ach = fl / (ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -227,15 +240,15 @@ def main():
         ach = by / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
-    # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py), if present
+    # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py) at this launch's batch
     pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_traffic.json")
     if os.path.exists(pmc):
-        rec = json.load(open(pmc)).get(dom)
-        if rec:
-            roof["traffic"] = round(rec["traffic_bytes"] / (1e9 if roof["unit"] == "GB/s" else 1.0) / (ms * 1e-3), 1) \
-                if roof["unit"] == "GB/s" else rec["traffic_bytes"]
+        rec = json.load(open(pmc)).get(f"{dom}@{Bg}")
+        if rec and roof["unit"] == "GB/s":
+            roof["traffic"] = round(rec["traffic_bytes"] / 1e9 / (ms * 1e-3), 1)
             roof["traffic_bytes_per_launch"] = rec["traffic_bytes"]
             roof["traffic_source"] = "profiles/r01_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
+    roof["measured"] = measured
     roof["kernel"] = dom
     roof["launch_ms"] = round(ms, 4)
     roof["algorithmic_per_launch"] = {"bytes": by, "flops": fl}

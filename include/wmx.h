@@ -172,6 +172,13 @@ int wmx_ctx_last_steps(wmx_ctx* c);
 wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float* avg_ms, double* bytes,
                                 double* flops);
 
+/* in-situ roofline probe: the launch of `kernel` (0 = decoder cross-attention) at decoder layer `layer` records
+ * its first workgroup start and last workgroup end (device wall clock, hipDeviceAttributeWallClockRate) at every
+ * decode step of the timed wmx_transcribe.  kernel < 0 disables the probe.  Stats of the last transcribe:
+ * average launch duration (ms), number of steps sampled, ALGORITHMIC bytes of one launch. */
+wmx_status wmx_ctx_set_probe(wmx_ctx* c, int kernel, int layer);
+wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -362,6 +362,12 @@ __global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(D
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
   const int nq = a.rows_per_win * a.Tn;
+  // in-situ probe: earliest workgroup start / latest workgroup end of this launch, wall-clock ticks
+  unsigned long long* probe = a.tprobe ? a.tprobe + 2 * (*a.slot0) : nullptr;
+  if (probe && tid == 0) atomicMin(probe, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  auto probe_end = [&] {
+    if (probe && tid == 0) atomicMax(probe + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  };
   const int i0 = qt * 16;  // first query (within the window) of this tile
   const int nqt = min(16, nq - i0);
   const int kc0 = ks * chunk, kc1 = min(a.Tk, kc0 + chunk);
@@ -533,7 +539,10 @@ __global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(D
       __hip_atomic_store(pr + 2 + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (KS == 1) return;
+  if (KS == 1) {
+    probe_end();
+    return;
+  }
   // ---- in-launch merge (cdna_hip_programming.md Guideline 16, sc1 form): every storing wave drains its
   //      write-through stores, one lane takes a ticket; the workgroup drawing KS-1 merges the records in chunk
   //      order with sc1 loads (no acquire fence needed) and re-arms the counter for the next launch ----
@@ -545,7 +554,10 @@ __global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(D
     sm[0][0] = old == KS - 1 ? 1.f : 0.f;
   }
   __syncthreads();
-  if (sm[0][0] == 0.f) return;
+  if (sm[0][0] == 0.f) {
+    probe_end();
+    return;
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // every record load is a buffer load with sc1 (aux 16): it bypasses this CU's L1, so no acquire is needed
   const float* wh = part + (long)(w * a.H + h) * KS * nq * 66;
@@ -578,6 +590,7 @@ __global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(D
     a.o[((long)w * nq + q) * a.d + h * 64 + e] = from_f32<T>(o2 / l);
   }
   if (tid == 0) __hip_atomic_store(cnt + w * a.H + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  probe_end();
 }
 
 // key chunk per workgroup; WMX_CROSS_CHUNK overrides the default for tuning runs

@@ -396,6 +396,11 @@ struct Ctx {
   int graph_B = -1;
   // profiling
   hipEvent_t ev[8];
+  // in-situ probe (wmx_ctx_set_probe): [slot][start, end] wall-clock ticks of the probed launch
+  int probe_kernel = -1, probe_layer = 0;
+  unsigned long long* probe_buf = nullptr;
+  double probe_sum_ms = 0, probe_bytes = 0, wall_khz = 0;
+  int probe_n = 0;
   float stage_ms[7] = {0};
   int last_steps = 0;
 };
@@ -485,6 +490,7 @@ static void alloc_ctx(Ctx& c) {
   // key-chunk records: chunked launches have <= 16 queries per window (more use one chunk, no records)
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
+  P.add(&c.probe_buf, (size_t)2 * T);
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
   P.add(&c.align_out, (size_t)B * T * 1500);
@@ -503,6 +509,11 @@ static void alloc_ctx(Ctx& c) {
     if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
   WMX_HIP(hipMemcpyAsync(c.mask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, c.st));
   for (auto& e : c.ev) WMX_HIP(hipEventCreate(&e));
+  {
+    int khz = 0;
+    WMX_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c.m->device));
+    c.wall_khz = khz;
+  }
   sync(c);
 }
 
@@ -723,6 +734,8 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.qpart_ld = dt;
     x.qbias = L.bcq;
     x.xcnt = c.xa_cnt;
+    x.slot0 = c.slot;
+    if (l == c.probe_layer && c.probe_kernel == 0) x.tprobe = c.probe_buf;
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
     S = gemm_p_part(c, c.dao, dt, L.wco, R, dt, dt);
     launch_reduce_ln(c.dt, c.part, S, L.bco, c.dx, L.ln3g, L.ln3b, c.dhb, R, dt, c.st);
@@ -1096,6 +1109,24 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   rec(c, 5);
   // ---- decode loop: one hipGraph replay per step ----
   const int need_done = K == 1 ? R : B;
+  c.probe_sum_ms = 0;
+  c.probe_n = 0;
+  if (c.probe_kernel >= 0) {  // start ticks = all ones (atomic min), end ticks = 0 (atomic max)
+    std::vector<unsigned long long> init((size_t)2 * T);
+    for (int i = 0; i < T; ++i) {
+      init[2 * i] = ~0ull;
+      init[2 * i + 1] = 0ull;
+    }
+    WMX_HIP(hipMemcpyAsync(c.probe_buf, init.data(), init.size() * 8, hipMemcpyHostToDevice, c.st));
+    sync(c);
+  }
+  {
+    const double dtm = m.d.n_text_state, mean_slot = 0.5 * (steps + max_new);
+    c.probe_bytes = c.probe_kernel == 0   ? (double)B * 1500 * 2 * dtm * 2 + 2.0 * R * dtm * 2
+                    : c.probe_kernel == 4 ? 4.0 * dtm * dtm * 2 + (double)R * dtm * 2 + (double)R * 4 * dtm * 2
+                    : c.probe_kernel == 5 ? (double)R * mean_slot * dtm * 2 * 2
+                                          : 0.0;
+  }
   hipGraphExec_t ge = nullptr;
   hipGraph_t gph = nullptr;
   if (c.o.use_graph && steps < max_new) {
@@ -1115,12 +1146,22 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     steps += chunk;
     WMX_HIP(hipMemcpyAsync(c.pinned_i, c.n_done, 4, hipMemcpyDeviceToHost, c.st));
     sync(c);
+
     if (c.pinned_i[0] >= need_done) break;
   }
   if (ge) WMX_HIP(hipGraphExecDestroy(ge));
   if (gph) WMX_HIP(hipGraphDestroy(gph));
   c.last_steps = steps;
   rec(c, 6);
+  if (c.probe_kernel >= 0) {
+    std::vector<unsigned long long> tk((size_t)2 * T);
+    WMX_HIP(hipMemcpy(tk.data(), c.probe_buf, tk.size() * 8, hipMemcpyDeviceToHost));
+    for (int i = 0; i < T; ++i)
+      if (tk[2 * i + 1] > tk[2 * i] && tk[2 * i] != ~0ull) {
+        c.probe_sum_ms += (double)(tk[2 * i + 1] - tk[2 * i]) / c.wall_khz;
+        c.probe_n += 1;
+      }
+  }
 
   // ---- read back and finalise (openai BeamSearchDecoder.finalize + MaximumLikelihoodRanker) ----
   std::vector<int> h((size_t)R * T), ns(R), done(R);
@@ -1714,6 +1755,24 @@ wmx_status wmx_ctx_stage_ms(wmx_ctx* x, float* out7) {
 }
 
 int wmx_ctx_last_steps(wmx_ctx* x) { return x->c.last_steps; }
+
+wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
+  return guard([&] {
+    WMX_CHECK(kernel < 0 || kernel == 0, "probe: only the decoder cross-attention (0) carries a probe");
+    WMX_CHECK(layer >= 0 && layer < x->c.m->d.n_text_layer, "probe: layer");
+    x->c.probe_kernel = kernel;
+    x->c.probe_layer = layer;
+  });
+}
+
+wmx_status wmx_ctx_probe_stats(wmx_ctx* x, float* avg_ms, int* n, double* bytes) {
+  return guard([&] {
+    const Ctx& c = x->c;
+    *n = c.probe_n;
+    *avg_ms = c.probe_n ? (float)(c.probe_sum_ms / c.probe_n) : 0.f;
+    *bytes = c.probe_bytes;
+  });
+}
 
 wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float* avg_ms, double* bytes, double* flops) {
   return guard([&] {

@@ -270,6 +270,18 @@ class Context:
 
     KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5}
 
+    def set_probe(self, kernel: str | None, layer: int = 0):
+        """Capture HIP events around one decode-step launch of `kernel` (cross_attn, dec_fc1, self_attn) at decoder
+        layer `layer`; every transcribe then samples that launch once per replay chunk inside its decode loop."""
+        k = -1 if kernel is None else self.KERNELS[kernel]
+        check(lib.wmx_ctx_set_probe(self._h, k, layer))
+
+    def probe_stats(self):
+        """(average in-situ launch duration ms, samples, algorithmic bytes of one launch) of the last transcribe."""
+        ms, n, by = C.c_float(), C.c_int(), C.c_double()
+        check(lib.wmx_ctx_probe_stats(self._h, C.byref(ms), C.byref(n), C.byref(by)))
+        return float(ms.value), int(n.value), float(by.value)
+
     def bench_kernel(self, kernel: str, batch: int, iters: int = 50):
         """Average launch duration (ms) of one hot-path kernel replayed on the context stream (HIP events),
         with its algorithmic bytes and flops per launch."""

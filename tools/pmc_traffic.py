@@ -27,10 +27,10 @@ MATCH = {
 }
 
 
-def run_pass(kernel, counter, out_dir):
-    d = os.path.join(out_dir, f"{kernel}_{counter}")
+def run_pass(kernel, counter, out_dir, batch):
+    d = os.path.join(out_dir, f"{kernel}_{batch}_{counter}")
     cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
-           sys.executable, os.path.join(ROOT, "tools", "kbench.py"), kernel, "--iters", "10"]
+           sys.executable, os.path.join(ROOT, "tools", "kbench.py"), kernel, "--iters", "10", "--batch", str(batch)]
     subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300)
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -46,17 +46,20 @@ def run_pass(kernel, counter, out_dir):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kernels", nargs="+")
+    ap.add_argument("--batch", type=int, nargs="+", default=[4, 8], help="windows per launch")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     res = {}
     for k in args.kernels:
-        fetch_kb, n1 = run_pass(k, "FETCH_SIZE", args.work)
-        write_kb, n2 = run_pass(k, "WRITE_SIZE", args.work)
-        res[k] = {"fetch_bytes": 2.0 * fetch_kb * 1024, "write_bytes": write_kb * 1024,
-                  "traffic_bytes": 2.0 * fetch_kb * 1024 + write_kb * 1024,
-                  "launches": min(n1, n2), "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B"}
-        print(k, json.dumps(res[k]))
+        for b in args.batch:
+            fetch_kb, n1 = run_pass(k, "FETCH_SIZE", args.work, b)
+            write_kb, n2 = run_pass(k, "WRITE_SIZE", args.work, b)
+            res[f"{k}@{b}"] = {"batch": b, "fetch_bytes": 2.0 * fetch_kb * 1024, "write_bytes": write_kb * 1024,
+                               "traffic_bytes": 2.0 * fetch_kb * 1024 + write_kb * 1024,
+                               "launches": min(n1, n2),
+                               "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B"}
+            print(k, b, json.dumps(res[f"{k}@{b}"]))
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1)
