@@ -351,13 +351,16 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 // KS > 1: each chunk writes a (max, sum, o[64]) record per query; dec_cross_combine merges them in order.
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxTk = kXS, kMaxSplits = 16;
+#ifndef WMX_XATTN_OCC
+#define WMX_XATTN_OCC 4  // waves per SIMD (4: best with two concurrent context groups, 3: best alone)
+#endif
 typedef __attribute__((address_space(1))) float gf32;
 
 // chunk records [nwin][H][KS][nq][66]; one arrival counter per (window, head) in DecAttnArgs::xcnt
 inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long)nwin * H * KS * nq * 66; }
 
 template <DT T, int KPW>
-__global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
+__global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z % KS, qt = blockIdx.z / KS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
@@ -375,66 +378,64 @@ __global__ __launch_bounds__(256, KPW <= 2 ? 3 : 1) void dec_cross_attn_kernel(D
   const int kw0 = kc0 + wave * per, kw1 = min(kc1, kw0 + per);
   const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
   const uint16_t* vbase = a.cv + (long)w * a.x_wstride + (long)h * a.x_hstride;
-  const long m_row = (long)w * nq + i0 + fr;  // query row held by this lane's column
-  const bool q_ok = fr < nqt;
 
   // ---- first batch of K / V^T loads (issued before the q reduction so their latency overlaps it) ----
   // K A-fragment of block b, pair u, dim half hh: key kb + 8*(fr>>2) + 4u + (fr&3), dims 32hh + 8g .. +8
   // V^T B-fragment of block b, dim block db: V^T[16db + fr][kb + 8g .. +8]
   u16x8 kf[KPW][2][2], vf[KPW][4];
+  // buffer loads: one 32-bit lane offset per image, the block / half / dim-block offsets in the scalar operand;
+  // keys past the image (kb + ... >= kXS) fall outside the descriptor's range and read as zeros
+  const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, (short)0, kXS * 64 * 2, 0x00020000);
+  const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, 64 * kXS * 2, 0x00020000);
+  const int kvoff = ((8 * (fr >> 2) + (fr & 3)) * 64 + 8 * g) * 2;
+  const int vvoff = (fr * kXS + 8 * g) * 2;
   auto load_batch = [&](int kb0) {
 #pragma unroll
     for (int b = 0; b < KPW; ++b) {
       const int kb = kb0 + 32 * b;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int key = min(kb + 8 * (fr >> 2) + 4 * u + (fr & 3), kXS - 1);
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
-          kf[b][u][hh] = *reinterpret_cast<const u16x8*>(kbase + (long)key * 64 + 32 * hh + 8 * g);
-      }
-      const int kk = min(kb + 8 * g, kXS - 8);
+          kf[b][u][hh] = __builtin_bit_cast(
+              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, kvoff, ((kb + 4 * u) * 64 + 32 * hh) * 2, 0));
 #pragma unroll
       for (int db = 0; db < 4; ++db)
-        vf[b][db] = *reinterpret_cast<const u16x8*>(vbase + (long)(16 * db + fr) * kXS + kk);
+        vf[b][db] = __builtin_bit_cast(
+            u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, vvoff, (16 * db * kXS + min(kb, kXS - 32)) * 2, 0));
     }
   };
   if (kw0 < kw1) load_batch(kw0);
 
-  // ---- Q^T B-fragments: lane (col q = fr, g): dims 32hh + 8g .. +8 ----
-  u16x8 qb[2];
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    u16x8 z = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (q_ok) {
-      const int col = h * 64 + 32 * hh + 8 * g;
+  // ---- the tile's queries into LDS (bf16/f16, rounded like the stored path), one element per thread:
+  //      q = bias + sum of the split-K partials in slice order, or the stored q ----
+  __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
+  for (int t = tid; t < 16 * 64; t += 256) {
+    const int q = t >> 6, e = t & 63;
+    uint16_t v = 0;
+    if (q < nqt) {
+      const long row = (long)w * nq + i0 + q;
+      const int col = h * 64 + e;
       if (a.qS > 0) {
-        // q = bias + sum of the split-K partials (slice order), rounded to the model dtype like the stored path
-        float p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        const float* src = a.qpart + m_row * a.qpart_ld + col;
-        for (int q0 = 0; q0 < a.qS; q0 += 4) {
-          float4 x0[4], x1[4];
+        const float* src = a.qpart + row * a.qpart_ld + col;
+        float tv[8];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const bool ok = q0 + u < a.qS;
-            const float* sp = src + (long)(ok ? q0 + u : 0) * a.qpart_stride;
-            x0[u] = ok ? *reinterpret_cast<const float4*>(sp) : make_float4(0, 0, 0, 0);
-            x1[u] = ok ? *reinterpret_cast<const float4*>(sp + 4) : make_float4(0, 0, 0, 0);
-          }
+        for (int u = 0; u < 8; ++u) tv[u] = u < a.qS ? src[u * a.qpart_stride] : 0.f;  // qS <= 8
+        float p = 0.f;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            p[0] += x0[u].x; p[1] += x0[u].y; p[2] += x0[u].z; p[3] += x0[u].w;
-            p[4] += x1[u].x; p[5] += x1[u].y; p[6] += x1[u].z; p[7] += x1[u].w;
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) z[e] = from_f32<T>(p[e] + (a.qbias ? a.qbias[col + e] : 0.f));
+        for (int u = 0; u < 8; ++u) p += tv[u];
+        v = from_f32<T>(p + (a.qbias ? a.qbias[col] : 0.f));
       } else {
-        z = *reinterpret_cast<const u16x8*>(a.q + m_row * a.q_ld + col);
+        v = a.q[row * a.q_ld + col];
       }
     }
-    qb[hh] = z;
+    qsh[q][e] = v;
   }
+  __syncthreads();
+  // Q^T B-fragments: lane (col q = fr, g): dims 32hh + 8g .. +8
+  u16x8 qb[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) qb[hh] = *reinterpret_cast<const u16x8*>(&qsh[fr][32 * hh + 8 * g]);
 
   // ---- online softmax over the wave's key range, P.V on MFMA ----
   float m_run = -INFINITY, l_run = 0.f;  // statistics of query fr (replicated over g)
