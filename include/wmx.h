@@ -172,6 +172,21 @@ int wmx_ctx_last_steps(wmx_ctx* c);
 wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float* avg_ms, double* bytes,
                                 double* flops);
 
+/* ---- pre-ASR DSP of the microphone loop, batched over B streams ----
+ * band-pass "vocal separation" (reference vocal_separation.py:335-358, SimpleFilterSeparator.separate):
+ * y = scipy.signal.filtfilt(b, a, x) with the caller's normalised coefficients (a[0] = 1, ntaps = len(b) = len(a)
+ * <= 17, zi = scipy.signal.lfilter_zi(b, a), ntaps - 1 values; padlen = 3 * ntaps).  Stream i has lens[i] samples
+ * at x + i * stride; y has the same layout.  fp64 recursion, as scipy. */
+wmx_status wmx_filtfilt(wmx_ctx* c, const float* x, int64_t stride, const int64_t* lens, int B, const double* b,
+                        const double* a, const double* zi, int ntaps, float* y);
+wmx_status wmx_filtfilt_device(wmx_ctx* c, const float* x_dev, int64_t stride, const int64_t* lens, int B,
+                               const double* b, const double* a, const double* zi, int ntaps, float* y_dev);
+/* audio-dedup features (reference audio_deduplicator.py:60-160, AudioDeduplicator._extract_features):
+ * out[i][0..4] = (rms, spectral centroid, zero-crossing rate, 85 % roll-off, bandwidth) / max|.| of stream i,
+ * lens[i] <= 8000 samples at sample rate sr.  The history / similarity decision stays on the host. */
+wmx_status wmx_dedup_features(wmx_ctx* c, const float* x, int64_t stride, const int64_t* lens, int B, float sr,
+                              float* out);
+
 /* in-situ roofline probe: the launch of `kernel` (0 = decoder cross-attention) at decoder layer `layer` records
  * its first workgroup start and last workgroup end (device wall clock, hipDeviceAttributeWallClockRate) at every
  * decode step of the timed wmx_transcribe.  kernel < 0 disables the probe.  Stats of the last transcribe:

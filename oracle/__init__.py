@@ -18,6 +18,12 @@ packages):
   normalise -> median filter 7 -> DTW) used for ``word_timestamps=True``
   (``asr_components.py:285``).
 
+* (``dsp_np``) the pre-ASR DSP of the microphone loop: scipy.signal.filtfilt of
+  the order-4 Butterworth band-pass (``vocal_separation.py:335-358``) and the
+  audio-dedup feature vector (``audio_deduplicator.py:60-160``), pinned against
+  the reference modules' own outputs (``tests/golden/make_dsp_golden.py`` imports
+  them; they need only numpy / scipy).
+
 Pinning: see ``tests/golden/make_golden.py`` — the log-mel, encoder, decoder
 logits, DTW and median filter are checked against transformers 5.15.0's
 independent Whisper implementation on seeded inputs / build-owned random

@@ -161,6 +161,18 @@ void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st);
 // raw cross-attention scores of selected heads (alignment): out [nh][R*Tn][Tk] f32
 void launch_cross_scores(DT dt, const DecAttnArgs& a, const int* heads_layer_local, int nh, float* out, hipStream_t st);
 
+// pre-ASR DSP (wmx_dsp.hip)
+constexpr int kMaxTaps = 17;      // filtfilt: up to an order-16 transfer function
+constexpr int kDedupMaxN = 8000;  // dedup features: samples per chunk (0.5 s at 16 kHz)
+struct IIRCoefs {
+  double b[kMaxTaps], a[kMaxTaps], zi[kMaxTaps - 1];
+  int ntaps, padlen;
+};
+void launch_filtfilt(const float* x, long xstride, const long* lens_dev, int B, const IIRCoefs& f, double* scratch,
+                     long sstride, float* y, long ystride, hipStream_t st);
+void launch_dedup_features(const float* x, long xstride, const long* lens_dev, int B, float sr, float* feats,
+                           hipStream_t st);
+
 // weights
 struct InitSpec {
   int tid;

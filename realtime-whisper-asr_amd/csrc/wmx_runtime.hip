@@ -396,6 +396,13 @@ struct Ctx {
   int graph_B = -1;
   // profiling
   hipEvent_t ev[8];
+  // pre-ASR DSP scratch (grown on demand, outside graphs)
+  double* dsp_scratch = nullptr;
+  size_t dsp_scratch_elems = 0;
+  float* dsp_io = nullptr;  // staging of host inputs / outputs
+  size_t dsp_io_elems = 0;
+  long* dsp_lens = nullptr;
+  int dsp_lens_cap = 0;
   // in-situ probe (wmx_ctx_set_probe): [slot][start, end] wall-clock ticks of the probed launch
   int probe_kernel = -1, probe_layer = 0;
   unsigned long long* probe_buf = nullptr;
@@ -1599,6 +1606,9 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       alloc_ctx(c);
     } catch (...) {
       if (c.buf) (void)hipFree(c.buf);
+  if (c.dsp_scratch) (void)hipFree(c.dsp_scratch);
+  if (c.dsp_io) (void)hipFree(c.dsp_io);
+  if (c.dsp_lens) (void)hipFree(c.dsp_lens);
       delete x;
       throw;
     }
@@ -1755,6 +1765,93 @@ wmx_status wmx_ctx_stage_ms(wmx_ctx* x, float* out7) {
 }
 
 int wmx_ctx_last_steps(wmx_ctx* x) { return x->c.last_steps; }
+
+// ---- pre-ASR DSP ----
+static void grow_bytes(void** p, size_t& cap, size_t need, size_t elem) {
+  if (need <= cap) return;
+  if (*p) WMX_HIP(hipFree(*p));
+  *p = nullptr;
+  WMX_HIP(hipMalloc(p, need * elem));
+  cap = need;
+}
+
+static void dsp_lens_upload(Ctx& c, const int64_t* lens, int B) {
+  if (B > c.dsp_lens_cap) {
+    if (c.dsp_lens) WMX_HIP(hipFree(c.dsp_lens));
+    c.dsp_lens = nullptr;
+    WMX_HIP(hipMalloc(&c.dsp_lens, (size_t)B * sizeof(long)));
+    c.dsp_lens_cap = B;
+  }
+  std::vector<long> l(lens, lens + B);
+  WMX_HIP(hipMemcpyAsync(c.dsp_lens, l.data(), (size_t)B * sizeof(long), hipMemcpyHostToDevice, c.st));
+  sync(c);  // l goes out of scope
+}
+
+static void filtfilt_dev(Ctx& c, const float* x, long stride, const int64_t* lens, int B, const double* b,
+                         const double* a, const double* zi, int ntaps, float* y) {
+  WMX_CHECK(B >= 1 && ntaps >= 2 && ntaps <= kMaxTaps, "filtfilt: batch / filter order");
+  IIRCoefs f{};
+  for (int i = 0; i < ntaps; ++i) {
+    f.b[i] = b[i];
+    f.a[i] = a[i];
+  }
+  for (int i = 0; i + 1 < ntaps; ++i) f.zi[i] = zi[i];
+  f.ntaps = ntaps;
+  f.padlen = 3 * ntaps;
+  long mx = 0;
+  for (int i = 0; i < B; ++i) {
+    WMX_CHECK(lens[i] >= 0 && lens[i] <= stride, "filtfilt: length exceeds stride");
+    WMX_CHECK(lens[i] == 0 || lens[i] > f.padlen, "filtfilt: input shorter than padlen (scipy raises)");
+    mx = std::max<long>(mx, lens[i]);
+  }
+  const long sstride = mx + 2L * f.padlen;
+  grow_bytes((void**)&c.dsp_scratch, c.dsp_scratch_elems, (size_t)B * sstride, sizeof(double));
+  dsp_lens_upload(c, lens, B);
+  launch_filtfilt(x, stride, c.dsp_lens, B, f, c.dsp_scratch, sstride, y, stride, c.st);
+}
+
+wmx_status wmx_filtfilt_device(wmx_ctx* x, const float* x_dev, int64_t stride, const int64_t* lens, int B,
+                               const double* b, const double* a, const double* zi, int ntaps, float* y_dev) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_HIP(hipSetDevice(c.m->device));
+    filtfilt_dev(c, x_dev, (long)stride, lens, B, b, a, zi, ntaps, y_dev);
+    sync(c);
+  });
+}
+
+wmx_status wmx_filtfilt(wmx_ctx* x, const float* xh, int64_t stride, const int64_t* lens, int B, const double* b,
+                        const double* a, const double* zi, int ntaps, float* y) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_HIP(hipSetDevice(c.m->device));
+    WMX_CHECK(B >= 1 && stride >= 1, "filtfilt: batch");
+    const size_t n = (size_t)B * stride;
+    grow_bytes((void**)&c.dsp_io, c.dsp_io_elems, 2 * n, sizeof(float));
+    WMX_HIP(hipMemcpyAsync(c.dsp_io, xh, n * 4, hipMemcpyHostToDevice, c.st));
+    filtfilt_dev(c, c.dsp_io, (long)stride, lens, B, b, a, zi, ntaps, c.dsp_io + n);
+    WMX_HIP(hipMemcpyAsync(y, c.dsp_io + n, n * 4, hipMemcpyDeviceToHost, c.st));
+    sync(c);
+  });
+}
+
+wmx_status wmx_dedup_features(wmx_ctx* x, const float* xh, int64_t stride, const int64_t* lens, int B, float sr,
+                              float* out) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_HIP(hipSetDevice(c.m->device));
+    WMX_CHECK(B >= 1 && stride >= 1 && sr > 0, "dedup features: batch / rate");
+    for (int i = 0; i < B; ++i)
+      WMX_CHECK(lens[i] >= 0 && lens[i] <= stride && lens[i] <= kDedupMaxN, "dedup features: chunk length");
+    const size_t n = (size_t)B * stride;
+    grow_bytes((void**)&c.dsp_io, c.dsp_io_elems, n + (size_t)B * 5, sizeof(float));
+    WMX_HIP(hipMemcpyAsync(c.dsp_io, xh, n * 4, hipMemcpyHostToDevice, c.st));
+    dsp_lens_upload(c, lens, B);
+    launch_dedup_features(c.dsp_io, (long)stride, c.dsp_lens, B, sr, c.dsp_io + n, c.st);
+    WMX_HIP(hipMemcpyAsync(out, c.dsp_io + n, (size_t)B * 5 * 4, hipMemcpyDeviceToHost, c.st));
+    sync(c);
+  });
+}
 
 wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
   return guard([&] {

@@ -55,6 +55,7 @@ EXPORTS = [
     "wmx_ctx_stream", "wmx_logmel", "wmx_logmel_device", "wmx_encode", "wmx_encode_device",
     "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device", "wmx_result_free",
     "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats",
+    "wmx_filtfilt", "wmx_filtfilt_device", "wmx_dedup_features",
 ]
 
 
@@ -91,6 +92,11 @@ def _load():
         "wmx_ctx_stage_ms": (C.c_int, [VP, P(F)]),
         "wmx_ctx_last_steps": (C.c_int, [VP]),
         "wmx_ctx_set_probe": (C.c_int, [VP, C.c_int, C.c_int]),
+        "wmx_filtfilt": (C.c_int, [VP, P(F), I64, P(I64), C.c_int, P(C.c_double), P(C.c_double), P(C.c_double),
+                                   C.c_int, P(F)]),
+        "wmx_filtfilt_device": (C.c_int, [VP, VP, I64, P(I64), C.c_int, P(C.c_double), P(C.c_double),
+                                          P(C.c_double), C.c_int, VP]),
+        "wmx_dedup_features": (C.c_int, [VP, P(F), I64, P(I64), C.c_int, F, P(F)]),
         "wmx_ctx_probe_stats": (C.c_int, [VP, P(F), P(C.c_int), P(C.c_double)]),
         "wmx_ctx_bench_kernel": (C.c_int, [VP, C.c_int, C.c_int, C.c_int, P(F), P(C.c_double), P(C.c_double)]),
     }
@@ -126,3 +132,8 @@ def iptr(a: np.ndarray):
 def lptr(a: np.ndarray):
     assert a.dtype == np.int64 and a.flags.c_contiguous
     return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_double))
