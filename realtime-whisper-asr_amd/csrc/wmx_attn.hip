@@ -344,7 +344,7 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 //
 // Per wave, per 32-key block kb: S^T = K.Q^T on MFMA with the block's keys permuted so that lane (q = l&15,
 // g = l>>4) ends up holding the scores of keys kb + 8g + 0..7 for query q -- exactly the A-operand layout of
-// the following P.V MFMA (A = P[16 q][32 keys]).  B of P.V is V^T[dim][kb + 8g .. +8]: one contiguous 16-B
+// the following P.V MFMA (A = P[16 q][32 keys]).  B of P.V is V^T[dim][kb + 8g .. +8]: one 16-B
 // load per lane from the transposed V image.  Softmax statistics are per lane (q = l&15) plus two xor
 // shuffles across the four 16-lane groups; P goes to the MFMA as bf16/f16 hi + lo halves (two MFMAs), so
 // the probabilities keep ~16 mantissa bits.  No LDS until the 4-wave combine at the end.
@@ -387,22 +387,21 @@ __global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_a
   // keys past the image (kb + ... >= kXS) fall outside the descriptor's range and read as zeros
   const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, (short)0, kXS * 64 * 2, 0x00020000);
   const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, 64 * kXS * 2, 0x00020000);
-  const int kvoff = ((8 * (fr >> 2) + (fr & 3)) * 64 + 8 * g) * 2;
-  const int vvoff = (fr * kXS + 8 * g) * 2;
+  // fragment-major images (crossk_off / crossv_off): every load below is one contiguous 1 KiB wave piece
+  const int loff = lane * 16;
   auto load_batch = [&](int kb0) {
 #pragma unroll
     for (int b = 0; b < KPW; ++b) {
-      const int kb = kb0 + 32 * b;
+      const int kbi = (kb0 >> 5) + b;  // 32-key block index (blocks past the image read as zeros)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
           kf[b][u][hh] = __builtin_bit_cast(
-              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, kvoff, ((kb + 4 * u) * 64 + 32 * hh) * 2, 0));
+              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, loff, ((kbi * 2 + u) * 2 + hh) * 1024, 0));
 #pragma unroll
       for (int db = 0; db < 4; ++db)
-        vf[b][db] = __builtin_bit_cast(
-            u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, vvoff, (16 * db * kXS + min(kb, kXS - 32)) * 2, 0));
+        vf[b][db] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, loff, (kbi * 4 + db) * 1024, 0));
     }
   };
   if (kw0 < kw1) load_batch(kw0);
@@ -617,6 +616,7 @@ static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
   const int KS = (a.Tk + chunk - 1) / chunk;
   const int QT = (nq + 15) / 16;
   WMX_CHECK(KS <= kMaxSplits, "cross attn: too many key chunks");
+  WMX_CHECK(KS == 1 || chunk % 32 == 0, "cross attn: key chunks must be whole 32-key blocks");
   WMX_CHECK(KS == 1 || (ws != nullptr && a.xcnt != nullptr && nq <= 16), "cross attn: split workspace required");
   dim3 grid(a.H, nwin, KS * QT);
   const int per_wave = ((chunk + 3) / 4 + 31) / 32;  // 32-key blocks per wave
@@ -651,11 +651,10 @@ __global__ __launch_bounds__(256) void cross_scores_kernel(DecAttnArgs a, const 
   __syncthreads();
   const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
   for (int s = threadIdx.x; s < a.Tk; s += 256) {
-    const uint16_t* kp = kbase + (long)s * 64;
     float acc = 0.f;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const u16x8 kv = *reinterpret_cast<const u16x8*>(kp + c * 8);
+      const u16x8 kv = *reinterpret_cast<const u16x8*>(kbase + crossk_off(s, c * 8));
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc += qs[c * 8 + e] * to_f32<T>(kv[e]);
     }

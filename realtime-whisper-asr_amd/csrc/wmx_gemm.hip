@@ -15,13 +15,14 @@
 
 namespace wmx {
 
-// K: [L][xw][H][kXS][64] (key rows), V: [L][xw][H][64][kXS] (V^T, key-contiguous): each (window, head) is one
-// contiguous stream for the decode step, and V^T rows are the MFMA B operand of P.V without a transpose
+// K and V^T of [L][xw][H] (window, head) images, each kXS x 64 in the fragment-major order of crossk_off /
+// crossv_off (wmx_kernels.h): each (window, head) is one contiguous stream for the decode step, read as whole
+// 1 KiB pieces that are already the MFMA operands of S^T = K.Q^T and P.V
 __device__ inline long crosskv_index(const Epi& e, int m, int n) {
   const int w = m / e.xt, t = m - w * e.xt;
   const int lk = n / e.d, c = n - lk * e.d;
   const long base = (((long)lk * e.xw + w) * (e.d >> 6) + (c >> 6)) * 64 * kXS;
-  return (lk & 1) ? base + (long)(c & 63) * kXS + t : base + (long)t * 64 + (c & 63);
+  return base + ((lk & 1) ? crossv_off(t, c & 63) : crossk_off(t, c & 63));
 }
 
 template <DT T>
@@ -284,6 +285,275 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Large-M GEMM (encoder projections, conv front end, cross-K/V): 256 x 256 tile, 8 waves (2 M x 4 N, wave tile
+// 128 x 64 = 8 x 4 MFMA fragments), K staged in 32-deep slices through a 4-slot LDS ring (32 KiB per slot) filled
+// by global_load_lds_dwordx4.  Up to three slices stay in flight across raw s_barriers: each slice is waited
+// for with a COUNTED vmcnt (cdna_hip_programming.md §5 "Pipelining across barriers"), never vmcnt(0) and never
+// __syncthreads() inside the loop.  All LDS is one extern array (§5 item 4(a)).
+// LDS rows are 64 B (32 k); the 16-B piece p of row r sits at p ^ ((r >> 2) & 3), so a ds_read_b128 of 16
+// consecutive rows touches 16 distinct 16-B slots (conflict-free); the swizzle is applied on the global SOURCE
+// address, the LDS image stays lane-linear (rule 21).
+// ------------------------------------------------------------------------------------------------
+// microbenchmark ablations (tools/mb_gemm256.hip): 1 = no MFMA, 2 = no DMA; the library builds mode 0
+#ifndef WMX_G256_MODE
+#define WMX_G256_MODE 0
+#endif
+#if WMX_G256_MODE == 1
+#define WMX_G256_MFMA(a, b, c) ((c) + __builtin_bit_cast(f32x4, (a) ^ (b)))
+#else
+#define WMX_G256_MFMA(a, b, c) mfma16<T>(a, b, c)
+#endif
+constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
+constexpr int kG256Lds = 4 * kG256Slot;     // 128 KiB
+
+// apply the epilogue to `rows` rows of an fp32 LDS image [rows][ldt] holding output rows mb.. and columns n0..n0+BN
+template <DT T, int BN, int NT>
+__device__ inline void epi_from_image(const Epi& e, const float* img, int ldt, int rows, int mb, int n0, int M, int N,
+                                      int tid) {
+  if (e.kind == EPI_CROSSKV && ((n0 / e.d) & 1)) {
+    // V^T tile (the host checks d % BN == 0, xt % 4 == 0): 4 consecutive keys of one column per 8-byte store
+    for (int idx = tid; idx < rows / 4 * BN; idx += NT) {
+      const int col = idx % BN, r4 = (idx / BN) * 4;
+      const int m = mb + r4, n = n0 + col;
+      if (m >= M || n >= N) continue;
+      const float b = e.bias ? e.bias[n] : 0.f;
+      u16x4 h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h[q] = from_f32<T>(img[(r4 + q) * ldt + col] + b);
+      *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)) = h;
+    }
+    return;
+  }
+  for (int idx = tid; idx < rows * BN / 4; idx += NT) {
+    const int row = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
+    const int m = mb + row, n = n0 + c4;
+    if (m >= M || n >= N) continue;
+    const float4 v = *reinterpret_cast<const float4*>(img + row * ldt + c4);
+    if (n + 3 < N && (e.ldc & 3) == 0) {
+      epi_store4<T>(e, m, n, v);
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int q = 0; q < 4 && n + q < N; ++q) epi_store<T>(e, m, n + q, vv[q]);
+    }
+  }
+}
+
+// fast form of epi_from_image for a 64-row x 256-column image and 512 threads: a thread owns one column quad
+// and rows r0, r0 + 8, ... (r0 = tid / 64): the bias is loaded once, and every row's loads (image, residual,
+// position) are issued before its stores, so the store tail is not a chain of dependent global round trips.
+template <DT T, int KIND>
+__device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid) {
+  const int c4 = (tid & 63) * 4, r0 = tid >> 6;
+  const int n = n0 + c4;
+  if (n >= N) return;
+  float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e.bias) b = *reinterpret_cast<const float4*>(e.bias + n);
+  float4 v[8], aux[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int row = r0 + 8 * u, m = mb + row;
+    v[u] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
+    v[u] = make_float4(v[u].x + b.x, v[u].y + b.y, v[u].z + b.z, v[u].w + b.w);
+    if (KIND == EPI_RESID32 && m < M)
+      aux[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
+    if (KIND == EPI_GELU_POS32 && m < M)
+      aux[u] = *reinterpret_cast<const float4*>(e.pos + (long)(m % e.posT) * e.ldc + n);
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = mb + r0 + 8 * u;
+    if (m >= M) continue;
+    float4 x = v[u];
+    if (KIND == EPI_GELU16 || KIND == EPI_GELU_POS32)
+      x = make_float4(gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w));
+    if (KIND == EPI_RESID32 || KIND == EPI_GELU_POS32)
+      x = make_float4(x.x + aux[u].x, x.y + aux[u].y, x.z + aux[u].z, x.w + aux[u].w);
+    if (KIND == EPI_STORE16 || KIND == EPI_GELU16 || KIND == EPI_CROSSKV) {
+      const u16x4 h = {from_f32<T>(x.x), from_f32<T>(x.y), from_f32<T>(x.z), from_f32<T>(x.w)};
+      uint16_t* dst = KIND == EPI_CROSSKV ? reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)
+                                          : reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n;
+      *reinterpret_cast<u16x4*>(dst) = h;
+    } else {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n) = x;
+    }
+  }
+}
+
+template <DT T>
+__device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid) {
+  const bool vec = (N & 3) == 0 && (e.ldc & 3) == 0;
+  const bool kpart = e.kind == EPI_CROSSKV && ((n0 / e.d) & 1) == 0;  // K image: row-major 64-wide head rows
+  if (vec || kpart) {
+    switch (e.kind) {
+      case EPI_STORE16: epi_rows64<T, EPI_STORE16>(e, img, ldt, mb, n0, M, N, tid); return;
+      case EPI_GELU16: epi_rows64<T, EPI_GELU16>(e, img, ldt, mb, n0, M, N, tid); return;
+      case EPI_RESID32: epi_rows64<T, EPI_RESID32>(e, img, ldt, mb, n0, M, N, tid); return;
+      case EPI_GELU_POS32: epi_rows64<T, EPI_GELU_POS32>(e, img, ldt, mb, n0, M, N, tid); return;
+      case EPI_STORE32: epi_rows64<T, EPI_STORE32>(e, img, ldt, mb, n0, M, N, tid); return;
+      case EPI_CROSSKV:
+        if (kpart) {
+          epi_rows64<T, EPI_CROSSKV>(e, img, ldt, mb, n0, M, N, tid);
+          return;
+        }
+        break;
+      default: break;
+    }
+  }
+  epi_from_image<T, 256, 512>(e, img, ldt, 64, mb, n0, M, N, tid);
+}
+
+template <DT T>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ W, long ldw, int M, int N, int K,
+                                                         Epi e) {
+  constexpr int BM = 256, BN = 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tilesN = (N + BN - 1) / BN;
+  const int tilesM = (M + BM - 1) / BM;
+  const int nwg = tilesN * tilesM;
+  int bid = blockIdx.x;
+  {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles (row panels share its L2)
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int tm = bid / tilesN, tn = bid - tm * tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nk = K >> 5;
+
+  // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
+  // Wave w issues pieces w, w + 8, w + 16, w + 24; lane l covers row l >> 2, 16-B column (l & 3).
+  const int srow = lane >> 2;
+  const int scol = ((lane & 3) ^ ((srow >> 2) & 3)) * 8;  // source k offset of this lane's swizzled piece
+  const uint16_t* src[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pc = wave + 8 * j;
+    if (pc < 16) {
+      src[j] = A + (long)min(m0 + pc * 16 + srow, M - 1) * lda + scol;
+    } else {
+      src[j] = W + (long)min(n0 + (pc - 16) * 16 + srow, N - 1) * ldw + scol;
+    }
+  }
+  // half h of slice kt: pieces 2h, 2h + 1 of this wave (h = 0: A rows, h = 1: W rows)
+  auto issue_half = [&](int kt, int h) {
+#if WMX_G256_MODE == 2
+    return;
+#endif
+    char* slot = smem + (kt & 3) * kG256Slot;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * h + jj;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + kt * 32),
+                                       (__attribute__((address_space(3))) void*)(slot + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+  auto issue = [&](int kt) {
+    issue_half(kt, 0);
+    issue_half(kt, 1);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int piece = (fq ^ (fr >> 2)) << 4;
+  const int aoff = (wm * 128 + fr) * 64 + piece;
+  const int boff = BM * 64 + (wn * 64 + fr) * 64 + piece;
+
+  // Ping-pong schedule (cdna_hip_programming.md §5 256² template, T3+T4+T5): every 32-deep slice is two phases;
+  // a phase is [memory segment] s_barrier [16-MFMA segment] s_barrier.  Waves 4..7 (wave row 1) run one barrier
+  // behind waves 0..3, so on every SIMD one wave computes while its partner reads LDS / issues DMA.
+  //   phase A of slice t: ds_read B frags 0..3 + A frags 0..3; issue the A half of slice t + 3 into slot (t-1)&3
+  //                       (every memory segment retires its ds_reads with lgkmcnt(0) BEFORE its barrier, so the
+  //                       lagging half's last reads of slice t-1 are done before the leading half restages it)
+  //   phase B of slice t: wait (counted vmcnt) for slice t + 1; ds_read A frags 4..7; issue the W half of t + 3
+  // The wait in phase B of slice t precedes, by at least one barrier, every wave's first read of slice t + 1.
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  if (nk > 2)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  if (lagging) __builtin_amdgcn_s_barrier();
+  u16x8 af[4], bfr[4];
+  for (int t = 0; t < nk; ++t) {
+    const char* S = smem + (t & 3) * kG256Slot;
+    // ---- phase A ----
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const u16x8*>(S + boff + j * 1024);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + i * 1024);
+    if (t + 3 < nk) issue_half(t + 3, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase B ----
+    // slice t + 1 is complete once only slice t + 2 (4 DMAs) and the first half of t + 3 (2) may be outstanding
+    if (t + 3 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (t + 2 < nk)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + (i + 4) * 1024);
+    if (t + 3 < nk) issue_half(t + 3, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i + 4][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i + 4][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (!lagging) __builtin_amdgcn_s_barrier();
+  __syncthreads();
+
+  // epilogue: 4 rounds of 64 rows through an fp32 LDS image [64][BN + 4]
+  constexpr int LDT = BN + 4;
+  float* img = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int rd = 0; rd < 4; ++rd) {
+    if (wm == (rd >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = (rd & 1) * 4 + ii;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) img[(ii * 16 + fq * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
+      }
+    }
+    __syncthreads();
+    epi_image64<T>(e, img, LDT, m0 + rd * 64, n0, M, N, tid);
+    __syncthreads();
+  }
+}
+
 template <DT T>
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(const float* __restrict__ ws, int splits, int M, int N,
                                                           Epi e) {
@@ -398,6 +668,10 @@ void gemm_init_attributes() {
   skinny_attr<DT::F16, 8, 8>();
   skinny_attr<DT::F16, 12, 4>();
   skinny_attr<DT::F16, 16, 4>();
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm256_kernel<DT::BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kG256Lds));
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm256_kernel<DT::F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kG256Lds));
   done = true;
 }
 
@@ -586,6 +860,14 @@ template <DT T>
 static void launch_t(const GemmCall& g, hipStream_t st) {
   if (g.tile == TILE_SKINNY) {
     launch_skinny<T>(g, st);
+    return;
+  }
+  if (g.tile == TILE_256) {
+    WMX_CHECK(g.K % 32 == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm256: K / leading dimensions");
+    WMX_CHECK(g.epi.kind != EPI_CROSSKV || (g.epi.d % 256 == 0 && g.epi.xt % 4 == 0), "gemm256: cross K/V shape");
+    const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+    hipLaunchKernelGGL((gemm256_kernel<T>), dim3(tiles), dim3(512), kG256Lds, st, g.A, g.lda, g.W, g.ldw, g.M, g.N,
+                       g.K, g.epi);
     return;
   }
   WMX_CHECK(g.K % 64 == 0, "gemm: K must be a multiple of 64");

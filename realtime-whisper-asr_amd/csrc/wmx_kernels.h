@@ -33,7 +33,26 @@ struct Epi {
 // padded key stride of the cross K/V images (a multiple of 32 keys; the pad stays zero)
 constexpr int kXS = 1504;
 
-enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3 };
+// Cross K / V^T images of one (layer, window, head): kXS keys x 64 dims each, stored MFMA-fragment-major so that
+// every wave-instruction of the decode cross attention streams one contiguous, lane-linear 1 KiB piece.
+// K (A operand of S^T = K.Q^T): 32-key block kb, pair u, dim half hh, lane l = fr + 16g holds dims 32hh + 8g .. +8
+//   of key 32kb + 8(fr >> 2) + 4u + (fr & 3)          -> element ((((kb*2 + u)*2 + hh)*64 + l) * 8 + j
+// V^T (B operand of P.V): block kb, dim block db, lane l = fr + 16g holds keys 32kb + 8g .. +8 of dim 16db + fr
+//                                                    -> element (((kb*4 + db)*64 + l) * 8 + j
+// Four consecutive dims (K) or four consecutive keys (V^T) starting at a multiple of 4 are contiguous.
+__host__ __device__ inline long crossk_off(int t, int c) {
+  const int kb = t >> 5, tt = t & 31;
+  const int u = (tt >> 2) & 1, fr = ((tt >> 3) << 2) | (tt & 3);
+  const int hh = c >> 5, g = (c >> 3) & 3;
+  return ((((long)kb * 2 + u) * 2 + hh) * 64 + fr + 16 * g) * 8 + (c & 7);
+}
+__host__ __device__ inline long crossv_off(int t, int c) {
+  const int kb = t >> 5, g = (t >> 3) & 3;
+  const int db = c >> 4, fr = c & 15;
+  return (((long)kb * 4 + db) * 64 + fr + 16 * g) * 8 + (t & 7);
+}
+
+enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3, TILE_256 = 4 };
 
 struct GemmCall {
   const uint16_t* A;
@@ -136,8 +155,8 @@ struct DecAttnArgs {
   const int* slot0;    // device scalar: slot of the first new token
   int kv_R;            // row stride of the KV cache ([slot][kv_R][d]); >= R
   // cross
-  // cross K/V of one layer, head-major: K[t][e] of (window w, head h) at ck + w*x_wstride + h*x_hstride + t*64,
-  // V^T[e][t] at cv + w*x_wstride + h*x_hstride + e*kXS + t
+  // cross K/V of one layer, head-major: the (window w, head h) image starts at ck / cv + w*x_wstride + h*x_hstride;
+  // inside it K[t][e] sits at crossk_off(t, e) and V^T[e][t] at crossv_off(t, e) (fragment-major, see above)
   const uint16_t* ck;
   const uint16_t* cv;
   long x_wstride, x_hstride;
