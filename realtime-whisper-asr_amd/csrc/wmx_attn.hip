@@ -186,7 +186,223 @@ void launch_attn_flash(DT dt, const AttnArgs& a, int causal, int causal_off, con
   WMX_HIP(hipGetLastError());
 }
 
-void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) { launch_attn_flash(dt, a, 0, 0, nullptr, st); }
+// ------------------------------------------------------------------------------------------------
+// Encoder self attention (non-causal, head_dim 64) on v_mfma_f32_32x32x16.  Workgroup = 4 waves x 32 queries
+// of one (window, head); K/V tiles of 64 keys arrive by LDS-DMA (global_load_lds_dwordx4, double-buffered,
+// the next tile in flight across the single barrier of each step).
+//   S^T = K.Q^T: lane (c = l&31, h = l>>5) holds 16 scores of query c per 32-key block (keys
+//     (r&3) + 8(r>>2) + 4h), so the row max is in-lane plus one permlane32_swap.
+//   O^T += V^T.P^T takes the exponentiated scores straight from the accumulator registers as its B operand
+//     (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand"): no LDS round trip for P;
+//     the V^T operand comes from the row-major V tile by ds_read_b64_tr_b16 (T10).
+// Both LDS tiles are [64 keys][64 dims] with 16-B chunk c of row r stored at c ^ (r & 7) (swizzle applied on
+// the DMA source address, the LDS image stays lane-linear).
+// ------------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+template <DT T> __device__ inline f32x16 mfma32(const u16x8& a, const u16x8& b, f32x16 c);
+template <> __device__ inline f32x16 mfma32<DT::BF16>(const u16x8& a, const u16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                 0);
+}
+template <> __device__ inline f32x16 mfma32<DT::F16>(const u16x8& a, const u16x8& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// max of v over lanes l and l ^ 32: v_permlane32_swap exchanges the two 32-lane halves between its two
+// operands, so of its two results one is this lane's value and the other the partner's, in either order
+__device__ inline float max_pair32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(v, fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
+}
+
+// eight f32 -> eight bf16 / f16 with the hardware round-to-nearest-even converts (v_cvt_pk_bf16_f32)
+// (elements o .. o + 7 of a 16-float accumulator)
+template <DT T> __device__ inline u16x8 pack8(const f32x16& v, int o);
+template <> __device__ inline u16x8 pack8<DT::BF16>(const f32x16& v, int o) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[o + j];
+  return __builtin_bit_cast(u16x8, r);
+}
+template <> __device__ inline u16x8 pack8<DT::F16>(const f32x16& v, int o) {
+  f16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (_Float16)v[o + j];
+  return __builtin_bit_cast(u16x8, r);
+}
+
+constexpr int kEncTile = 64;                       // keys per step
+constexpr int kEncTileBytes = kEncTile * 64 * 2;   // one K or V tile
+template <DT T>
+__global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = lane & 31, hl = lane >> 5;
+  __shared__ __attribute__((aligned(16))) char lds[4 * kEncTileBytes];  // [buf][K | V]
+  const uint16_t* qb = a.q + (long)b * a.q_bstride + (long)h * a.head_stride;
+  const uint16_t* kb = a.k + (long)b * a.k_bstride + (long)h * a.head_stride;
+  const uint16_t* vb = a.v + (long)b * a.v_bstride + (long)h * a.head_stride;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int Tk = a.Tk;
+  const int ntiles = (Tk + kEncTile - 1) / kEncTile;
+
+  // DMA staging: a tile is 8 pieces of 1 KiB (8 rows x 128 B); wave w stages K pieces w, w+4 and V pieces w, w+4.
+  // Lane l covers row l >> 3 of its piece and reads source chunk (l & 7) ^ (row & 7).
+  const int srow = lane >> 3;
+  const int schunk = ((lane & 7) ^ srow) * 8;  // (row & 7) == srow for 8-row pieces
+  auto stage = [&](int t, int buf) {
+    char* kd = lds + buf * 2 * kEncTileBytes;
+    char* vd = kd + kEncTileBytes;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = wave + 4 * i;
+      const int key = min(t * kEncTile + piece * 8 + srow, Tk - 1);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + (long)key * a.k_ld + schunk),
+                                       (__attribute__((address_space(3))) void*)(kd + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(vb + (long)key * a.v_ld + schunk),
+                                       (__attribute__((address_space(3))) void*)(vd + piece * 1024), 16, 0, 0);
+    }
+  };
+  stage(0, 0);
+
+  // Q^T fragments (B operand): lane holds Q[q0 + c][16s + 8hl .. +8] for dim steps s = 0..3
+  u16x8 qf[4];
+  {
+    const int q = min(q0 + c, a.Tq - 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) qf[s2] = *reinterpret_cast<const u16x8*>(qb + (long)q * a.q_ld + 16 * s2 + 8 * hl);
+  }
+  f32x16 o[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const float C = 0.125f * kLog2e;
+
+  // per-lane LDS offsets.  K A-operand: row 32kb + c, chunk 2s + hl.
+  const int krow_sw = c & 7;
+  // V^T A-operand by transposed reads: group G = lane >> 4 covers dims 16(G&1) .. +16 of keys base + 4(G>>1) + q;
+  // lane 4q + p of the group addresses row (base + q), dims 16(G&1) + 4p .. +4
+  const int G = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile t landed for every wave; every wave is done with buffer buf ^ 1
+    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
+    const char* Ks = lds + buf * 2 * kEncTileBytes;
+    const char* Vs = Ks + kEncTileBytes;
+    // ---- S^T = K.Q^T (two 32-key blocks) ----
+    f32x16 st[2];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[kb2][r] = 0.f;
+      const int row = 32 * kb2 + c;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const u16x8 kf = *reinterpret_cast<const u16x8*>(Ks + row * 128 + (((2 * s2 + hl) ^ krow_sw) << 4));
+        st[kb2] = mfma32<T>(kf, qf[s2], st[kb2]);
+      }
+    }
+    if ((t + 1) * kEncTile > Tk) {  // last, partial tile: keys past Tk never count
+#pragma unroll
+      for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = t * kEncTile + 32 * kb2 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= Tk) st[kb2][r] = -INFINITY;
+        }
+    }
+    // ---- online softmax (raw-score max; scale folded into the exponent) ----
+    float mx = st[0][0];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb2][r]);
+    mx = max_pair32(mx);
+    // deferred rescale (cdna_hip_programming.md T13): the running max moves only when this tile's max exceeds it
+    // by more than 8 (log2 units), so P <= 2^8; the decision precedes this tile's exponentials, and O and l are
+    // rescaled together with the same factor.  The first tile always rescales (m_run = -inf, alpha = 0).
+    if (__builtin_amdgcn_ballot_w64((mx - m_run) * C > 8.0f) != 0) {
+      const float m_new = (mx - m_run) * C > 8.0f ? mx : m_run;
+      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * C);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
+    }
+    const float mc = m_run * C;
+    float ls = 0.f;
+    u16x8 pf[2][2];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[kb2][r], C, -mc));
+        st[kb2][r] = p;
+        ls += p;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) pf[kb2][s2] = pack8<T>(st[kb2], 8 * s2);
+    }
+    l_run += ls;
+    // ---- O^T += V^T.P^T ----
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          u16x8 vf;
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int row = 32 * kb2 + 16 * s2 + 8 * half + 4 * (G >> 1) + tq;
+            const int col = 32 * db + 16 * (G & 1) + 4 * tp;
+            const int off = row * 128 + ((((col >> 3) ^ (row & 7))) << 4) + (col & 7) * 2;
+            const s16x4 v4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(Vs + off));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vf[4 * half + e] = (uint16_t)v4[e];
+          }
+          o[db] = mfma32<T>(vf, pf[kb2][s2], o[db]);
+        }
+      }
+  }
+  // ---- epilogue: lane holds O^T[dim 32db + (r&3) + 8(r>>2) + 4hl][query c] ----
+  const float lt = l_run + __shfl_xor(l_run, 32);
+  const float inv = lt > 0.f ? 1.0f / lt : 0.f;
+  const int q = q0 + c;
+  if (q < a.Tq) {
+    uint16_t* ob = a.o + (long)b * a.o_bstride + (long)h * a.head_stride + (long)q * a.o_ld;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        u16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = from_f32<T>(o[db][4 * rg + e] * inv);
+        *reinterpret_cast<u16x4*>(ob + 32 * db + 8 * rg + 4 * hl) = w;
+      }
+  }
+}
+
+void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) {
+  static const bool legacy = getenv("WMX_ENC_ATTN_LEGACY") != nullptr;  // A/B switch for tuning runs
+  if (legacy || a.head_stride % 8 != 0 || a.k_ld % 8 != 0 || a.v_ld % 8 != 0 || a.q_ld % 8 != 0 ||
+      a.kv_head_stride != 0) {
+    launch_attn_flash(dt, a, 0, 0, nullptr, st);
+    return;
+  }
+  dim3 grid(cdiv(a.Tq, 128), a.H, a.B);
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(enc_attn_kernel<DT::BF16>, grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(enc_attn_kernel<DT::F16>, grid, dim3(256), 0, st, a);
+  WMX_HIP(hipGetLastError());
+}
 
 // ------------------------------------------------------------------------------------------------
 // decoder self attention for decode steps: workgroup = (head, row); the row's keys are its ancestry
@@ -601,7 +817,7 @@ static int cross_chunk(int Tk, int nq) {
   }();
   if (nq > 16) return Tk;  // prefill: many query tiles already fill the chip
   if (env) return env;
-  return 256;
+  return 512;  // large-v3, 8 windows: 512-key chunks beat 256 by 5-10 % per decode step (bench.py sweep, r01)
 }
 
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
