@@ -252,6 +252,18 @@ def main():
     roof["kernel"] = dom
     roof["launch_ms"] = round(ms, 4)
     roof["algorithmic_per_launch"] = {"bytes": by, "flops": fl}
+    # encoder MFMA utilisation (north_star: >= 40 % in the encoder): one whole encoder pass over a context's
+    # windows, isolated (HIP events), and the in-situ encoder stage of the timed region (all groups concurrent)
+    e_ms, _, e_fl = ctx.bench_kernel("encoder", Bg, iters=3)
+    e_tf = e_fl / (e_ms * 1e-3) / 1e12
+    insitu_tf = G * e_fl / (stages[1] * 1e-3) / 1e12 if stages[1] > 0 else None
+    encoder = {"windows": Bg, "gflop_per_window": round(e_fl / Bg / 1e9, 1), "isolated_ms": round(e_ms, 2),
+               "isolated_tflops": round(e_tf, 1), "isolated_mfma_util": round(e_tf / MFMA_BF16_PEAK_TFLOPS, 4),
+               "insitu_stage_ms": round(stages[1], 2),
+               "insitu_tflops": round(insitu_tf, 1) if insitu_tf else None,
+               "insitu_mfma_util": round(insitu_tf / MFMA_BF16_PEAK_TFLOPS, 4) if insitu_tf else None,
+               "peak_tflops": MFMA_BF16_PEAK_TFLOPS}
+    log(f"[rank {rank}] encoder: {encoder}")
     log(f"[rank {rank}] kernel ms/launch: " + ", ".join(f"{k}={v[0]:.4f}" for k, v in kern_stats.items()))
     log(f"[rank {rank}] est. ms per transcribe step: " + ", ".join(f"{k}={v:.1f}" for k, v in per_step_ms.items()))
 
@@ -278,6 +290,7 @@ def main():
                    "use_graph": not args.no_graph, "context_groups": G},
         "stage_ms": [round(s, 2) for s in stages],
         "roofline": roof,
+        "encoder": encoder,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -168,7 +168,7 @@ int wmx_ctx_last_steps(wmx_ctx* c);
  * the last wmx_transcribe, B windows) between two HIP events; returns the average launch duration and the
  * ALGORITHMIC bytes / flops of one launch.  kernel: 0 decoder cross-attention (one layer, decode step),
  * 1 encoder fc1 GEMM, 2 encoder self-attention (one layer), 3 log-mel (raw pass), 4 decoder fc1 GEMM (step),
- * 5 decoder self-attention (one layer, at the last decoded length). */
+ * 5 decoder self-attention (one layer, at the last decoded length), 6 the whole encoder over B windows. */
 wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float* avg_ms, double* bytes,
                                 double* flops);
 

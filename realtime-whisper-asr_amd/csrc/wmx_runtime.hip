@@ -1969,6 +1969,13 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       by = (double)R * (s + 1) * dt * 2 * 2;
       fl = 4.0 * R * (s + 1) * dt;
       fn = [&c, a] { launch_self_attn(c.dt, a, c.st); };
+    } else if (kernel == 6) {
+      // the whole encoder (conv front end + every layer + final LN) over B windows: its MFMA work per window
+      const double T = 1500, M = m.d.n_mels, Ha = m.d.n_audio_head, La = m.d.n_audio_layer;
+      fl = B * (2.0 * 3000 * 3 * M * da + 2.0 * T * 3 * da * da +
+                La * (2.0 * T * da * 3 * da + 4.0 * Ha * T * T * 64 + 2.0 * T * da * da + 4.0 * T * da * 4 * da));
+      by = (double)La * 12 * da * da * 2;
+      fn = [&c, B] { encode(c, B); };
     } else {
       WMX_CHECK(false, "bench_kernel: unknown kernel");
     }

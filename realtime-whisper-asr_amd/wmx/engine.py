@@ -268,7 +268,7 @@ class Context:
     def last_steps(self) -> int:
         return int(lib.wmx_ctx_last_steps(self._h))
 
-    KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5}
+    KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5, "encoder": 6}
 
     def set_probe(self, kernel: str | None, layer: int = 0):
         """Capture HIP events around one decode-step launch of `kernel` (cross_attn, dec_fc1, self_attn) at decoder
