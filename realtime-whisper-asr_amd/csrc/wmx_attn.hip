@@ -235,14 +235,23 @@ constexpr int kEncTile = 64;                       // keys per step
 constexpr int kEncTileBytes = kEncTile * 64 * 2;   // one K or V tile
 template <DT T>
 __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
-  const int b = blockIdx.z, h = blockIdx.y;
+  // 1-D grid, XCD-grouped (§5.5 T1): the query tiles of one (window, head) run on one XCD, so its K/V stream is
+  // fetched into that XCD's L2 once instead of once per tile
+  const int nqt = (a.Tq + 127) / 128, nwg = nqt * a.H * a.B;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  }
+  const int qt = bid % nqt, bh = bid / nqt;
+  const int h = bh % a.H, b = bh / a.H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c = lane & 31, hl = lane >> 5;
   __shared__ __attribute__((aligned(16))) char lds[4 * kEncTileBytes];  // [buf][K | V]
   const uint16_t* qb = a.q + (long)b * a.q_bstride + (long)h * a.head_stride;
   const uint16_t* kb = a.k + (long)b * a.k_bstride + (long)h * a.head_stride;
   const uint16_t* vb = a.v + (long)b * a.v_bstride + (long)h * a.head_stride;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = qt * 128 + wave * 32;
   const int Tk = a.Tk;
   const int ntiles = (Tk + kEncTile - 1) / kEncTile;
 
@@ -396,7 +405,7 @@ void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) {
     launch_attn_flash(dt, a, 0, 0, nullptr, st);
     return;
   }
-  dim3 grid(cdiv(a.Tq, 128), a.H, a.B);
+  dim3 grid(cdiv(a.Tq, 128) * a.H * a.B);
   if (dt == DT::BF16)
     hipLaunchKernelGGL(enc_attn_kernel<DT::BF16>, grid, dim3(256), 0, st, a);
   else

@@ -81,7 +81,7 @@ template <> __device__ inline f32x4 mfma16<DT::F16>(const u16x8& a, const u16x8&
 // which cost the encoder's fc1 epilogue ~50 us per layer at large-v3 x 8 windows.
 __device__ inline float erf_fast(float z) {
   const float a = fabsf(z);
-  const float t = __frcp_rn(fmaf(0.3275911f, a, 1.0f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
   float p = fmaf(1.061405429f, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);

@@ -413,11 +413,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   const int tilesM = (M + BM - 1) / BM;
   const int nwg = tilesN * tilesM;
   int bid = blockIdx.x;
-  {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles (row panels share its L2)
+  {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int tm = bid / tilesN, tn = bid - tm * tilesN;
+  // grouped order inside that range: 4 row panels walk the columns together, so the ~32 tiles an XCD runs at
+  // once share 4 A panels and ~8 W panels in its L2 (row-major order shared 2 A panels but 16+ W panels)
+  constexpr int GM = 4;
+  const int gsz = GM * tilesN;
+  const int grp = bid / gsz, gr = bid - grp * gsz;
+  const int gm = min(GM, tilesM - grp * GM);
+  const int tm = grp * GM + gr % gm, tn = gr / gm;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;

@@ -21,8 +21,8 @@ MATCH = {
     "cross_attn": "dec_cross_attn_kernel",
     "self_attn": "dec_self_attn_kernel",
     "dec_fc1": "gemm_packed_kernel",
-    "enc_fc1": "gemm_kernel",
-    "enc_attn": "attn_flash_kernel",
+    "enc_fc1": "gemm256_kernel",
+    "enc_attn": "enc_attn_kernel",
     "logmel": "logmel_raw_kernel",
 }
 
@@ -47,7 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kernels", nargs="+")
     ap.add_argument("--batch", type=int, nargs="+", default=[4, 8], help="windows per launch")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01b_pmc_traffic.json"))
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     res = {}
@@ -59,7 +59,7 @@ def main():
                                "traffic_bytes": 2.0 * fetch_kb * 1024 + write_kb * 1024,
                                "launches": min(n1, n2),
                                "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B"}
-            print(k, b, json.dumps(res[f"{k}@{b}"]))
+            print(k, b, json.dumps(res[f"{k}@{b}"]), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1)
