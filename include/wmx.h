@@ -39,7 +39,9 @@ enum {
   WMX_ERR_NOMEM = 4,
 };
 
-enum { WMX_DTYPE_BF16 = 0, WMX_DTYPE_F16 = 1 };
+/* WMX_DTYPE_MX8: bf16 everywhere except the encoder projections (q/k/v, out, fc1, fc2), which run on the
+ * CDNA4 MX-fp8 MFMA (OCP e4m3 elements, e8m0 scale per 32 K) with MX-fp8 activations (BASELINE config 5). */
+enum { WMX_DTYPE_BF16 = 0, WMX_DTYPE_F16 = 1, WMX_DTYPE_MX8 = 2 };
 enum { WMX_TASK_TRANSCRIBE = 0, WMX_TASK_TRANSLATE = 1 };
 
 typedef struct wmx_model wmx_model;

@@ -124,6 +124,52 @@ def round_dtype(x: np.ndarray, dtype: str) -> np.ndarray:
     return x.astype(np.float32)
 
 
+# ----------------------------------------------------------------------------------------------
+# OCP MX-fp8 (BASELINE config 5: the encoder projections on the CDNA4 MX-fp8 MFMA).  No reference fixture exists
+# for this path (faster-whisper/CT2 have no fp8 mode; the reference CPU config is int8): the rule below restates
+# the OCP Microscaling spec's fp8 e4m3 element format with one e8m0 scale per 32 consecutive K elements, the
+# scale chosen as the smallest power of two that brings the block max within the e4m3 range (no saturation);
+# tools/mx8_check.hip pins the hardware conversion (round-to-nearest-even) and the scaled-MFMA lane maps.
+# ----------------------------------------------------------------------------------------------
+def mx8_exp(amax: np.ndarray) -> np.ndarray:
+    """Block exponent e (scale 2^e): amax = m 2^k, m in [0.5, 1) -> e = k - 9 + (m > 0.875), clamped to [-126, 126]
+    (the float32 bits of amax, exactly as wmx_common.h mx8_exp)."""
+    u = np.ascontiguousarray(amax, dtype=np.float32).view(np.uint32)
+    E = ((u >> np.uint32(23)) & np.uint32(255)).astype(np.int32)
+    Mt = (u & np.uint32(0x7FFFFF)).astype(np.int32)
+    return np.clip(E - 135 + (Mt > 0x600000), -126, 126).astype(np.int32)
+
+
+def e4m3_round(v: np.ndarray) -> np.ndarray:
+    """Nearest-even OCP e4m3 value of float32 v with |v| <= 448 (subnormal step 2^-9, normal step 2^(E-3))."""
+    v = np.asarray(v, dtype=np.float32)
+    a = np.abs(v).astype(np.float64)
+    m, k = np.frexp(np.maximum(a, 2.0 ** -6))  # a = m 2^k, m in [0.5, 1): binade exponent E = k - 1
+    step = np.ldexp(1.0, k - 4)                  # 2^(E-3); at a < 2^-6 the clamp gives the subnormal step 2^-9
+    q = np.rint(a / step) * step
+    return (np.sign(v) * q).astype(np.float32)
+
+
+def mx8_quantize(x: np.ndarray) -> np.ndarray:
+    """MX-fp8 round trip along the last axis (blocks of 32): the dequantized float32 values the MFMA consumes."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    K = x.shape[-1]
+    assert K % 32 == 0
+    b = x.reshape(x.shape[:-1] + (K // 32, 32))
+    e = mx8_exp(np.abs(b).max(-1))[..., None]
+    inv = np.ldexp(np.float32(1.0), -e).astype(np.float32)
+    q = e4m3_round((b * inv).astype(np.float32))
+    return (q.astype(np.float64) * np.ldexp(1.0, e)).astype(np.float32).reshape(x.shape)
+
+
+def linear_mx8(x, W, p, bias=True):
+    """linear() with both operands MX-fp8-quantized along K (fp32 accumulation of the exact products)."""
+    y = mx8_quantize(x).astype(np.float64) @ mx8_quantize(W[p + ".weight"]).astype(np.float64).T
+    if bias:
+        y = y + W[p + ".bias"]
+    return y.astype(np.float32)
+
+
 def tensor_specs(d: Dims):
     """(name, logical shape, scale, offset) in generation order; tid = index in this list.
 
@@ -313,20 +359,22 @@ def conv1d_k3(x, w, b, stride):
     return y.astype(np.float32)
 
 
-def encoder(W, d: Dims, mel: np.ndarray) -> np.ndarray:
-    """WhisperEncoder.forward (modeling_whisper.py:592): conv-GELU x2, + sinusoid, L pre-LN blocks, LN."""
+def encoder(W, d: Dims, mel: np.ndarray, mx8: bool = False) -> np.ndarray:
+    """WhisperEncoder.forward (modeling_whisper.py:592): conv-GELU x2, + sinusoid, L pre-LN blocks, LN.
+    mx8: the four projections of every layer take MX-fp8-quantized operands (model dtype float8 / config 5)."""
+    lin = linear_mx8 if mx8 else linear
     x = gelu(conv1d_k3(mel.astype(np.float32), W["encoder.conv1.weight"], W["encoder.conv1.bias"], 1))
     x = gelu(conv1d_k3(x, W["encoder.conv2.weight"], W["encoder.conv2.bias"], 2))
     x = (x.T + W["encoder.embed_positions.weight"][: x.shape[1]]).astype(np.float32)
     for i in range(d.n_audio_layer):
         p = f"encoder.layers.{i}"
         h = layer_norm(x, W[p + ".self_attn_layer_norm.weight"], W[p + ".self_attn_layer_norm.bias"])
-        q = linear(h, W, p + ".self_attn.q_proj")
-        k = linear(h, W, p + ".self_attn.k_proj", bias=False)
-        v = linear(h, W, p + ".self_attn.v_proj")
-        x = x + linear(mha(q, k, v, d.n_audio_head), W, p + ".self_attn.out_proj")
+        q = lin(h, W, p + ".self_attn.q_proj")
+        k = lin(h, W, p + ".self_attn.k_proj", bias=False)
+        v = lin(h, W, p + ".self_attn.v_proj")
+        x = x + lin(mha(q, k, v, d.n_audio_head), W, p + ".self_attn.out_proj")
         h = layer_norm(x, W[p + ".final_layer_norm.weight"], W[p + ".final_layer_norm.bias"])
-        x = x + linear(gelu(linear(h, W, p + ".fc1")), W, p + ".fc2")
+        x = x + lin(gelu(lin(h, W, p + ".fc1")), W, p + ".fc2")
     return layer_norm(x, W["encoder.layer_norm.weight"], W["encoder.layer_norm.bias"])
 
 

@@ -384,7 +384,28 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
   const float lt = l_run + __shfl_xor(l_run, 32);
   const float inv = lt > 0.f ? 1.0f / lt : 0.f;
   const int q = q0 + c;
-  if (q < a.Tq) {
+  if (a.o8) {
+    // MX-fp8 output (the A operand of the MX-fp8 out-projection): block db of this head's 64 dims is split over
+    // lanes c and c + 32 (16 values each), which agree on its scale through one permlane32 swap
+    if (q < a.Tq) {
+      const long row = (long)b * a.Tq + q;
+      uint8_t* ob = a.o8 + row * a.o8_ld + (long)h * 64;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        float am = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) am = fmaxf(am, fabsf(o[db][r] * inv));
+        const int ex = mx8_exp(max_pair32(am));
+        const float is = mx8_inv_scale(ex);
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+          *reinterpret_cast<uint32_t*>(ob + 32 * db + 8 * rg + 4 * hl) =
+              mx8_pack4(o[db][4 * rg] * inv * is, o[db][4 * rg + 1] * inv * is, o[db][4 * rg + 2] * inv * is,
+                        o[db][4 * rg + 3] * inv * is);
+        if (hl == 0) a.os[row * a.os_ld + 2 * h + db] = (uint8_t)(ex + 127);
+      }
+    }
+  } else if (q < a.Tq) {
     uint16_t* ob = a.o + (long)b * a.o_bstride + (long)h * a.head_stride + (long)q * a.o_ld;
 #pragma unroll
     for (int db = 0; db < 2; ++db)
@@ -400,8 +421,8 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
 
 void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) {
   static const bool legacy = getenv("WMX_ENC_ATTN_LEGACY") != nullptr;  // A/B switch for tuning runs
-  if (legacy || a.head_stride % 8 != 0 || a.k_ld % 8 != 0 || a.v_ld % 8 != 0 || a.q_ld % 8 != 0 ||
-      a.kv_head_stride != 0) {
+  if (!a.o8 && (legacy || a.head_stride % 8 != 0 || a.k_ld % 8 != 0 || a.v_ld % 8 != 0 || a.q_ld % 8 != 0 ||
+                a.kv_head_stride != 0)) {
     launch_attn_flash(dt, a, 0, 0, nullptr, st);
     return;
   }

@@ -104,4 +104,31 @@ __device__ inline float wave_sum(float v) {
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// ---- OCP MX-fp8: e4m3 elements (OCP "fn", max 448), one e8m0 scale 2^e per 32 consecutive K elements ----
+// e = the smallest power of two with amax / 2^e <= 448, taken from the f32 bits of amax (amax = m 2^k with
+// m in [0.5, 1): e = k - 9 + (m > 0.875)), clamped to [-126, 126]; the scale byte is e + 127.  Elements are
+// x / 2^e rounded to nearest-even e4m3 by v_cvt_pk_fp8_f32 (tools/mx8_check.hip: bit-exact vs RNE on 2^16
+// values).  oracle/whisper_np.py mx8_quantize restates the same rule.
+__device__ __host__ inline int mx8_exp(float amax) {
+  uint32_t u;
+  __builtin_memcpy(&u, &amax, 4);
+  const int E = (int)((u >> 23) & 255u), Mt = (int)(u & 0x7fffffu);
+  const int e = E - 135 + (Mt > 0x600000 ? 1 : 0);
+  return e < -126 ? -126 : (e > 126 ? 126 : e);
+}
+__device__ inline float mx8_inv_scale(int e) { return __int_as_float((127 - e) << 23); }  // 2^-e, exact
+// four values (already divided by the block scale) -> four e4m3 bytes, little-endian in one dword
+__device__ inline uint32_t mx8_pack4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+// max |x| over the 8 consecutive lanes of an aligned group (a 32-element block held 4 per lane)
+__device__ inline float max8_lanes(float v) {
+  v = fmaxf(v, __shfl_xor(v, 1));
+  v = fmaxf(v, __shfl_xor(v, 2));
+  v = fmaxf(v, __shfl_xor(v, 4));
+  return v;
+}
+
 }  // namespace wmx

@@ -12,6 +12,7 @@ enum EpiKind {
   EPI_STORE32 = 4,     // out32 = acc (+ bias)          (logits)
   EPI_QKV_CACHE = 5,   // decoder self-attn: q -> out16, k/v -> KV cache at slot *slot0 + (m % Tn)
   EPI_CROSSKV = 6,     // cross K/V of all decoder layers, head-major: K [L][xw][H][kXS][64], V^T [L][xw][H][64][kXS]
+  EPI_GELU_MX8 = 7,    // out8 = MX-fp8(gelu(acc + bias)): e4m3 bytes at out (ldc bytes / row), e8m0 scales at out2
 };
 
 struct Epi {
@@ -28,6 +29,9 @@ struct Epi {
   uint16_t* vc = nullptr;
   // EPI_CROSSKV: row m = w * xt + t, column n = (l * 2 + kv) * d + h * 64 + e
   int xw = 1, xt = 1500;
+  // EPI_GELU_MX8: the block scales (one byte per 32 columns, ldc2 bytes per row)
+  uint8_t* out2 = nullptr;
+  long ldc2 = 0;
 };
 
 // padded key stride of the cross K/V images (a multiple of 32 keys; the pad stays zero)
@@ -68,6 +72,28 @@ struct GemmCall {
 };
 
 void launch_gemm(DT dt, const GemmCall& g, hipStream_t st);
+
+// MX-fp8 GEMM (v_mfma_scale_f32_16x16x128_f8f6f4): C[M][N] = dequant(A)[M][K] . dequant(W)[N][K]^T.
+// A / W: e4m3 bytes, row stride lda / ldw bytes; AS / WS: e8m0 scale bytes per 32 K (row stride ldas / ldws).
+// K % 128 == 0; epilogues STORE16 / RESID32 / GELU_MX8 / STORE32 (the output dtype of STORE16 is `dt`).
+struct Mx8Call {
+  const uint8_t* A;
+  long lda;
+  const uint8_t* AS;
+  long ldas;
+  const uint8_t* W;
+  long ldw;
+  const uint8_t* WS;
+  long ldws;
+  int M, N, K;
+  Epi epi;
+};
+void launch_gemm_mx8(DT dt, const Mx8Call& g, hipStream_t st);
+// rows x K (bf16 / f16) -> MX-fp8 bytes [rows][K] + scales [rows][K/32] (weight preparation)
+void launch_mx8_quantize_rows(DT dt, const uint16_t* src, long rows, int K, uint8_t* q, uint8_t* s, hipStream_t st);
+// LayerNorm of fp32 rows straight to MX-fp8 (the A operand of the next MX-fp8 GEMM)
+void launch_layernorm_mx8(const float* x, const float* g, const float* b, uint8_t* q, uint8_t* s, int rows, int d,
+                          hipStream_t st);
 
 // ---- decoder weights in MFMA-fragment-major ("packed") layout ----
 // A [N][K] weight is stored as tiles of 16 rows x 32 k (1 KiB); tile (n/16, k/32) at ((n/16)*(K/32) + k/32)*512,
@@ -135,6 +161,10 @@ struct AttnArgs {
   int B, H, Tq, Tk;
   int head_stride;     // elements between heads (64 for [t][h*64] layouts)
   long kv_head_stride = 0;  // K/V head stride when it differs from head_stride (0: same)
+  // encoder attention only: write O as MX-fp8 (bytes [row][o8_ld], scales [row][os_ld]) instead of o
+  uint8_t* o8 = nullptr;
+  uint8_t* os = nullptr;
+  long o8_ld = 0, os_ld = 0;
 };
 void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st);
 // flash attention with optional causal mask (key <= query + causal_off) and per-entry first valid key

@@ -72,6 +72,101 @@ void launch_layernorm(DT dt, const float* x, const float* g, const float* b, uin
   launch_layernorm_rows(dt, x, nullptr, g, b, out, rows, d, st);
 }
 
+// ---------------- LayerNorm straight to MX-fp8 (encoder, MX-fp8 mode): the same two-pass statistics as
+// layernorm_kernel; the 8 lanes holding a 32-column block (4 columns each) agree on its e8m0 scale ----------------
+__global__ __launch_bounds__(256) void layernorm_mx8_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                            const float* __restrict__ bb, uint8_t* __restrict__ q,
+                                                            uint8_t* __restrict__ sc, int rows, int d) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const float4* xr = reinterpret_cast<const float4*>(x + (long)row * d);
+  const int n4 = d >> 2;
+  float4 v[8];  // d <= 2048
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      v[i] = xr[c];
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+  }
+  const float mean = wave_sum(s) / d;
+  float qq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, e = v[i].w - mean;
+      qq += a * a + b * b + cc * cc + e * e;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(qq) / d + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {  // n4 is a multiple of 8 (d % 32 == 0): a block's 8 lanes are all inside or all outside
+      const float4 gg = reinterpret_cast<const float4*>(g)[c];
+      const float4 be = reinterpret_cast<const float4*>(bb)[c];
+      const float y0 = (v[i].x - mean) * rstd * gg.x + be.x, y1 = (v[i].y - mean) * rstd * gg.y + be.y;
+      const float y2 = (v[i].z - mean) * rstd * gg.z + be.z, y3 = (v[i].w - mean) * rstd * gg.w + be.w;
+      const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3)))));
+      const float is = mx8_inv_scale(ex);
+      reinterpret_cast<uint32_t*>(q + (long)row * d)[c] = mx8_pack4(y0 * is, y1 * is, y2 * is, y3 * is);
+      if ((lane & 7) == 0) sc[(long)row * (d >> 5) + (c >> 3)] = (uint8_t)(ex + 127);
+    }
+  }
+}
+
+void launch_layernorm_mx8(const float* x, const float* g, const float* b, uint8_t* q, uint8_t* s, int rows, int d,
+                          hipStream_t st) {
+  if (rows <= 0) return;
+  WMX_CHECK(d % 32 == 0 && d <= 2048, "layernorm_mx8: d");
+  hipLaunchKernelGGL(layernorm_mx8_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows, d);
+  WMX_HIP(hipGetLastError());
+}
+
+// ---------------- 16-bit rows -> MX-fp8 (weight preparation): one thread per 32-element block ----------------
+template <DT T>
+__global__ __launch_bounds__(256) void mx8_quantize_rows_kernel(const uint16_t* __restrict__ src, long rows, int K,
+                                                                uint8_t* __restrict__ q, uint8_t* __restrict__ sc) {
+  const int nb = K >> 5;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * nb) return;
+  const long row = i / nb;
+  const int b = (int)(i - row * nb);
+  const uint16_t* p = src + row * K + 32 * b;
+  float v[32];
+  float am = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const u16x8 h = *reinterpret_cast<const u16x8*>(p + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[8 * c + e] = to_f32<T>(h[e]);
+      am = fmaxf(am, fabsf(v[8 * c + e]));
+    }
+  }
+  const int ex = mx8_exp(am);
+  const float is = mx8_inv_scale(ex);
+  uint32_t* o = reinterpret_cast<uint32_t*>(q + row * K + 32 * b);
+#pragma unroll
+  for (int w = 0; w < 8; ++w) o[w] = mx8_pack4(v[4 * w] * is, v[4 * w + 1] * is, v[4 * w + 2] * is, v[4 * w + 3] * is);
+  sc[row * nb + b] = (uint8_t)(ex + 127);
+}
+
+void launch_mx8_quantize_rows(DT dt, const uint16_t* src, long rows, int K, uint8_t* q, uint8_t* s, hipStream_t st) {
+  WMX_CHECK(K % 32 == 0, "mx8 quantize: K");
+  const long n = rows * (K / 32);
+  if (n <= 0) return;
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(mx8_quantize_rows_kernel<DT::BF16>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, rows, K, q, s);
+  else
+    hipLaunchKernelGGL(mx8_quantize_rows_kernel<DT::F16>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, rows, K, q, s);
+  WMX_HIP(hipGetLastError());
+}
+
 // ---------------- conv1 im2col: out[b*3000+t][kk*M + c] = mel[b][c][t+kk-1] (0 outside / in the K pad) ----------------
 template <DT T>
 __global__ __launch_bounds__(256) void im2col1_kernel(const float* __restrict__ mel, int B, int M, int Kp,

@@ -116,6 +116,9 @@ struct TensorEntry {
 struct EncLayer {
   float *ln1g, *ln1b, *bqkv, *bo, *ln2g, *ln2b, *bfc1, *bfc2;
   uint16_t *wqkv, *wo, *wfc1, *wfc2;
+  // MX-fp8 copies of the four projections (model dtype WMX_DTYPE_MX8): e4m3 [N][K] + e8m0 scales [N][K/32]
+  uint8_t *qkv8 = nullptr, *qkv8s = nullptr, *o8 = nullptr, *o8s = nullptr, *fc18 = nullptr, *fc18s = nullptr,
+          *fc28 = nullptr, *fc28s = nullptr;
 };
 struct DecLayer {
   float *ln1g, *ln1b, *bqkv, *bo, *ln2g, *ln2b, *bcq, *bco, *ln3g, *ln3b, *bfc1, *bfc2;
@@ -126,6 +129,7 @@ struct Model {
   wmx_dims d{};
   int device = 0;
   DT dt = DT::BF16;
+  bool mx8 = false;  // encoder projections on MX-fp8 MFMA (BASELINE config 5); everything else in `dt`
   char* arena = nullptr;
   size_t arena_bytes = 0;
   int K1p = 0;
@@ -184,6 +188,19 @@ static void build_model(Model& m) {
     P.add(&L.bfc1, 4 * da);
     P.add(&L.wfc2, (size_t)4 * da * da);
     P.add(&L.bfc2, da);
+  }
+  if (m.mx8) {
+    WMX_CHECK(da % 128 == 0, "model: MX-fp8 encoder needs a width multiple of 128");
+    for (auto& L : m.enc) {
+      P.add(&L.qkv8, (size_t)3 * da * da);
+      P.add(&L.qkv8s, (size_t)3 * da * da / 32);
+      P.add(&L.o8, (size_t)da * da);
+      P.add(&L.o8s, (size_t)da * da / 32);
+      P.add(&L.fc18, (size_t)4 * da * da);
+      P.add(&L.fc18s, (size_t)4 * da * da / 32);
+      P.add(&L.fc28, (size_t)4 * da * da);
+      P.add(&L.fc28s, (size_t)4 * da * da / 32);
+    }
   }
   P.add(&m.lnpg, da);
   P.add(&m.lnpb, da);
@@ -330,6 +347,20 @@ static void build_model(Model& m) {
   WMX_HIP(hipStreamSynchronize(m.st));
 }
 
+// MX-fp8 mode: derive the e4m3 + e8m0 copies of the encoder projections from the 16-bit weights (after every
+// weight load; deterministic, so ranks that receive the broadcast arena may redo it harmlessly)
+static void prepare_mx8(Model& m) {
+  if (!m.mx8) return;
+  const int da = m.d.n_audio_state;
+  for (auto& L : m.enc) {
+    launch_mx8_quantize_rows(m.dt, L.wqkv, 3L * da, da, L.qkv8, L.qkv8s, m.st);
+    launch_mx8_quantize_rows(m.dt, L.wo, da, da, L.o8, L.o8s, m.st);
+    launch_mx8_quantize_rows(m.dt, L.wfc1, 4L * da, da, L.fc18, L.fc18s, m.st);
+    launch_mx8_quantize_rows(m.dt, L.wfc2, da, 4 * da, L.fc28, L.fc28s, m.st);
+  }
+  WMX_HIP(hipStreamSynchronize(m.st));
+}
+
 // ------------------------------------------------------------------------------------------------
 // context
 // ------------------------------------------------------------------------------------------------
@@ -362,6 +393,8 @@ struct Ctx {
   int* wmax = nullptr;
   uint16_t *im1 = nullptr, *h1 = nullptr, *im2 = nullptr, *ehb = nullptr, *eqkv = nullptr, *eao = nullptr, *ef1 = nullptr,
            *enc_out = nullptr, *ckv = nullptr;
+  // MX-fp8 encoder operands: e4m3 [rows][K] + e8m0 scales [rows][K/32] (LN out, attention out, fc1 out)
+  uint8_t *eh8 = nullptr, *eh8s = nullptr, *ea8 = nullptr, *ea8s = nullptr, *ef8 = nullptr, *ef8s = nullptr;
   float* ex = nullptr;
   // decoder
   int dec_rows_max = 0;  // rows*Tn capacity of the decoder activation buffers
@@ -443,6 +476,14 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.eao, (size_t)B * 1500 * da);
   P.add(&c.ef1, (size_t)B * 1500 * 4 * da);
   P.add(&c.enc_out, (size_t)B * 1500 * da);
+  if (c.m->mx8) {
+    P.add(&c.eh8, (size_t)B * 1500 * da);
+    P.add(&c.eh8s, (size_t)B * 1500 * da / 32);
+    P.add(&c.ea8, (size_t)B * 1500 * da);
+    P.add(&c.ea8s, (size_t)B * 1500 * da / 32);
+    P.add(&c.ef8, (size_t)B * 1500 * 4 * da);
+    P.add(&c.ef8s, (size_t)B * 1500 * 4 * da / 32);
+  }
   P.add(&c.ckv, (size_t)B * kXS * Lt * 2 * dt);  // K and V^T images, key stride kXS (pad stays zero)
   const int DR = c.dec_rows_max;
   P.add(&c.dx, (size_t)DR * dt);
@@ -621,6 +662,82 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
 // ------------------------------------------------------------------------------------------------
 // encoder
 // ------------------------------------------------------------------------------------------------
+// MX-fp8 encoder layers (BASELINE config 5): the four projections of every layer run on
+// v_mfma_scale_f32_16x16x128_f8f6f4 with their A operands produced directly in MX-fp8 by the LayerNorm, the
+// attention epilogue and the fc1 GELU epilogue; q/k/v, the attention itself and the fp32 residual stay as in
+// the 16-bit path.
+static void gemm_mx8(Ctx& c, const uint8_t* A, const uint8_t* AS, const uint8_t* W, const uint8_t* WS, int M, int N,
+                     int K, const Epi& e) {
+  Mx8Call g;
+  g.A = A;
+  g.lda = K;
+  g.AS = AS;
+  g.ldas = K / 32;
+  g.W = W;
+  g.ldw = K;
+  g.WS = WS;
+  g.ldws = K / 32;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.epi = e;
+  launch_gemm_mx8(c.dt, g, c.st);
+}
+
+static void encode_layers_mx8(Ctx& c, int B) {
+  Model& m = *c.m;
+  const int da = m.d.n_audio_state, H = m.d.n_audio_head;
+  const int rows = B * 1500;
+  for (auto& L : m.enc) {
+    launch_layernorm_mx8(c.ex, L.ln1g, L.ln1b, c.eh8, c.eh8s, rows, da, c.st);
+    Epi eq;
+    eq.kind = EPI_STORE16;
+    eq.bias = L.bqkv;
+    eq.out = c.eqkv;
+    eq.ldc = 3L * da;
+    gemm_mx8(c, c.eh8, c.eh8s, L.qkv8, L.qkv8s, rows, 3 * da, da, eq);
+    AttnArgs a{};
+    a.q = c.eqkv;
+    a.k = c.eqkv + da;
+    a.v = c.eqkv + 2 * da;
+    a.q_ld = a.k_ld = a.v_ld = 3 * da;
+    a.q_bstride = a.k_bstride = a.v_bstride = 1500L * 3 * da;
+    a.o = c.eao;
+    a.o_ld = da;
+    a.o_bstride = 1500L * da;
+    a.B = B;
+    a.H = H;
+    a.Tq = a.Tk = 1500;
+    a.head_stride = 64;
+    a.o8 = c.ea8;
+    a.os = c.ea8s;
+    a.o8_ld = da;
+    a.os_ld = da / 32;
+    launch_attn_encoder(c.dt, a, c.st);
+    Epi eo;
+    eo.kind = EPI_RESID32;
+    eo.bias = L.bo;
+    eo.out = c.ex;
+    eo.ldc = da;
+    gemm_mx8(c, c.ea8, c.ea8s, L.o8, L.o8s, rows, da, da, eo);
+    launch_layernorm_mx8(c.ex, L.ln2g, L.ln2b, c.eh8, c.eh8s, rows, da, c.st);
+    Epi e1;
+    e1.kind = EPI_GELU_MX8;
+    e1.bias = L.bfc1;
+    e1.out = c.ef8;
+    e1.ldc = 4L * da;
+    e1.out2 = c.ef8s;
+    e1.ldc2 = 4L * da / 32;
+    gemm_mx8(c, c.eh8, c.eh8s, L.fc18, L.fc18s, rows, 4 * da, da, e1);
+    Epi e2;
+    e2.kind = EPI_RESID32;
+    e2.bias = L.bfc2;
+    e2.out = c.ex;
+    e2.ldc = da;
+    gemm_mx8(c, c.ef8, c.ef8s, L.fc28, L.fc28s, rows, da, 4 * da, e2);
+  }
+}
+
 static void encode(Ctx& c, int B) {
   Model& m = *c.m;
   const int da = m.d.n_audio_state, H = m.d.n_audio_head, M = m.d.n_mels;
@@ -632,6 +749,11 @@ static void encode(Ctx& c, int B) {
   e2.pos = m.enc_pos;
   e2.posT = 1500;
   gemm(c, c.im2, 3 * da, m.conv2w, 3 * da, (int)rows, da, 3 * da, e2);
+  if (m.mx8) {
+    encode_layers_mx8(c, B);
+    launch_layernorm(c.dt, c.ex, m.lnpg, m.lnpb, c.enc_out, (int)rows, da, c.st);
+    return;
+  }
   for (auto& L : m.enc) {
     launch_layernorm(c.dt, c.ex, L.ln1g, L.ln1b, c.ehb, (int)rows, da, c.st);
     gemm(c, c.ehb, da, L.wqkv, da, (int)rows, 3 * da, da, epi(EPI_STORE16, L.bqkv, c.eqkv, 3 * da));
@@ -1410,12 +1532,13 @@ int wmx_device_count(void) {
 wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_model** out) {
   return guard([&] {
     WMX_CHECK(dims && out, "null argument");
-    WMX_CHECK(dtype == WMX_DTYPE_BF16 || dtype == WMX_DTYPE_F16, "dtype");
+    WMX_CHECK(dtype == WMX_DTYPE_BF16 || dtype == WMX_DTYPE_F16 || dtype == WMX_DTYPE_MX8, "dtype");
     auto* w = new wmx_model();
     try {
       w->m.d = *dims;
       w->m.device = device;
       w->m.dt = dtype == WMX_DTYPE_F16 ? DT::F16 : DT::BF16;
+      w->m.mx8 = dtype == WMX_DTYPE_MX8;
       WMX_HIP(hipSetDevice(device));
       WMX_HIP(hipStreamCreateWithFlags(&w->m.st, hipStreamNonBlocking));
       build_model(w->m);
@@ -1455,6 +1578,7 @@ wmx_status wmx_model_init_synthetic(wmx_model* w, uint64_t seed) {
       launch_init_tensor(m.dt, seed, s, m.st);
     }
     WMX_HIP(hipStreamSynchronize(m.st));
+    prepare_mx8(m);
     m.initialized = true;
   });
 }
@@ -1550,7 +1674,11 @@ wmx_status wmx_model_arena(wmx_model* w, void** ptr, size_t* bytes) {
 }
 
 wmx_status wmx_model_arena_loaded(wmx_model* w) {
-  return guard([&] { w->m.initialized = true; });
+  return guard([&] {
+    WMX_HIP(hipSetDevice(w->m.device));
+    prepare_mx8(w->m);
+    w->m.initialized = true;
+  });
 }
 
 void wmx_opts_default(wmx_opts* o) {

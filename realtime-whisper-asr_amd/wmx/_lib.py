@@ -12,7 +12,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("WMX_LIB", os.path.join(_HERE, "libwmx.so"))
 
-WMX_DTYPE_BF16, WMX_DTYPE_F16 = 0, 1
+WMX_DTYPE_BF16, WMX_DTYPE_F16, WMX_DTYPE_MX8 = 0, 1, 2
 WMX_TASK_TRANSCRIBE, WMX_TASK_TRANSLATE = 0, 1
 
 

@@ -65,8 +65,12 @@ class Model:
             self.dtype = L.WMX_DTYPE_BF16
         elif ct in ("float16", "f16", "fp16", "int8_float16", "default", "auto"):
             self.dtype = L.WMX_DTYPE_F16
+        elif ct in ("float8", "fp8", "mxfp8", "mx8", "float8_bfloat16"):
+            # BASELINE config 5: encoder projections on the CDNA4 MX-fp8 MFMA, the rest in bf16
+            self.dtype = L.WMX_DTYPE_MX8
         else:
-            raise ValueError(f"compute_type {compute_type!r} is not supported on MI355X (use float16 / bfloat16)")
+            raise ValueError(f"compute_type {compute_type!r} is not supported on MI355X "
+                             "(use float16 / bfloat16 / float8)")
         self.device = device
         h = C.c_void_p()
         ds = _dims_struct(self.dims)

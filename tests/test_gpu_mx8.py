@@ -1,0 +1,71 @@
+"""GPU parity of the MX-fp8 encoder (model compute_type "float8", BASELINE config 5): the four projections of every
+encoder layer on v_mfma_scale_f32_16x16x128_f8f6f4 with MX-fp8 activations produced by the LayerNorm, the
+attention epilogue and the fc1 GELU epilogue.
+
+Oracle: oracle/whisper_np.py encoder(..., mx8=True) on the same bf16-rounded weights (both operands of each
+projection quantized with the same OCP MX rule, fp32 accumulation).  Tolerance: relative L2 <= 3e-2 (the bf16
+path's bound: q/k/v and the attention stay bf16, and an activation whose f32 value differs in the last bits
+from the oracle's may round to the neighbouring e4m3 code).  The fp8 model's distance to the bf16 model is
+printed for reference.  Translate task: greedy tokens equal the oracle's until the first low-margin step."""
+import numpy as np
+import pytest
+
+from oracle import whisper_np as O
+from wmx import synth
+
+pytestmark = pytest.mark.gpu
+
+WIDE = O.Dims(128, 51866, 1280, 20, 2, 1280, 20, 1)
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _dims(E, d):
+    return E.ModelDims(d.n_mels, d.n_vocab, d.n_audio_state, d.n_audio_head, d.n_audio_layer, d.n_text_state,
+                       d.n_text_head, d.n_text_layer)
+
+
+@pytest.mark.parametrize("name", ["micro", "wide"])
+def test_mx8_encoder_matches_oracle(name):
+    from wmx import engine as E
+    d = O.DIMS["micro"] if name == "micro" else WIDE
+    m = E.Model(_dims(E, d), 0, "float8").init_synthetic(9)
+    ctx = E.Context(m, max_batch=3, beam_size=1, max_new_tokens=8, word_timestamps=False)
+    W = O.make_weights(d, 9, "bf16")
+    mels = np.stack([O.logmel_segment(synth.speech_like(s, n), d.n_mels)
+                     for s, n in ((81, 480000), (82, 200000), (83, 60000))])
+    got = ctx.encode(mels)
+    for b in range(3):
+        ref = O.encoder(W, d, mels[b], mx8=True)
+        e = rel_l2(got[b], ref)
+        e16 = rel_l2(got[b], O.encoder(W, d, mels[b]))
+        print(name, "mx8 encoder window", b, "rel_l2 vs mx8 oracle", e, "| vs bf16 oracle", e16)
+        assert e <= 3e-2, (b, e)
+
+
+def test_mx8_translate_greedy_matches_oracle():
+    from wmx import engine as E
+    d = O.DIMS["micro"]
+    m = E.Model("micro", 0, "float8").init_synthetic(9)
+    ctx = E.Context(m, max_batch=2, beam_size=1, max_new_tokens=24, task="translate", word_timestamps=False)
+    W = O.make_weights(d, 9, "bf16")
+    audios = [synth.speech_like(91, 480000), synth.speech_like(92, 96000)]
+    res = ctx.transcribe(audios)
+    n_cmp = 0
+    for a, r in zip(audios, res):
+        enc = O.encoder(W, d, O.logmel_segment(a, d.n_mels), mx8=True)
+        lang, _ = O.detect_language(W, d, enc)
+        assert r.language == lang
+        ref = O.decode(W, d, enc, O.DecodeOptions(language=lang, beam_size=1, max_new_tokens=24, task="translate"))
+        k = 0
+        for _, margin in ref.trace:
+            if margin < 0.15:
+                break
+            k += 1
+        k = min(k, len(ref.tokens), len(r.tokens))
+        assert r.tokens[:k] == ref.tokens[:k], (r.tokens, ref.tokens, k)
+        n_cmp += k
+    print("mx8 translate greedy tokens compared", n_cmp)
+    assert n_cmp > 0
