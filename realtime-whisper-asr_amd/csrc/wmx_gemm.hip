@@ -412,6 +412,57 @@ __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int 
   epi_from_image<T, 256, 512>(e, img, ldt, 64, mb, n0, M, N, tid);
 }
 
+// 64-row x 128-column image, 512 threads: a thread owns column quad (tid & 31) and rows (tid >> 5) + 16u
+template <DT T, int KIND>
+__device__ inline void epi_rows64_n128(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid) {
+  const int c4 = (tid & 31) * 4, r0 = tid >> 5;
+  const int n = n0 + c4;
+  if (n >= N) return;
+  float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e.bias) b = *reinterpret_cast<const float4*>(e.bias + n);
+  float4 v[4], aux[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = r0 + 16 * u, m = mb + row;
+    v[u] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
+    v[u] = make_float4(v[u].x + b.x, v[u].y + b.y, v[u].z + b.z, v[u].w + b.w);
+    if (KIND == EPI_RESID32 && m < M)
+      aux[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int m = mb + r0 + 16 * u;
+    if (m >= M) continue;  // uniform over each 32-lane half (same row)
+    float4 x = v[u];
+    if (KIND == EPI_GELU_MX8) {
+      x = make_float4(gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w));
+      const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)))));
+      const float is = mx8_inv_scale(ex);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(e.out) + (long)m * e.ldc + n) =
+          mx8_pack4(x.x * is, x.y * is, x.z * is, x.w * is);
+      if ((tid & 7) == 0) e.out2[(long)m * e.ldc2 + (n >> 5)] = (uint8_t)(ex + 127);
+    } else if (KIND == EPI_STORE16) {
+      const u16x4 h = {from_f32<T>(x.x), from_f32<T>(x.y), from_f32<T>(x.z), from_f32<T>(x.w)};
+      *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
+    } else {
+      if (KIND == EPI_RESID32) x = make_float4(x.x + aux[u].x, x.y + aux[u].y, x.z + aux[u].z, x.w + aux[u].w);
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n) = x;
+    }
+  }
+}
+
+template <DT T>
+__device__ inline void epi_image64_n128(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N,
+                                        int tid) {
+  switch (e.kind) {  // the host allows only these kinds, with N and ldc multiples of 4
+    case EPI_STORE16: epi_rows64_n128<T, EPI_STORE16>(e, img, ldt, mb, n0, M, N, tid); break;
+    case EPI_RESID32: epi_rows64_n128<T, EPI_RESID32>(e, img, ldt, mb, n0, M, N, tid); break;
+    case EPI_STORE32: epi_rows64_n128<T, EPI_STORE32>(e, img, ldt, mb, n0, M, N, tid); break;
+    case EPI_GELU_MX8: epi_rows64_n128<T, EPI_GELU_MX8>(e, img, ldt, mb, n0, M, N, tid); break;
+    default: break;
+  }
+}
+
 template <DT T>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int M, int N, int K,
@@ -570,18 +621,19 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
-// MX-fp8 GEMM: 256 x 256 tile, 8 waves (2 M x 4 N, wave tile 128 x 64), K staged in 128-deep slices (128 B of
-// e4m3 per row) through a 2-slot LDS ring by global_load_lds (rows: 16-B chunk c of row r at c ^ (r & 7); the
-// e8m0 scales of the slice: one dword per row = its four 32-blocks).  v_mfma_scale_f32_16x16x128_f8f6f4 takes
-// lane l = (r = l & 15, g = l >> 4) as row r with k = 16g .. +15 and 64 + 16g .. +15 (chunks g and g + 4 of the
-// row) and its scale operand as the scale of block g of row r (tools/mx8_check.hip measures both maps).
-// Same ping-pong phase schedule as gemm256_kernel: per slice two phases of 16 MFMAs; the slice t + 1 DMA is
-// issued in slice t's two memory segments and waited for (vmcnt(0)) right before the barrier that precedes the
-// first read of it by either wave half.
+// MX-fp8 GEMM: 256 (M) x 128 (N) tile, 8 waves (4 M x 2 N, wave tile 64 x 64 = 4 x 4 fragments: 64 accumulator
+// + 64 operand VGPRs, no spills at two waves per SIMD), K staged in 128-deep slices (128 B of e4m3 per row)
+// through a 3-slot LDS ring by global_load_lds (16-B chunk c of row r at c ^ (r & 7)); the slice's e8m0 scales
+// are one dword per row (its four 32-blocks).  v_mfma_scale_f32_16x16x128_f8f6f4 takes lane l = (r = l & 15,
+// g = l >> 4) as row r with k = 16g .. +15 and 64 + 16g .. +15 (chunks g and g + 4 of the row), and its scale
+// operand as the scale of block g of row r (tools/mx8_check.hip measures both maps).
+// Ping-pong phase schedule as gemm256_kernel; slice t + 2 is in flight while slice t computes: each wave issues
+// 7 DMAs per slice (4 A pieces + the scale dword in phase A, 2 W pieces in phase B) and waits for slice t + 1 with
+// a counted vmcnt(7) right before the barrier that precedes the first read of it by either wave half.
 // ------------------------------------------------------------------------------------------------
-constexpr int kMx8Rows = 256 * 128;                    // bytes of the A (or W) rows of one slice
-constexpr int kMx8Slot = 2 * kMx8Rows + 2 * 256 * 4;   // + A and W scale dwords
-constexpr int kMx8Lds = 2 * kMx8Slot;                  // 132 KiB
+constexpr int kMx8ARows = 256 * 128, kMx8WRows = 128 * 128;
+constexpr int kMx8Slot = kMx8ARows + kMx8WRows + 512 * 4;  // + scale dwords: 256 A rows, 128 W rows, 128 spare
+constexpr int kMx8Lds = 3 * kMx8Slot;                       // 150 KiB
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -592,7 +644,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
                                                           const uint8_t* __restrict__ W, long ldw,
                                                           const uint8_t* __restrict__ WS, long ldws, int M, int N,
                                                           int K, Epi e) {
-  constexpr int BM = 256, BN = 256;
+  constexpr int BM = 256, BN = 128;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesN = (N + BN - 1) / BN;
   const int tilesM = (M + BM - 1) / BM;
@@ -609,84 +661,95 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
   const int tm = grp * GM + gr % gm, tn = gr / gm;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave >> 1, wn = wave & 1;
   const int nk = K >> 7;
 
-  // staging: 32 A pieces + 32 W pieces of 1 KiB (8 rows x 128 B); wave w issues A / W pieces w + 8j (j < 4).
-  // Scale dwords: waves 0..3 stage A rows 64w .. 64w + 63, waves 4..7 W rows 64(w-4) .. +63 (256 B each).
+  // staging (8-row x 128-B pieces): wave w issues A pieces w + 8j (j < 4) and W pieces w + 8j (j < 2); scale
+  // dwords: wave w stages rows 64w .. 64w + 63 of [256 A rows | 128 W rows | 128 spare] (waves 6, 7 re-read W
+  // rows into the spare area so that every wave issues the same 7 DMAs per slice)
   const int srow = lane >> 3;
   const int scol = ((lane & 7) ^ srow) * 16;
-  const uint8_t* asrc[4];
-  const uint8_t* wsrc[4];
+  int aoff[4], woff[2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    asrc[j] = A + (long)min(m0 + (wave + 8 * j) * 8 + srow, M - 1) * lda + scol;
-    wsrc[j] = W + (long)min(n0 + (wave + 8 * j) * 8 + srow, N - 1) * ldw + scol;
-  }
+  for (int j = 0; j < 4; ++j) aoff[j] = (int)min((long)min(m0 + (wave + 8 * j) * 8 + srow, M - 1) * lda, 0x7fffffffL);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) woff[j] = (int)((long)min(n0 + (wave + 8 * j) * 8 + srow, N - 1) * ldw);
   const uint8_t* ssrc = wave < 4 ? AS + (long)min(m0 + 64 * wave + lane, M - 1) * ldas
-                                 : WS + (long)min(n0 + 64 * (wave - 4) + lane, N - 1) * ldws;
-  const int sdst = 2 * kMx8Rows + wave * 256;  // waves 0..3 -> A scale rows, 4..7 -> W scale rows
-  auto issue_half = [&](int kt, int h) {
-    char* slot = smem + (kt & 1) * kMx8Slot;
+                                 : WS + (long)min(n0 + 64 * ((wave - 4) & 1) + lane, N - 1) * ldws;
+  const int sdst = kMx8ARows + kMx8WRows + wave * 256;
+  auto issue_a = [&](int kt) {
+    char* slot = smem + (kt % 3) * kMx8Slot;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint8_t* src = (h == 0 ? asrc[j] : wsrc[j]) + kt * 128;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(slot + h * kMx8Rows +
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(A + aoff[j] + scol + kt * 128),
+                                       (__attribute__((address_space(3))) void*)(slot + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc + kt * 4),
+                                     (__attribute__((address_space(3))) void*)(slot + sdst), 4, 0, 0);
+  };
+  auto issue_w = [&](int kt) {
+    char* slot = smem + (kt % 3) * kMx8Slot;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(W + woff[j] + scol + kt * 128),
+                                       (__attribute__((address_space(3))) void*)(slot + kMx8ARows +
                                                                                  (wave + 8 * j) * 1024),
                                        16, 0, 0);
-    }
-    if (h == 0)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc + kt * 4),
-                                       (__attribute__((address_space(3))) void*)(slot + sdst), 4, 0, 0);
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
 
   const int fr = lane & 15, g = lane >> 4;
   const int c0 = (g ^ (fr & 7)) << 4, c1 = ((g + 4) ^ (fr & 7)) << 4;
-  const int arow = wm * 128 + fr, brow = wn * 64 + fr;
+  const int arow = wm * 64 + fr, brow = wn * 64 + fr;
   auto frag = [&](const char* base, int row) {
     const i32x4 lo = *reinterpret_cast<const i32x4*>(base + row * 128 + c0);
     const i32x4 hi = *reinterpret_cast<const i32x4*>(base + row * 128 + c1);
     return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   };
 
-  issue_half(0, 0);
-  issue_half(0, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue_a(0);
+  issue_w(0);
+  if (nk > 1) {
+    issue_a(1);
+    issue_w(1);
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
-  i32x8 af[4], bfr[4];
-  int sa[4], sb[4];
+  i32x8 af[2], bfr[4];
+  int sa[2], sb[4];
   for (int t = 0; t < nk; ++t) {
-    const char* S = smem + (t & 1) * kMx8Slot;
-    const char* Wb = S + kMx8Rows;
-    const uint32_t* SA = reinterpret_cast<const uint32_t*>(S + 2 * kMx8Rows);
+    const char* S = smem + (t % 3) * kMx8Slot;
+    const char* Wb = S + kMx8ARows;
+    const uint32_t* SA = reinterpret_cast<const uint32_t*>(S + kMx8ARows + kMx8WRows);
     const uint32_t* SB = SA + 256;
-    // ---- phase A: B fragments 0..3 and A fragments 0..3; first half of the next slice's DMA ----
+    const bool more = t + 2 < nk;
+    // ---- phase A: B fragments 0..3, A fragments 0, 1; A half (+ scales) of slice t + 2 ----
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bfr[j] = frag(Wb, brow + 16 * j);
       sb[j] = (int)(SB[brow + 16 * j] >> (8 * g));
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 2; ++i) {
       af[i] = frag(S, arow + 16 * i);
       sa[i] = (int)(SA[arow + 16 * i] >> (8 * g));
     }
-    if (t + 1 < nk) issue_half(t + 1, 0);
+    if (more) issue_a(t + 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sa[i], 0,
@@ -694,55 +757,64 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    // ---- phase B: A fragments 4..7; second half of the next slice's DMA ----
+    // ---- phase B: A fragments 2, 3; W half of slice t + 2 ----
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      af[i] = frag(S, arow + 16 * (i + 4));
-      sa[i] = (int)(SA[arow + 16 * (i + 4)] >> (8 * g));
+    for (int i = 0; i < 2; ++i) {
+      af[i] = frag(S, arow + 16 * (i + 2));
+      sa[i] = (int)(SA[arow + 16 * (i + 2)] >> (8 * g));
     }
-    if (t + 1 < nk) issue_half(t + 1, 1);
-    if (lagging) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the barrier ahead of slice t+1's reads
+    if (more) issue_w(t + 2);
+    if (lagging) {  // slice t + 1 complete before the barrier ahead of its first read (slice t + 2 may fly)
+      if (more)
+        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[i + 4][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i + 4][j], 0, 0, 0, sa[i],
+        acc[i + 2][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i + 2][j], 0, 0, 0, sa[i],
                                                                          0, sb[j]);
     __builtin_amdgcn_s_setprio(0);
-    if (!lagging) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the same barrier, seen from the leading half
+    if (!lagging) {  // the same barrier, seen from the leading half
+      if (more)
+        asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
 
+  // epilogue: 4 rounds of 64 rows (one wave row each) through an fp32 LDS image [64][BN + 4]
   constexpr int LDT = BN + 4;
   float* img = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int rd = 0; rd < 4; ++rd) {
-    if (wm == (rd >> 1)) {
+    if (wm == rd) {
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int i = (rd & 1) * 4 + ii;
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) img[(ii * 16 + g * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
-      }
+          for (int r = 0; r < 4; ++r) img[(i * 16 + g * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
     }
     __syncthreads();
-    epi_image64<T>(e, img, LDT, m0 + rd * 64, n0, M, N, tid);
+    epi_image64_n128<T>(e, img, LDT, m0 + rd * 64, n0, M, N, tid);
     __syncthreads();
   }
 }
 
 template <DT T>
 static void launch_mx8_t(const Mx8Call& g, hipStream_t st) {
-  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  const int tiles = ((g.M + 255) / 256) * ((g.N + 127) / 128);
   hipLaunchKernelGGL((gemm_mx8_kernel<T>), dim3(tiles), dim3(512), kMx8Lds, st, g.A, g.lda, g.AS, g.ldas, g.W, g.ldw,
                      g.WS, g.ldws, g.M, g.N, g.K, g.epi);
 }
@@ -751,8 +823,8 @@ void launch_gemm_mx8(DT dt, const Mx8Call& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return;
   WMX_CHECK(g.K % 128 == 0 && g.lda % 16 == 0 && g.ldw % 16 == 0 && g.ldas % 4 == 0 && g.ldws % 4 == 0,
             "gemm_mx8: K must be a multiple of 128, rows 16-B aligned");
-  WMX_CHECK(g.epi.kind == EPI_STORE16 || g.epi.kind == EPI_RESID32 || g.epi.kind == EPI_STORE32 ||
-                (g.epi.kind == EPI_GELU_MX8 && g.N % 256 == 0 && g.epi.ldc % 4 == 0),
+  WMX_CHECK((g.epi.kind == EPI_STORE16 || g.epi.kind == EPI_RESID32 || g.epi.kind == EPI_STORE32 ||
+             g.epi.kind == EPI_GELU_MX8) && g.N % 32 == 0 && g.epi.ldc % 4 == 0,
             "gemm_mx8: epilogue");
   if (dt == DT::BF16)
     launch_mx8_t<DT::BF16>(g, st);
