@@ -44,7 +44,9 @@ def parse():
     p.add_argument("--groups", type=int, default=2, help="concurrent decoding contexts the streams are split over")
     p.add_argument("--beam", type=int, default=5)
     p.add_argument("--max-new-tokens", type=int, default=224)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "f16"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8"],
+                   help="fp8: BASELINE config 5 (encoder projections on the MX-fp8 MFMA, the rest bf16)")
+    p.add_argument("--task", default="transcribe", choices=["transcribe", "translate"])
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -122,7 +124,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from wmx import engine, synth
 
-    dt = {"bf16": "bfloat16", "f16": "float16"}[args.dtype]
+    dt = {"bf16": "bfloat16", "f16": "float16", "fp8": "float8"}[args.dtype]
     model = engine.Model(args.model, local, dt)
     t = time.time()
     if world > 1:
@@ -145,7 +147,7 @@ def main():
     heads = engine.ALIGNMENT_HEADS.get(args.model)
     # G decoding contexts (each its own HIP stream and captured decode graph) share the weights; their window
     # groups run concurrently, so one group's kernel boundaries and latency-bound phases overlap the other's work
-    ctxs = [engine.Context(model, max_batch=Bg, beam_size=args.beam, max_new_tokens=args.max_new_tokens,
+    ctxs = [engine.Context(model, max_batch=Bg, beam_size=args.beam, max_new_tokens=args.max_new_tokens, task=args.task,
                            language=None, word_timestamps=True, alignment_heads=heads, use_graph=not args.no_graph)
             for _ in range(G)]
     ctx = ctxs[0]
@@ -262,7 +264,9 @@ def main():
                "insitu_stage_ms": round(stages[1], 2),
                "insitu_tflops": round(insitu_tf, 1) if insitu_tf else None,
                "insitu_mfma_util": round(insitu_tf / MFMA_BF16_PEAK_TFLOPS, 4) if insitu_tf else None,
-               "peak_tflops": MFMA_BF16_PEAK_TFLOPS}
+               "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
+               "note": ("fp8: the projections run on the MX-fp8 MFMA (5 PF dense peak), attention and convs bf16; "
+                        "utilisation quoted against the bf16 peak" if args.dtype == "fp8" else "bf16 MFMA")}
     log(f"[rank {rank}] encoder: {encoder}")
     log(f"[rank {rank}] kernel ms/launch: " + ", ".join(f"{k}={v[0]:.4f}" for k, v in kern_stats.items()))
     log(f"[rank {rank}] est. ms per transcribe step: " + ", ".join(f"{k}={v:.1f}" for k, v in per_step_ms.items()))
@@ -283,7 +287,7 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (seeded speech-like 30 s audio; build-owned PRNG weights of the named architecture)",
-        "config": {"workload": f"whisper-{args.model} transcribe, {B} x 30 s windows per GPU, beam {args.beam}, "
+        "config": {"workload": f"whisper-{args.model} {args.task}, {B} x 30 s windows per GPU, beam {args.beam}, "
                                f"word_timestamps, language auto-detect, max_new_tokens {args.max_new_tokens}",
                    "model": f"whisper-{args.model}", "global_batch": B * world, "seq_len": 480000,
                    "parallelism": f"dp{world} (independent streams)", "decode_steps": steps_done,
