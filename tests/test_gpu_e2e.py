@@ -61,3 +61,23 @@ def test_stream_batcher_matches_single_stream_calls(asr):
     for b, s in zip(batched, single):
         assert [seg.tokens for seg in b] == [seg.tokens for seg in s]
     assert StreamBatcher(model, asr) is not None
+
+
+@pytest.mark.parametrize("kind,n", [("zeros", 32000), ("noise", 16000), ("speech", 8000), ("speech", 16000 * 31),
+                                    ("speech", 116800), ("empty", 0)])
+def test_asr_controls_and_lengths(asr, kind, n):
+    """SURVEY §8d controls: all-zeros, white noise, 0.5 s / 7.3 s / 31 s (> one 30 s window: the seek loop moves
+    to a second window) and empty input; every word lies inside the audio and segments are time-ordered."""
+    audio = {"zeros": lambda: np.zeros(n, np.float32), "noise": lambda: synth.white_noise(5, n),
+             "speech": lambda: synth.speech_like(6, n), "empty": lambda: np.zeros(0, np.float32)}[kind]()
+    segs = asr.transcribe(audio)
+    dur = n / 16000.0
+    if n == 0:
+        assert segs == []
+        return
+    prev = 0.0
+    for seg in segs:
+        assert prev - 1e-6 <= seg.start <= seg.end <= dur + 0.02, (seg.start, seg.end, dur)
+        prev = seg.start
+    for s, e, w in asr.ts_words(segs):
+        assert 0.0 <= s <= e <= dur + 0.02
