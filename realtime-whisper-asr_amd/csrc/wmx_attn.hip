@@ -195,8 +195,12 @@ void launch_attn_flash(DT dt, const AttnArgs& a, int causal, int causal_off, con
 //   O^T += V^T.P^T takes the exponentiated scores straight from the accumulator registers as its B operand
 //     (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand"): no LDS round trip for P;
 //     the V^T operand comes from the row-major V tile by ds_read_b64_tr_b16 (T10).
-// Both LDS tiles are [64 keys][64 dims] with 16-B chunk c of row r stored at c ^ (r & 7) (swizzle applied on
-// the DMA source address, the LDS image stays lane-linear).
+// Both LDS tiles are [64 keys][64 dims] with 16-B chunk c of row r stored at c ^ enc_sw(r) (swizzle applied on the
+// DMA source address, the LDS image stays lane-linear).  enc_sw permutes bits 1..3 of the row so that both reads
+// are bank-conflict-free under gfx950's lane grouping: the K ds_read_b128 (four 16-lane groups {0-3,12-15,20-27},
+// ...: every group sees 16 distinct (row parity, chunk) slots) and the V ds_read_b64_tr_b16 (per 32-lane half,
+// rows r and r + 2 of a 4-row block land in opposite chunk quads).  Plain c ^ (r & 7) measured 2.7 conflict
+// cycles per LDS instruction (SQ_LDS_BANK_CONFLICT).
 // ------------------------------------------------------------------------------------------------
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -231,6 +235,8 @@ template <> __device__ inline u16x8 pack8<DT::F16>(const f32x16& v, int o) {
   return __builtin_bit_cast(u16x8, r);
 }
 
+__device__ inline int enc_sw(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2); }
+
 constexpr int kEncTile = 64;                       // keys per step
 constexpr int kEncTileBytes = kEncTile * 64 * 2;   // one K or V tile
 template <DT T>
@@ -256,19 +262,35 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
   const int ntiles = (Tk + kEncTile - 1) / kEncTile;
 
   // DMA staging: a tile is 8 pieces of 1 KiB (8 rows x 128 B); wave w stages K pieces w, w+4 and V pieces w, w+4.
-  // Lane l covers row l >> 3 of its piece and reads source chunk (l & 7) ^ (row & 7).
+  // Lane l covers row l >> 3 of its piece and reads source chunk (l & 7) ^ enc_sw(row).
   const int srow = lane >> 3;
-  const int schunk = ((lane & 7) ^ srow) * 8;  // (row & 7) == srow for 8-row pieces
+  const int schunk0 = ((lane & 7) ^ enc_sw(wave * 8 + srow)) * 8, schunk1 = ((lane & 7) ^ enc_sw((wave + 4) * 8 + srow)) * 8;
+  // per-lane source pointers of tile 0, advanced by a wave-uniform 64 rows per tile; only the last tile clamps
+  const uint16_t* ksrc[2];
+  const uint16_t* vsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave + 4 * i) * 8 + srow;
+    ksrc[i] = kb + (long)r * a.k_ld + (i ? schunk1 : schunk0);
+    vsrc[i] = vb + (long)r * a.v_ld + (i ? schunk1 : schunk0);
+  }
   auto stage = [&](int t, int buf) {
     char* kd = lds + buf * 2 * kEncTileBytes;
     char* vd = kd + kEncTileBytes;
+    const bool edge = (t + 1) * kEncTile > Tk;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int piece = wave + 4 * i;
-      const int key = min(t * kEncTile + piece * 8 + srow, Tk - 1);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + (long)key * a.k_ld + schunk),
+      const uint16_t* ks = ksrc[i] + (long)t * kEncTile * a.k_ld;
+      const uint16_t* vs = vsrc[i] + (long)t * kEncTile * a.v_ld;
+      if (edge) {  // rows past Tk re-read row Tk - 1 (finite data; their scores are masked)
+        const int key = min(t * kEncTile + piece * 8 + srow, Tk - 1);
+        ks = kb + (long)key * a.k_ld + (i ? schunk1 : schunk0);
+        vs = vb + (long)key * a.v_ld + (i ? schunk1 : schunk0);
+      }
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ks,
                                        (__attribute__((address_space(3))) void*)(kd + piece * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(vb + (long)key * a.v_ld + schunk),
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)vs,
                                        (__attribute__((address_space(3))) void*)(vd + piece * 1024), 16, 0, 0);
     }
   };
@@ -290,10 +312,19 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
   const float C = 0.125f * kLog2e;
 
   // per-lane LDS offsets.  K A-operand: row 32kb + c, chunk 2s + hl.
-  const int krow_sw = c & 7;
+  const int krow_sw = enc_sw(c);  // rows 32 kb + c: bits 1..3 are c's
   // V^T A-operand by transposed reads: group G = lane >> 4 covers dims 16(G&1) .. +16 of keys base + 4(G>>1) + q;
   // lane 4q + p of the group addresses row (base + q), dims 16(G&1) + 4p .. +4
   const int G = lane >> 4, gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+  int voff[2][2];  // [db][half]: rows 8 half + 4 (G >> 1) + tq of a 16-row group, dims 32 db + 16 (G & 1) + 4 tp
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = 8 * half + 4 * (G >> 1) + tq;
+      const int col = 32 * db + 16 * (G & 1) + 4 * tp;
+      voff[db][half] = row * 128 + (((col >> 3) ^ enc_sw(row)) << 4) + (col & 7) * 2;
+    }
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -368,11 +399,9 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
           u16x8 vf;
 #pragma unroll
           for (int half = 0; half < 2; ++half) {
-            const int row = 32 * kb2 + 16 * s2 + 8 * half + 4 * (G >> 1) + tq;
-            const int col = 32 * db + 16 * (G & 1) + 4 * tp;
-            const int off = row * 128 + ((((col >> 3) ^ (row & 7))) << 4) + (col & 7) * 2;
+            // enc_sw only sees bits 1..3 of the row, so 32 kb + 16 s is a plain immediate offset
             const s16x4 v4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(Vs + off));
+                (__attribute__((address_space(3))) s16x4*)(Vs + voff[db][half] + (32 * kb2 + 16 * s2) * 128));
 #pragma unroll
             for (int e = 0; e < 4; ++e) vf[4 * half + e] = (uint16_t)v4[e];
           }
