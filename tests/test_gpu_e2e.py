@@ -81,3 +81,48 @@ def test_asr_controls_and_lengths(asr, kind, n):
         prev = seg.start
     for s, e, w in asr.ts_words(segs):
         assert 0.0 <= s <= e <= dur + 0.02
+
+
+def test_config2_base_fp16_streaming_vac_1s_chunks():
+    """BASELINE config 2 plumbing: Whisper base fp16 (PRNG weights of the base architecture) behind the drop-in
+    ASR, driven through DynamicVACOnlineASRProcessor (reference asr_components.py:81-179) with 1 s online
+    chunks fed at the 640-sample VAC cadence (一键.py:1286) and a scripted VAD track (Silero is not available
+    offline).  Every ASR call sees a growing buffer; committed words are time-ordered and inside the audio."""
+    import time
+    from wmx.asr import MI355XWhisperASR
+    from wmx.online import DynamicVACOnlineASRProcessor, ScriptedVAD
+    asr = MI355XWhisperASR(lan="auto", modelsize="base", device="cuda", compute_type="float16",
+                           transcribe_kwargs={"beam_size": 5}, max_new_tokens=16)
+    calls = []
+    inner = asr.transcribe
+
+    def timed(audio, init_prompt=""):
+        t0 = time.perf_counter()
+        out = inner(audio, init_prompt=init_prompt)
+        calls.append((len(audio), time.perf_counter() - t0))
+        return out
+
+    asr.transcribe = timed
+    secs = 12
+    n_win = secs * 16000 // 512
+    probs = [0.0] * 30 + [0.95] * (n_win - 60) + [0.0] * 30  # silence, speech, silence
+    vac = DynamicVACOnlineASRProcessor(1.0, asr, vad_model=ScriptedVAD(probs))
+    audio = synth.speech_like(8, secs * 16000)
+    committed = []
+    for i in range(0, len(audio), 640):
+        vac.insert_audio_chunk(audio[i: i + 640])
+        beg, end, text = vac.process_iter()
+        if beg is not None:
+            committed.append((beg, end, text))
+    beg, end, text = vac.finish()
+    if beg is not None:
+        committed.append((beg, end, text))
+    assert calls, "voiced audio must reach the ASR"
+    assert all(n > 0 for n, _ in calls)
+    prev = 0.0
+    for b, e, _ in committed:
+        assert prev - 1e-6 <= b <= e <= secs + 0.05
+        prev = b
+    lat = sorted(t for _, t in calls)
+    print(f"config 2: {len(calls)} ASR calls, p50 latency {1000 * lat[len(lat) // 2]:.1f} ms, "
+          f"{len(committed)} commits")
