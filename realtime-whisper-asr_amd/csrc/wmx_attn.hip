@@ -634,8 +634,9 @@ typedef __attribute__((address_space(1))) float gf32;
 // chunk records [nwin][H][KS][nq][66]; one arrival counter per (window, head) in DecAttnArgs::xcnt
 inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long)nwin * H * KS * nq * 66; }
 
-template <DT T, int KPW>
-__global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
+template <DT T, int KPW, int NWV>
+__global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
+  constexpr int NT = 64 * NWV;
   const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z % KS, qt = blockIdx.z / KS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_a
   const int i0 = qt * 16;  // first query (within the window) of this tile
   const int nqt = min(16, nq - i0);
   const int kc0 = ks * chunk, kc1 = min(a.Tk, kc0 + chunk);
-  const int per = ((kc1 - kc0 + 3) / 4 + 31) / 32 * 32;  // keys per wave, whole 32-key blocks
+  const int per = ((kc1 - kc0 + NWV - 1) / NWV + 31) / 32 * 32;  // keys per wave, whole 32-key blocks
   const int kw0 = kc0 + wave * per, kw1 = min(kc1, kw0 + per);
   const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
   const uint16_t* vbase = a.cv + (long)w * a.x_wstride + (long)h * a.x_hstride;
@@ -684,7 +685,7 @@ __global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_a
   // ---- the tile's queries into LDS (bf16/f16, rounded like the stored path), one element per thread:
   //      q = bias + sum of the split-K partials in slice order, or the stored q ----
   __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
-  for (int t = tid; t < 16 * 64; t += 256) {
+  for (int t = tid; t < 16 * 64; t += NT) {
     const int q = t >> 6, e = t & 63;
     uint16_t v = 0;
     if (q < nqt) {
@@ -779,9 +780,9 @@ __global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_a
     }
   }
 
-  // ---- combine the 4 waves (LDS), then output or a chunk record ----
-  __shared__ float sm[4][16], sl[4][16];
-  __shared__ float so[4][16][65];
+  // ---- combine the NWV waves (LDS), then output or a chunk record ----
+  __shared__ float sm[NWV][16], sl[NWV][16];
+  __shared__ float so[NWV][16][65];
   if (g == 0) {
     sm[wave][fr] = m_run;
     sl[wave][fr] = l_run;
@@ -791,12 +792,14 @@ __global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_a
 #pragma unroll
     for (int r = 0; r < 4; ++r) so[wave][4 * g + r][16 * db + fr] = o[db][r];
   __syncthreads();
-  for (int t = tid; t < nqt * 64; t += 256) {
+  for (int t = tid; t < nqt * 64; t += NT) {
     const int q = t >> 6, e = t & 63;
-    float M = fmaxf(fmaxf(sm[0][q], sm[1][q]), fmaxf(sm[2][q], sm[3][q]));
+    float M = sm[0][q];
+#pragma unroll
+    for (int wv = 1; wv < NWV; ++wv) M = fmaxf(M, sm[wv][q]);
     float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int wv = 0; wv < 4; ++wv) {
+    for (int wv = 0; wv < NWV; ++wv) {
       const float f = sm[wv][q] == -INFINITY ? 0.f : __expf(sm[wv][q] - M);
       L += sl[wv][q] * f;
       O += so[wv][q][e] * f;
@@ -837,7 +840,7 @@ __global__ __launch_bounds__(256, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_a
   // every record load is a buffer load with sc1 (aux 16): it bypasses this CU's L1, so no acquire is needed
   const float* wh = part + (long)(w * a.H + h) * KS * nq * 66;
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)wh, (short)0, KS * nq * 66 * 4, 0x00020000);
-  for (int t = tid; t < nq * 64; t += 256) {
+  for (int t = tid; t < nq * 64; t += NT) {
     const int q = t >> 6, e = t & 63;
     float rec[kMaxSplits][3];
 #pragma unroll
@@ -894,12 +897,27 @@ static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
   WMX_CHECK(KS == 1 || chunk % 32 == 0, "cross attn: key chunks must be whole 32-key blocks");
   WMX_CHECK(KS == 1 || (ws != nullptr && a.xcnt != nullptr && nq <= 16), "cross attn: split workspace required");
   dim3 grid(a.H, nwin, KS * QT);
+  // WMX_XATTN_WAVES=8: 8 waves per workgroup (half the keys per wave), for tuning runs
+  static const int waves = [] {
+    const char* v = getenv("WMX_XATTN_WAVES");
+    return v && atoi(v) == 8 ? 8 : 4;
+  }();
+  if (waves == 8 && nq <= 16) {
+    const int per_wave = ((chunk + 7) / 8 + 31) / 32;
+    switch (std::min(per_wave, 4)) {
+      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+    }
+    return;
+  }
   const int per_wave = ((chunk + 3) / 4 + 31) / 32;  // 32-key blocks per wave
   switch (std::min(per_wave, 4)) {
-    case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
-    case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
-    case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
-    default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
   }
 }
 
