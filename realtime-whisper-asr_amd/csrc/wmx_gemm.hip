@@ -391,8 +391,29 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
   }
 }
 
-template <DT T>
+template <DT T, int KIND>
 __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid) {
+  if constexpr (KIND == EPI_CROSSKV) {  // specialised cross-K/V launch (host: d % 256 == 0, xt % 4 == 0)
+    if (((n0 / e.d) & 1) == 0) {
+      epi_rows64<T, EPI_CROSSKV>(e, img, ldt, mb, n0, M, N, tid);
+    } else {  // V^T: 4 consecutive keys of one column per 8-byte store
+      const int col = tid & 255, r4 = (tid >> 8) * 4, n = n0 + col;
+      const float b = e.bias ? e.bias[n] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = r4 + 8 * u, m = mb + rr;
+        if (m >= M) continue;
+        u16x4 h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) h[q] = from_f32<T>(img[(rr + q) * ldt + col] + b);
+        *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)) = h;
+      }
+    }
+    return;
+  } else if constexpr (KIND >= 0) {  // specialised launch: the host checked the vector conditions
+    epi_rows64<T, KIND>(e, img, ldt, mb, n0, M, N, tid);
+    return;
+  }
   const bool vec = (N & 3) == 0 && (e.ldc & 3) == 0;
   const bool kpart = e.kind == EPI_CROSSKV && ((n0 / e.d) & 1) == 0;  // K image: row-major 64-wide head rows
   if (vec || kpart) {
@@ -466,7 +487,7 @@ __device__ inline void epi_image64_n128(const Epi& e, const float* img, int ldt,
   }
 }
 
-template <DT T>
+template <DT T, int KIND>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int M, int N, int K,
                                                          Epi e) {
@@ -618,7 +639,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
       }
     }
     __syncthreads();
-    epi_image64<T>(e, img, LDT, m0 + rd * 64, n0, M, N, tid);
+    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid);
     __syncthreads();
   }
 }
@@ -935,6 +956,9 @@ static void skinny_attr() {
 }
 
 // set every kernel attribute up front (never inside a stream capture)
+template <DT T>
+static void g256_attr();
+
 void gemm_init_attributes() {
   static bool done = false;
   if (done) return;
@@ -950,10 +974,8 @@ void gemm_init_attributes() {
   skinny_attr<DT::F16, 8, 8>();
   skinny_attr<DT::F16, 12, 4>();
   skinny_attr<DT::F16, 16, 4>();
-  WMX_HIP(hipFuncSetAttribute((const void*)gemm256_kernel<DT::BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kG256Lds));
-  WMX_HIP(hipFuncSetAttribute((const void*)gemm256_kernel<DT::F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kG256Lds));
+  g256_attr<DT::BF16>();
+  g256_attr<DT::F16>();
   WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_kernel<DT::BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kMx8Lds));
   WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_kernel<DT::F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1142,6 +1164,45 @@ static void launch_cfg(const GemmCall& g, hipStream_t st) {
   }
 }
 
+// gemm256 instantiations: one per vectorisable epilogue kind (the epilogue's registers then hold only what that
+// kind needs), plus the generic one (-1) for the cross-K/V scatter and unaligned outputs
+template <DT T, int KIND>
+static void g256_attr_one() {
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm256_kernel<T, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kG256Lds));
+}
+template <DT T>
+static void g256_attr() {
+  g256_attr_one<T, -1>();
+  g256_attr_one<T, EPI_STORE16>();
+  g256_attr_one<T, EPI_GELU16>();
+  g256_attr_one<T, EPI_RESID32>();
+  g256_attr_one<T, EPI_GELU_POS32>();
+  g256_attr_one<T, EPI_STORE32>();
+  g256_attr_one<T, EPI_GELU_MX8>();
+  g256_attr_one<T, EPI_CROSSKV>();
+}
+template <DT T>
+static void launch_g256(const GemmCall& g, hipStream_t st) {
+  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  const bool vec = (g.N & 3) == 0 && (g.epi.ldc & 3) == 0;
+  const int kind = (vec || g.epi.kind == EPI_CROSSKV) ? g.epi.kind : -1;
+#define WMX_G256_LAUNCH(KD)                                                                                    \
+  hipLaunchKernelGGL((gemm256_kernel<T, KD>), dim3(tiles), dim3(512), kG256Lds, st, g.A, g.lda, g.W, g.ldw, g.M, \
+                     g.N, g.K, g.epi)
+  switch (kind) {
+    case EPI_STORE16: WMX_G256_LAUNCH(EPI_STORE16); break;
+    case EPI_GELU16: WMX_G256_LAUNCH(EPI_GELU16); break;
+    case EPI_RESID32: WMX_G256_LAUNCH(EPI_RESID32); break;
+    case EPI_GELU_POS32: WMX_G256_LAUNCH(EPI_GELU_POS32); break;
+    case EPI_STORE32: WMX_G256_LAUNCH(EPI_STORE32); break;
+    case EPI_GELU_MX8: WMX_G256_LAUNCH(EPI_GELU_MX8); break;
+    case EPI_CROSSKV: WMX_G256_LAUNCH(EPI_CROSSKV); break;
+    default: WMX_G256_LAUNCH(-1); break;
+  }
+#undef WMX_G256_LAUNCH
+}
+
 template <DT T>
 static void launch_t(const GemmCall& g, hipStream_t st) {
   if (g.tile == TILE_SKINNY) {
@@ -1151,9 +1212,7 @@ static void launch_t(const GemmCall& g, hipStream_t st) {
   if (g.tile == TILE_256) {
     WMX_CHECK(g.K % 32 == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm256: K / leading dimensions");
     WMX_CHECK(g.epi.kind != EPI_CROSSKV || (g.epi.d % 256 == 0 && g.epi.xt % 4 == 0), "gemm256: cross K/V shape");
-    const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
-    hipLaunchKernelGGL((gemm256_kernel<T>), dim3(tiles), dim3(512), kG256Lds, st, g.A, g.lda, g.W, g.ldw, g.M, g.N,
-                       g.K, g.epi);
+    launch_g256<T>(g, st);
     return;
   }
   WMX_CHECK(g.K % 64 == 0, "gemm: K must be a multiple of 64");
