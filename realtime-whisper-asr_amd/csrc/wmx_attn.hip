@@ -296,20 +296,33 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
   };
   stage(0, 0);
 
-  // Q^T fragments (B operand): lane holds Q[q0 + c][16s + 8hl .. +8] for dim steps s = 0..3
+  // Q^T fragments (B operand): lane holds Q[q0 + c][16s + 8hl .. +8] for dim steps s = 0..3, pre-scaled by
+  // C = log2(e) / sqrt(64) and rounded once to T, so the MFMA produces scores in log2 units directly (the
+  // reference rounds its scaled q, and then its scores, to the same 16-bit type)
+  const float C = 0.125f * kLog2e;
   u16x8 qf[4];
   {
     const int q = min(q0 + c, a.Tq - 1);
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) qf[s2] = *reinterpret_cast<const u16x8*>(qb + (long)q * a.q_ld + 16 * s2 + 8 * hl);
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const u16x8 raw = *reinterpret_cast<const u16x8*>(qb + (long)q * a.q_ld + 16 * s2 + 8 * hl);
+      f32x16 sc;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sc[e] = to_f32<T>(raw[e]) * C;
+      qf[s2] = pack8<T>(sc, 0);
+    }
   }
   f32x16 o[2];
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
-  const float C = 0.125f * kLog2e;
+  // m_run: this lane's query's softmax baseline (log2 units); negm = -m_run in every element is the QK^T
+  // accumulator's initial value, so the scores come out of the MFMA already shifted (no per-score subtract)
+  float m_run = 0.f, l_run = 0.f;
+  f32x16 negm;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negm[r] = 0.f;
 
   // per-lane LDS offsets.  K A-operand: row 32kb + c, chunk 2s + hl.
   const int krow_sw = enc_sw(c);  // rows 32 kb + c: bits 1..3 are c's
@@ -336,13 +349,11 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
     f32x16 st[2];
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[kb2][r] = 0.f;
       const int row = 32 * kb2 + c;
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
         const u16x8 kf = *reinterpret_cast<const u16x8*>(Ks + row * 128 + (((2 * s2 + hl) ^ krow_sw) << 4));
-        st[kb2] = mfma32<T>(kf, qf[s2], st[kb2]);
+        st[kb2] = mfma32<T>(kf, qf[s2], s2 == 0 ? negm : st[kb2]);
       }
     }
     if ((t + 1) * kEncTile > Tk) {  // last, partial tile: keys past Tk never count
@@ -354,40 +365,46 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
           if (key >= Tk) st[kb2][r] = -INFINITY;
         }
     }
-    // ---- online softmax (raw-score max; scale folded into the exponent) ----
+    // ---- online softmax on baseline-relative log2 scores ----
     float mx = st[0][0];
 #pragma unroll
     for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb2][r]);
     mx = max_pair32(mx);
-    // deferred rescale (cdna_hip_programming.md T13): the running max moves only when this tile's max exceeds it
-    // by more than 8 (log2 units), so P <= 2^8; the decision precedes this tile's exponentials, and O and l are
-    // rescaled together with the same factor.  The first tile always rescales (m_run = -inf, alpha = 0).
-    if (__builtin_amdgcn_ballot_w64((mx - m_run) * C > 8.0f) != 0) {
-      const float m_new = (mx - m_run) * C > 8.0f ? mx : m_run;
-      const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * C);
-      m_run = m_new;
+    // deferred rescale (cdna_hip_programming.md T13): the baseline moves only when this tile's max exceeds it by
+    // more than 8, so P <= 2^8; the decision precedes this tile's exponentials, and O and l are rescaled together
+    // with the same factor.  The first tile always moves the baseline to its max (alpha multiplies zeros).
+    float ls = 0.f;
+    if (__builtin_amdgcn_ballot_w64(mx > 8.0f || t == 0) != 0) {  // rare: wave-uniform branch
+      const float d = (mx > 8.0f || t == 0) ? mx : 0.f;
+      const float alpha = t == 0 ? 0.f : __builtin_amdgcn_exp2f(-d);  // t = 0: O and l are still zero
+      m_run += d;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) negm[r] = -m_run;
       l_run *= alpha;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[db][r] *= alpha;
-    }
-    const float mc = m_run * C;
-    float ls = 0.f;
-    u16x8 pf[2][2];
 #pragma unroll
-    for (int kb2 = 0; kb2 < 2; ++kb2) {
+      for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[kb2][r] -= d;
+    }
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(st[kb2][r], C, -mc));
+        const float p = __builtin_amdgcn_exp2f(st[kb2][r]);
         st[kb2][r] = p;
         ls += p;
       }
+    u16x8 pf[2][2];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) pf[kb2][s2] = pack8<T>(st[kb2], 8 * s2);
-    }
     l_run += ls;
     // ---- O^T += V^T.P^T ----
 #pragma unroll
