@@ -1,6 +1,8 @@
 // Memory-bound helper kernels: LayerNorm (fp32 residual -> 16-bit GEMM operand), conv im2col, token+position
 // embedding, dtype conversion, and the build-owned synthetic weight generator (same counter PRNG as
 // oracle/whisper_np.py prng_uniform, bit-exact).
+#include <cstdlib>
+
 #include "wmx_common.h"
 #include "wmx_kernels.h"
 
@@ -337,10 +339,72 @@ __global__ __launch_bounds__(kRedThreads) void reduce_ln_kernel(const float* __r
   }
 }
 
+// float4 form (d % 4 == 0, d <= 4096): one thread per column quad (d / 4 threads rounded up to whole waves, 320
+// for large-v3), all S + 2 quads of the thread loaded in one batch; fewer, wider loads and 5 waves instead of 16
+// in the two block reductions, which is what this latency-bound step pays for
+template <DT T>
+__global__ __launch_bounds__(1024) void reduce_ln4_kernel(const float* __restrict__ part, int S, long pstride,
+                                                          const float* __restrict__ bias, float* __restrict__ x,
+                                                          const float* __restrict__ g, const float* __restrict__ b,
+                                                          uint16_t* __restrict__ out, int d) {
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  __shared__ float red[2][16];
+  const int c = tid * 4;
+  const bool ok = c < d;
+  float4 t[kRedMaxS], xv = make_float4(0.f, 0.f, 0.f, 0.f), bv = xv;
+  if (ok) {
+    xv = *reinterpret_cast<const float4*>(x + (long)m * d + c);
+    if (bias) bv = *reinterpret_cast<const float4*>(bias + c);
+  }
+#pragma unroll
+  for (int u = 0; u < kRedMaxS; ++u)
+    t[u] = (ok && u < S) ? *reinterpret_cast<const float4*>(part + u * pstride + (long)m * d + c)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int u = 0; u < kRedMaxS; ++u) p = make_float4(p.x + t[u].x, p.y + t[u].y, p.z + t[u].z, p.w + t[u].w);
+  const float4 v = make_float4(xv.x + bv.x + p.x, xv.y + bv.y + p.y, xv.z + bv.z + p.z, xv.w + bv.w + p.w);
+  if (ok) *reinterpret_cast<float4*>(x + (long)m * d + c) = v;
+  if (!g) return;
+  float sum = ok ? (v.x + v.y) + (v.z + v.w) : 0.f;
+  sum = wave_sum(sum);
+  if (lane == 0) red[0][wave] = sum;
+  __syncthreads();
+  float tot = 0.f;
+  for (int w2 = 0; w2 < nw; ++w2) tot += red[0][w2];
+  const float mean = tot / d;
+  const float4 q = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+  float sq = ok ? (q.x * q.x + q.y * q.y) + (q.z * q.z + q.w * q.w) : 0.f;
+  sq = wave_sum(sq);
+  if (lane == 0) red[1][wave] = sq;
+  __syncthreads();
+  float tq = 0.f;
+  for (int w2 = 0; w2 < nw; ++w2) tq += red[1][w2];
+  const float rstd = 1.0f / sqrtf(tq / d + 1e-5f);
+  if (ok) {
+    const float4 gg = *reinterpret_cast<const float4*>(g + c), bb = *reinterpret_cast<const float4*>(b + c);
+    const u16x4 h = {from_f32<T>(q.x * rstd * gg.x + bb.x), from_f32<T>(q.y * rstd * gg.y + bb.y),
+                     from_f32<T>(q.z * rstd * gg.z + bb.z), from_f32<T>(q.w * rstd * gg.w + bb.w)};
+    *reinterpret_cast<u16x4*>(out + (long)m * d + c) = h;
+  }
+}
+
 void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float* x, const float* g, const float* b,
                       uint16_t* out16, int rows, int d, hipStream_t st) {
   WMX_CHECK(d <= 2 * kRedThreads && S >= 1 && S <= kRedMaxS, "reduce_ln: width / split count");
   const long pstride = (long)rows * d;
+  static const bool legacy = getenv("WMX_REDLN_LEGACY") != nullptr;  // A/B switch for tuning runs
+  if (!legacy && d % 4 == 0 && d <= 4096) {
+    const int nt = ((d / 4 + 63) / 64) * 64;
+    if (dt == DT::BF16)
+      hipLaunchKernelGGL(reduce_ln4_kernel<DT::BF16>, dim3(rows), dim3(nt), 0, st, part, S, pstride, bias, x, g, b,
+                         out16, d);
+    else
+      hipLaunchKernelGGL(reduce_ln4_kernel<DT::F16>, dim3(rows), dim3(nt), 0, st, part, S, pstride, bias, x, g, b,
+                         out16, d);
+    WMX_HIP(hipGetLastError());
+    return;
+  }
   if (dt == DT::BF16)
     hipLaunchKernelGGL(reduce_ln_kernel<DT::BF16>, dim3(rows), dim3(kRedThreads), 0, st, part, S, pstride, bias, x, g,
                        b, out16, d);
