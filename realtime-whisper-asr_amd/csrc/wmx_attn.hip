@@ -570,9 +570,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) p += q[e] * to_f32<T>(kv[j][e]);
       }
-      p += __shfl_xor(p, 1);
-      p += __shfl_xor(p, 2);
-      p += __shfl_xor(p, 4);
+      p = sum8_lanes(p);
       sc[j] = key <= slot_q ? p : -INFINITY;
       mx = fmaxf(mx, sc[j]);
     }
@@ -603,9 +601,8 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
   // reduce over the 8 key groups of the wave, then over the 4 waves
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    acc[e] += __shfl_xor(acc[e], 8);
-    acc[e] += __shfl_xor(acc[e], 16);
-    acc[e] += __shfl_xor(acc[e], 32);
+    acc[e] += dpp_mov<kDppXor8>(acc[e]);
+    acc[e] = sum_xor32(sum_xor16(acc[e]));
   }
   const float lw = wave_sum(l_run);
   if (lane == 0) red[1][wave] = lw;
@@ -756,8 +753,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     for (int b = 0; b < KPW; ++b)
 #pragma unroll
       for (int j = 0; j < 8; ++j) mx = fmaxf(mx, sv[b][j]);
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = max_xor32(max_xor16(mx));
     const float m_new = fmaxf(m_run, mx);
     const float alpha = __expf(m_run - m_new);  // 0 on the first batch (m_run = -inf)
     float ls = 0.f;
@@ -769,8 +765,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         sv[b][j] = e;
         ls += e;
       }
-    ls += __shfl_xor(ls, 16);
-    ls += __shfl_xor(ls, 32);
+    ls = sum_xor32(sum_xor16(ls));
     l_run = l_run * alpha + ls;
     m_run = m_new;
     // o rows are queries 4g + r: their alpha lives in lane (4g + r) of any group

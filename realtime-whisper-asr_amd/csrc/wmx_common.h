@@ -91,15 +91,53 @@ __device__ inline float erf_fast(float z) {
 }
 __device__ inline float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
-__device__ inline float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
+// ---- cross-lane reductions on DPP and permlane swaps (VALU latency, no LDS round trip as ds_bpermute has).
+// Every lane of the wave must be active.  All lanes end with the bit-identical result (each step combines
+// a value with its partner's, and + / max are commutative).
+template <int CTRL>
+__device__ inline float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppXor1 = 0xB1;      // quad_perm [1,0,3,2]: lane ^ 1
+constexpr int kDppXor2 = 0x4E;      // quad_perm [2,3,0,1]: lane ^ 2
+constexpr int kDppHalfMirror = 0x141;  // lane i <-> 7 - i within 8: the other quad of an 8-lane group
+constexpr int kDppMirror = 0x140;   // lane i <-> 15 - i within 16: the other 8-lane group of a row
+constexpr int kDppXor8 = 0x128;     // row_ror:8: lane ^ 8
+// v + v[lane ^ 16] and v + v[lane ^ 32]: a permlane swap of (v, v) returns this lane's value and its partner's,
+// in either order
+__device__ inline float sum_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float max_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ inline float max_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// sum over each aligned group of 8 lanes
+__device__ inline float sum8_lanes(float v) {
+  v += dpp_mov<kDppXor1>(v);
+  v += dpp_mov<kDppXor2>(v);
+  return v + dpp_mov<kDppHalfMirror>(v);
 }
 __device__ inline float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v = sum8_lanes(v);
+  v += dpp_mov<kDppMirror>(v);
+  return sum_xor32(sum_xor16(v));
+}
+__device__ inline float wave_max(float v) {
+  v = fmaxf(v, dpp_mov<kDppXor1>(v));
+  v = fmaxf(v, dpp_mov<kDppXor2>(v));
+  v = fmaxf(v, dpp_mov<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_mov<kDppMirror>(v));
+  return max_xor32(max_xor16(v));
 }
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
