@@ -424,9 +424,10 @@ struct Ctx {
   int *a_ntok = nullptr, *a_nframes = nullptr, *a_target = nullptr, *a_heads = nullptr;
   int a_heads_cap = 0;
   int* pinned_i = nullptr;
-  // graph
-  hipGraphExec_t graph = nullptr;
-  int graph_B = -1;
+  // decode-step graphs, kept across calls: [0] one step, [1] kGraphChunk steps; valid while graph_key matches
+  // (batch, the rule options baked into the captured launches, the probe placement)
+  hipGraphExec_t graph[2] = {nullptr, nullptr};
+  std::vector<long> graph_key;
   // profiling
   hipEvent_t ev[8];
   // pre-ASR DSP scratch (grown on demand, outside graphs)
@@ -1113,6 +1114,42 @@ static void run_step(Ctx& c, int B) {
                      c.hist_tmp, c.anc, c.anc_tmp, c.Tctx, c.bs, c.n_done, c.st);
 }
 
+// decode steps between n_done read-backs; the chunk is one graph launch
+constexpr int kGraphChunk = 8;
+
+static void drop_step_graphs(Ctx& c) {
+  for (auto& g : c.graph)
+    if (g) {
+      (void)hipGraphExecDestroy(g);
+      g = nullptr;
+    }
+  c.graph_key.clear();
+}
+
+// capture (once per batch size / rule options / probe placement) a one-step and a kGraphChunk-step graph of
+// run_step: every launch reads its step from device state (*slot, histories, ancestry), so a captured step
+// replays correctly at any position of the loop, and consecutive captured steps chain on the stream order
+static void ensure_step_graphs(Ctx& c, int B) {
+  const std::vector<long> key = {B,
+                                 c.o.suppress_blank,
+                                 c.o.max_initial_timestamp_index,
+                                 c.o.without_timestamps,
+                                 (long)(intptr_t)c.mask,
+                                 c.probe_kernel,
+                                 c.probe_layer};
+  if (c.graph[0] && c.graph[1] && key == c.graph_key) return;
+  drop_step_graphs(c);
+  for (int gi = 0; gi < 2; ++gi) {
+    hipGraph_t gph = nullptr;
+    WMX_HIP(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < (gi ? kGraphChunk : 1); ++i) run_step(c, B);
+    WMX_HIP(hipStreamEndCapture(c.st, &gph));
+    WMX_HIP(hipGraphInstantiate(&c.graph[gi], gph, nullptr, nullptr, 0));
+    WMX_HIP(hipGraphDestroy(gph));
+  }
+  c.graph_key = key;
+}
+
 static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const long* lens, const int32_t* seek, int B,
                                 const int32_t* prompt_ids, const int32_t* prompt_lens) {
   Model& m = *c.m;
@@ -1264,21 +1301,15 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
                     : c.probe_kernel == 5 ? (double)R * mean_slot * dtm * 2 * 2
                                           : 0.0;
   }
-  hipGraphExec_t ge = nullptr;
-  hipGraph_t gph = nullptr;
-  if (c.o.use_graph && steps < max_new) {
-    WMX_HIP(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
-    run_step(c, B);
-    WMX_HIP(hipStreamEndCapture(c.st, &gph));
-    WMX_HIP(hipGraphInstantiate(&ge, gph, nullptr, nullptr, 0));
-  }
+  if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
   while (steps < max_new) {
-    const int chunk = std::min(8, max_new - steps);
-    for (int i = 0; i < chunk; ++i) {
-      if (ge)
-        WMX_HIP(hipGraphLaunch(ge, c.st));
-      else
-        run_step(c, B);
+    const int chunk = std::min(kGraphChunk, max_new - steps);
+    if (!c.o.use_graph) {
+      for (int i = 0; i < chunk; ++i) run_step(c, B);
+    } else if (chunk == kGraphChunk) {
+      WMX_HIP(hipGraphLaunch(c.graph[1], c.st));  // one launch per chunk: no per-step graph launch bubble
+    } else {
+      for (int i = 0; i < chunk; ++i) WMX_HIP(hipGraphLaunch(c.graph[0], c.st));
     }
     steps += chunk;
     WMX_HIP(hipMemcpyAsync(c.pinned_i, c.n_done, 4, hipMemcpyDeviceToHost, c.st));
@@ -1286,8 +1317,6 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
 
     if (c.pinned_i[0] >= need_done) break;
   }
-  if (ge) WMX_HIP(hipGraphExecDestroy(ge));
-  if (gph) WMX_HIP(hipGraphDestroy(gph));
   c.last_steps = steps;
   rec(c, 6);
   if (c.probe_kernel >= 0) {
@@ -1757,6 +1786,7 @@ void wmx_ctx_destroy(wmx_ctx* x) {
   Ctx& c = x->c;
   (void)hipSetDevice(c.m->device);
   (void)hipStreamSynchronize(c.st);
+  drop_step_graphs(c);
   if (c.buf) (void)hipFree(c.buf);
   if (c.pinned_i) (void)hipHostFree(c.pinned_i);
   for (auto& e : c.ev)
