@@ -64,6 +64,12 @@ __device__ inline MS ms_add(MS a, float v) {
   }
   return a;
 }
+// branch-free ms_add: identical values (the skipped factor is exp(0) = 1 and s * 1 is exact)
+__device__ inline MS ms_add_nb(MS a, float v) {
+  const float m = fmaxf(a.m, v);
+  const float s = a.s * __expf(a.m - m) + __expf(v - m);
+  return v == -INFINITY ? a : MS{m, s};
+}
 __device__ inline MS ms_merge(MS a, MS b) {
   if (b.m == -INFINITY) return a;
   if (a.m == -INFINITY) return b;
@@ -71,6 +77,29 @@ __device__ inline MS ms_merge(MS a, MS b) {
   return MS{m, a.s * __expf(a.m - m) + b.s * __expf(b.m - m)};
 }
 __device__ inline float ms_lse(MS a) { return a.m == -INFINITY ? -INFINITY : a.m + __logf(a.s); }
+// wave-wide ms_merge on DPP / permlane exchanges (all lanes active; ms_merge is commutative, so every lane ends
+// with the same pair)
+template <int CTRL>
+__device__ inline MS ms_step_dpp(MS a) {
+  return ms_merge(a, MS{dpp_mov<CTRL>(a.m), dpp_mov<CTRL>(a.s)});
+}
+__device__ inline MS wave_ms(MS a) {
+  a = ms_step_dpp<kDppXor1>(a);
+  a = ms_step_dpp<kDppXor2>(a);
+  a = ms_step_dpp<kDppHalfMirror>(a);
+  a = ms_step_dpp<kDppMirror>(a);
+  {
+    const auto m = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.m), __float_as_uint(a.m), false, false);
+    const auto sv = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.s), __float_as_uint(a.s), false, false);
+    a = ms_merge(MS{__uint_as_float(m[0]), __uint_as_float(sv[0])}, MS{__uint_as_float(m[1]), __uint_as_float(sv[1])});
+  }
+  {
+    const auto m = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.m), __float_as_uint(a.m), false, false);
+    const auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.s), __float_as_uint(a.s), false, false);
+    a = ms_merge(MS{__uint_as_float(m[0]), __uint_as_float(sv[0])}, MS{__uint_as_float(m[1]), __uint_as_float(sv[1])});
+  }
+  return a;
+}
 
 constexpr int kSelThreads = 512;
 constexpr int kMaxKP = 9;
@@ -110,6 +139,22 @@ __device__ inline void topk_push(TopK& t, float v, int i, int KP) {
     }
   }
 }
+// compile-time list length, branch-free compare-and-swap chain (the runtime-KP form above compiles to an
+// exec-mask branch per slot; this is ~6 VALU per slot).  better_nb: better() without short-circuit branches.
+__device__ inline bool better_nb(float va, int ia, float vb, int ib) { return (va > vb) | ((va == vb) & (ia < ib)); }
+template <int KPT>
+__device__ inline void topk_push_c(TopK& t, float v, int i) {
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
+    const bool sw = better_nb(v, i, t.v[k], t.i[k]);
+    const float tv = t.v[k];
+    const int ti = t.i[k];
+    t.v[k] = sw ? v : tv;
+    t.i[k] = sw ? i : ti;
+    v = sw ? tv : v;
+    i = sw ? ti : i;
+  }
+}
 __device__ inline void topk_pop(TopK& t) {
 #pragma unroll
   for (int k = 0; k + 1 < kMaxKP; ++k) {
@@ -120,39 +165,93 @@ __device__ inline void topk_pop(TopK& t) {
   t.i[kMaxKP - 1] = 0x7FFFFFFF;
 }
 
-// block-wide: extract the KP best heads of all threads' lists into out (rank order)
+// (v, i) of the best lane of the wave under better(); every lane ends with the same pair.  DPP / permlane
+// exchanges (all lanes active): each step keeps the better of this lane's pair and its partner's, and better()
+// is a strict total order, so both partners keep the same pair.
+template <int CTRL>
+__device__ inline void argmax_step_dpp(float& v, int& i) {
+  const float v2 = dpp_mov<CTRL>(v);
+  const int i2 = __builtin_amdgcn_mov_dpp(i, CTRL, 0xF, 0xF, false);
+  if (better(v2, i2, v, i)) {
+    v = v2;
+    i = i2;
+  }
+}
+__device__ inline void argmax_pick(float& v, int& i, const uint32_t* rv, const uint32_t* ri) {
+  // rv / ri: a permlane swap of (v, v) and (i, i): elements 0 come from one lane, elements 1 from the other
+  const float va = __uint_as_float(rv[0]), vb = __uint_as_float(rv[1]);
+  const int ia = (int)ri[0], ib = (int)ri[1];
+  if (better(va, ia, vb, ib)) {
+    v = va;
+    i = ia;
+  } else {
+    v = vb;
+    i = ib;
+  }
+}
+__device__ inline void wave_argmax(float& v, int& i) {
+  argmax_step_dpp<kDppXor1>(v, i);
+  argmax_step_dpp<kDppXor2>(v, i);
+  argmax_step_dpp<kDppHalfMirror>(v, i);
+  argmax_step_dpp<kDppMirror>(v, i);
+  {
+    const auto rv = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const auto ri = __builtin_amdgcn_permlane16_swap((uint32_t)i, (uint32_t)i, false, false);
+    const uint32_t a[2] = {rv[0], rv[1]}, b[2] = {ri[0], ri[1]};
+    argmax_pick(v, i, a, b);
+  }
+  {
+    const auto rv = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const auto ri = __builtin_amdgcn_permlane32_swap((uint32_t)i, (uint32_t)i, false, false);
+    const uint32_t a[2] = {rv[0], rv[1]}, b[2] = {ri[0], ri[1]};
+    argmax_pick(v, i, a, b);
+  }
+}
+
+// block-wide: extract the KP best heads of all threads' lists into ov / oi (rank order; (-inf, INT_MAX) pads).
+// Each wave first extracts its own KP best (KP wave arg-maxes, the owning lane pops its head: indices are
+// unique, so exactly one lane owns the pair), then wave 0 extracts the KP best of the waves' candidates.
+// Every thread of the block must call it.  rv / ri: scratch of at least (NT / 64) * kMaxKP entries.
 template <int NT>
 __device__ inline void block_topk(TopK& t, int KP, float* ov, int* oi, float* rv, int* ri) {
+  constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int k = 0; k < KP; ++k) {
     float v = t.v[0];
     int i = t.i[0];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const float v2 = __shfl_xor(v, off);
-      const int i2 = __shfl_xor(i, off);
-      if (better(v2, i2, v, i)) {
-        v = v2;
-        i = i2;
+    wave_argmax(v, i);
+    if (t.i[0] == i && i != 0x7FFFFFFF) topk_pop(t);
+    if (NW == 1) {
+      if (lane == 0) {
+        ov[k] = v;
+        oi[k] = i;
       }
+    } else if (lane == 0) {
+      rv[wave * kMaxKP + k] = v;
+      ri[wave * kMaxKP + k] = i;
     }
-    if (lane == 0) {
-      rv[wave] = v;
-      ri[wave] = i;
+  }
+  if (NW == 1) return;
+  __syncthreads();
+  if (wave == 0) {
+    float cv = -INFINITY;
+    int ci = 0x7FFFFFFF;
+    if (lane < NW * KP) {
+      cv = rv[(lane / KP) * kMaxKP + lane % KP];
+      ci = ri[(lane / KP) * kMaxKP + lane % KP];
     }
-    __syncthreads();
-    float bv = rv[0];
-    int bi = ri[0];
-    for (int w = 1; w < NT / 64; ++w)
-      if (better(rv[w], ri[w], bv, bi)) {
-        bv = rv[w];
-        bi = ri[w];
+    for (int k = 0; k < KP; ++k) {
+      float v = cv;
+      int i = ci;
+      wave_argmax(v, i);
+      if (ci == i && i != 0x7FFFFFFF) {
+        cv = -INFINITY;
+        ci = 0x7FFFFFFF;
       }
-    __syncthreads();
-    if (t.i[0] == bi && bi != 0x7FFFFFFF) topk_pop(t);
-    if (tid == 0) {
-      ov[k] = bv;
-      oi[k] = bi;
+      if (lane == 0) {
+        ov[k] = v;
+        oi[k] = i;
+      }
     }
   }
 }
@@ -160,8 +259,9 @@ __device__ inline void block_topk(TopK& t, int KP, float* ov, int* oi, float* rv
 // workspace per (row, slice): [0..4] stats (text.m, text.s, ts.m, ts.s, text max), then KP text (v,i), KP ts (v,i)
 __device__ inline int sel_ws_stride(int KP) { return 5 + 4 * KP; }
 
+template <int KP>
 __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict__ logits, int ldl, RuleOpts o,
-                                                         RowState rs, int KP, const int* row_map, float* __restrict__ ws) {
+                                                         RowState rs, const int* row_map, float* __restrict__ ws) {
   const int r = blockIdx.x, sl = blockIdx.y;
   const int lrow = row_map ? row_map[r] : r;
   const float* x = logits + (long)lrow * ldl;
@@ -190,27 +290,26 @@ __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int t = t0 + 2 * (tid + u * kSelA) + hh;
-      if (t >= o.V || ((mw[u] >> (t & 31)) & 1u) || !allowed_rules(o, t, ns, last_ts, pen_ts, lts)) continue;
-      const float v = hh ? xv[u].y : xv[u].x;
-      if (t < o.tb) {
-        text = ms_add(text, v);
+      // a suppressed token enters as (-inf, INT_MAX): a no-op for the statistics and the top-KP lists
+      const bool ok = t < o.V && !((mw[u] >> (t & 31)) & 1u) && allowed_rules(o, t, ns, last_ts, pen_ts, lts);
+      const float v = ok ? (hh ? xv[u].y : xv[u].x) : -INFINITY;
+      const int ti = ok ? t : 0x7FFFFFFF;
+      if (t < o.tb) {  // wave-uniform except in the slice that holds timestamp_begin
+        text = ms_add_nb(text, v);
         tmax = fmaxf(tmax, v);
-        topk_push(ktx, v, t, KP);
+        topk_push_c<KP>(ktx, v, ti);
       } else {
-        ts = ms_add(ts, v);
-        topk_push(kts, v, t, KP);
+        ts = ms_add_nb(ts, v);
+        topk_push_c<KP>(kts, v, ti);
       }
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    text = ms_merge(text, MS{__shfl_xor(text.m, off), __shfl_xor(text.s, off)});
-    ts = ms_merge(ts, MS{__shfl_xor(ts.m, off), __shfl_xor(ts.s, off)});
-    tmax = fmaxf(tmax, __shfl_xor(tmax, off));
-  }
+  text = wave_ms(text);
+  ts = wave_ms(ts);
+  tmax = wave_max(tmax);
   __shared__ float sm[5][kSelA / 64];
-  __shared__ float rv[kSelA / 64];
-  __shared__ int ri[kSelA / 64];
+  __shared__ float rv[(kSelA / 64) * kMaxKP];
+  __shared__ int ri[(kSelA / 64) * kMaxKP];
   const int wave = tid >> 6, lane = tid & 63;
   if (lane == 0) {
     sm[0][wave] = text.m;
@@ -664,7 +763,23 @@ void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const
   WMX_CHECK(KP <= kMaxKP, "beam too large");
   WMX_CHECK(o.V <= kSlices * kSelPer && ldl % 2 == 0, "logits select: vocabulary / row stride");
   RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
-  hipLaunchKernelGGL(logits_select_a, dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, KP, row_map, ws);
+  switch (KP) {
+#define WMX_SEL_A(N)                                                                                             \
+  case N:                                                                                                        \
+    hipLaunchKernelGGL(logits_select_a<N>, dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, row_map, ws); \
+    break;
+    WMX_SEL_A(1)
+    WMX_SEL_A(2)
+    WMX_SEL_A(3)
+    WMX_SEL_A(4)
+    WMX_SEL_A(5)
+    WMX_SEL_A(6)
+    WMX_SEL_A(7)
+    WMX_SEL_A(8)
+    WMX_SEL_A(9)
+#undef WMX_SEL_A
+    default: WMX_CHECK(false, "logits select: list length");
+  }
   hipLaunchKernelGGL(logits_select_b, dim3(R), dim3(64), 0, st, ws, o, KP, tok, lp);
   WMX_HIP(hipGetLastError());
 }
