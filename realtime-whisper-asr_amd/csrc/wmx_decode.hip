@@ -109,8 +109,8 @@ __device__ inline bool better(float va, int ia, float vb, int ib) { return va > 
 
 // ---- phase A: one block per (row, vocab slice): masked statistics + top-KP of allowed text and timestamp
 //      tokens, kept separately because whether text is masked depends on the whole row ----
-constexpr int kSlices = 8, kSelA = 256;
-constexpr int kSelPer = 6656;                   // vocab entries per slice (8 x 6656 >= 51866), even
+constexpr int kSlices = 16, kSelA = 256;
+constexpr int kSelPer = 3584;                   // vocab entries per slice (16 x 3584 >= 51866), a multiple of 2 kSelA
 constexpr int kSelNL = kSelPer / (2 * kSelA);   // 8-byte loads per thread per slice
 
 struct TopK {
@@ -352,19 +352,25 @@ __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict
 }
 
 // ---- phase B: one wave per row merges the slices: timestamp-forcing rule, log-softmax normaliser, top-KP ----
-__global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ ws, RuleOpts o, int KP,
+template <int KP>
+__global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ ws, RuleOpts o,
                                                       int* __restrict__ out_tok, float* __restrict__ out_lp) {
+  static_assert(kSlices <= 64, "one lane per slice");
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   const float* w = ws + (long)r * kSlices * sel_ws_stride(KP);
+  // lane q < kSlices loads slice q's statistics; one wave-wide merge
   MS T{-INFINITY, 0.f}, S{-INFINITY, 0.f};
   float tmax = -INFINITY;
-  for (int q = 0; q < kSlices; ++q) {
-    const float* x = w + q * sel_ws_stride(KP);
-    T = ms_merge(T, MS{x[0], x[1]});
-    S = ms_merge(S, MS{x[2], x[3]});
-    tmax = fmaxf(tmax, x[4]);
+  if (lane < kSlices) {
+    const float* x = w + lane * sel_ws_stride(KP);
+    T = MS{x[0], x[1]};
+    S = MS{x[2], x[3]};
+    tmax = x[4];
   }
+  T = wave_ms(T);
+  S = wave_ms(S);
+  tmax = wave_max(tmax);
   const float lse_ts = ms_lse(S);
   const bool mask_text = !o.without_ts && (lse_ts > tmax);
   const float lse_text = ms_lse(T);
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ 
     const int q = c / (2 * KP), rem = c % (2 * KP), kind = rem / KP, k = rem % KP;
     if (kind == 0 && mask_text) continue;
     const float* x = w + q * sel_ws_stride(KP) + 5 + 2 * KP * kind;
-    topk_push(t, x[k], __float_as_int(x[KP + k]), KP);
+    topk_push_c<KP>(t, x[k], __float_as_int(x[KP + k]));
   }
   __shared__ float rv[1];
   __shared__ int ri[1];
@@ -767,6 +773,7 @@ void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const
 #define WMX_SEL_A(N)                                                                                             \
   case N:                                                                                                        \
     hipLaunchKernelGGL(logits_select_a<N>, dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, row_map, ws); \
+    hipLaunchKernelGGL(logits_select_b<N>, dim3(R), dim3(64), 0, st, ws, o, tok, lp);                           \
     break;
     WMX_SEL_A(1)
     WMX_SEL_A(2)
@@ -780,7 +787,6 @@ void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const
 #undef WMX_SEL_A
     default: WMX_CHECK(false, "logits select: list length");
   }
-  hipLaunchKernelGGL(logits_select_b, dim3(R), dim3(64), 0, st, ws, o, KP, tok, lp);
   WMX_HIP(hipGetLastError());
 }
 
