@@ -456,21 +456,17 @@ __global__ void beam_select_kernel(RowState rs, const int* __restrict__ ctok, co
   }
   __syncthreads();
   const int s = *slot;
+  // rank sort, one candidate per lane (score desc, beam asc, token asc: a strict total order, since a beam's
+  // candidate tokens are distinct): order[rank of c] = c
+  for (int c = lane; c < nc; c += 64) {
+    int rank = 0;
+    for (int y = 0; y < nc; ++y)
+      rank += cv[y] > cv[c] || (cv[y] == cv[c] && (cb[y] < cb[c] || (cb[y] == cb[c] && ct[y] < ct[c])));
+    order[rank] = c;
+  }
+  __syncthreads();
   if (lane == 0) {
     bs.win_active[w] = 1;
-    for (int c = 0; c < nc; ++c) order[c] = c;
-    for (int a = 1; a < nc; ++a) {  // insertion sort: score desc, beam asc, token asc
-      const int x = order[a];
-      int b = a - 1;
-      while (b >= 0) {
-        const int y = order[b];
-        const bool xb = cv[x] > cv[y] || (cv[x] == cv[y] && (cb[x] < cb[y] || (cb[x] == cb[y] && ct[x] < ct[y])));
-        if (!xb) break;
-        order[b + 1] = y;
-        --b;
-      }
-      order[b + 1] = x;
-    }
     int saved = 0, nn = 0;
     int nf = bs.fin_count[w];
     for (int q = 0; q < nc && saved < K; ++q) {
