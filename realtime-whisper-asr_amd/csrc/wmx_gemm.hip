@@ -10,6 +10,8 @@
 // Epilogues are fused: bias, exact-erf GELU, fp32 residual add (the residual stream stays fp32), conv2's
 // GELU + sinusoidal position add, the decoder QKV scatter straight into the self-attention KV cache, and
 // split-K fp32 partial slabs reduced deterministically (fixed order) by gemm_splitk_reduce.
+#include <cstdlib>
+
 #include "wmx_common.h"
 #include "wmx_kernels.h"
 
@@ -1007,13 +1009,14 @@ static void launch_skinny(const GemmCall& g, hipStream_t st) {
 // fragments + MT activation fragments) before their MFMAs, partial tiles are summed through LDS.
 // Grid (col groups, S, row chunks).  S == 1: epilogue; S > 1: raw fp32 partials part[s][M][N].
 // ------------------------------------------------------------------------------------------------
-template <DT T, int MT, int NCT>
-__global__ __launch_bounds__(256) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
-                                                          const uint16_t* __restrict__ Wp, int M, int N, int K, int S,
-                                                          Epi e, float* __restrict__ part) {
+template <DT T, int MT, int NCT, int NW>
+__global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
+                                                              const uint16_t* __restrict__ Wp, int M, int N, int K,
+                                                              int S, Epi e, float* __restrict__ part) {
   constexpr int KU = (MT + NCT) <= 8 ? 2 : 1;
   constexpr int LDR = 16 * NCT + 1;
-  __shared__ float red[4][MT * 16][LDR];
+  constexpr int NT = 64 * NW;
+  __shared__ float red[NW][MT * 16][LDR];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int ntiles = (N + 15) >> 4;
@@ -1023,7 +1026,7 @@ __global__ __launch_bounds__(256) void gemm_packed_kernel(const uint16_t* __rest
   const int ksteps = K >> 5;
   const int kps = (ksteps + S - 1) / S;
   const int kb = sp * kps, ke = min(ksteps, kb + kps);
-  const int per = (max(0, ke - kb) + 3) >> 2;
+  const int per = (max(0, ke - kb) + NW - 1) / NW;
   const int ks0 = kb + wave * per, ks1 = min(ke, ks0 + per);
   f32x4 acc[MT][NCT];
 #pragma unroll
@@ -1065,13 +1068,18 @@ __global__ __launch_bounds__(256) void gemm_packed_kernel(const uint16_t* __rest
   __syncthreads();
   // 4 consecutive columns per thread
   constexpr int C4 = 4 * NCT;  // column quads per row
-  for (int idx = tid; idx < MT * 16 * C4; idx += 256) {
+  for (int idx = tid; idx < MT * 16 * C4; idx += NT) {
     const int row = idx / C4, c = (idx - row * C4) * 4;
     const int m = m0 + row, n = t0 * 16 + c;
     if (m >= M || n >= N) continue;
     float v4[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v4[q] = red[0][row][c + q] + red[1][row][c + q] + red[2][row][c + q] + red[3][row][c + q];
+    for (int q = 0; q < 4; ++q) {
+      float v = red[0][row][c + q];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += red[w][row][c + q];
+      v4[q] = v;
+    }
     if (S > 1) {
       float* dst = part + ((long)sp * M + m) * N + n;
       if (n + 3 < N && (N & 3) == 0) {
@@ -1111,12 +1119,29 @@ int packed_splits(int M, int N, int K, long cap_elems) {
   return (int)std::max<long>(1, S);
 }
 
+// waves per workgroup: enough that each wave's share of its K slice is at most ~4 k-steps (two dependent load
+// batches), so long unsplit slices (fc1, whose GELU epilogue needs S = 1) are not a chain of five round trips
 template <DT T, int MT, int NCT>
 static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ntiles = (g.N + 15) / 16;
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
-  hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT>), grid, dim3(256), 0, st, g.A, g.lda, g.W, g.M, g.N, g.K, g.S,
-                     g.epi, g.part);
+  const int ksteps = g.K / 32, kps = (ksteps + g.S - 1) / g.S;
+  const int per4 = (kps + 3) / 4;
+  static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
+#define WMX_PACKED_LAUNCH(NWV)                                                                                \
+  hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W, g.M, \
+                     g.N, g.K, g.S, g.epi, g.part)
+  // the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] stays within 64 KiB of static LDS
+  constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 65536;
+  constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 65536;
+  if (only4 || per4 <= 4 || !fit8) {
+    WMX_PACKED_LAUNCH(4);
+  } else if (per4 <= 8 || !fit16) {
+    if constexpr (fit8) WMX_PACKED_LAUNCH(8);
+  } else {
+    if constexpr (fit16) WMX_PACKED_LAUNCH(16);
+  }
+#undef WMX_PACKED_LAUNCH
 }
 
 template <DT T, int NCT>
