@@ -505,20 +505,26 @@ __global__ void beam_select_kernel(RowState rs, const int* __restrict__ ctok, co
 }
 
 // block per row: new row r' <- parent history + token; ancestry row; state.  Windows inactive this step are frozen.
-__global__ void beam_reorder_kernel(RowState rs, int K, int tb, const int* __restrict__ slot, const int* __restrict__ hist,
-                                    int* __restrict__ hist_tmp, const int* __restrict__ anc, int* __restrict__ anc_tmp,
-                                    int ld, BeamState bs, RowState tmp) {
-  const int r = blockIdx.x;
-  const int w = r / K;
+// beam update, one 1024-thread workgroup for all rows (so its barriers order the three phases): (1) copy each
+// row's parent history / ancestry / rule state into the tmp rows, appending the new token at slot + 1; (2) copy
+// the tmp rows back; (3) advance the slot once every thread has read it.  One launch instead of three.
+constexpr int kBeamUpdThreads = 1024;
+__global__ __launch_bounds__(kBeamUpdThreads) void beam_update_kernel(RowState rs, int R, int K, int tb,
+                                                                      int* __restrict__ slot, int* __restrict__ hist,
+                                                                      int* __restrict__ hist_tmp, int* __restrict__ anc,
+                                                                      int* __restrict__ anc_tmp, int ld, BeamState bs,
+                                                                      RowState tmp) {
   const int s = *slot;
-  const bool frozen = !bs.win_active[w];
-  const int p = frozen ? r : bs.new_parent[r];
-  for (int t = threadIdx.x; t <= s; t += blockDim.x) {
+  const int n = s + 1;  // history slots 0..s of every row
+  for (int e = threadIdx.x; e < R * n; e += kBeamUpdThreads) {
+    const int r = e / n, t = e - r * n;
+    const int p = bs.win_active[r / K] ? bs.new_parent[r] : r;
     hist_tmp[(long)r * ld + t] = hist[(long)p * ld + t];
     anc_tmp[(long)r * ld + t] = anc[(long)p * ld + t];
   }
-  if (threadIdx.x == 0) {
-    if (frozen) {
+  if (threadIdx.x < R) {
+    const int r = threadIdx.x;
+    if (!bs.win_active[r / K]) {
       tmp.ns[r] = rs.ns[r];
       tmp.last[r] = rs.last[r];
       tmp.pen[r] = rs.pen[r];
@@ -526,6 +532,7 @@ __global__ void beam_reorder_kernel(RowState rs, int K, int tb, const int* __res
       tmp.sum_lp[r] = rs.sum_lp[r];
       hist_tmp[(long)r * ld + s + 1] = 0;
     } else {
+      const int p = bs.new_parent[r];
       const int t = bs.new_tok[r];
       hist_tmp[(long)r * ld + s + 1] = t;
       tmp.ns[r] = rs.ns[p] + 1;
@@ -536,27 +543,24 @@ __global__ void beam_reorder_kernel(RowState rs, int K, int tb, const int* __res
     }
     anc_tmp[(long)r * ld + s + 1] = r;
   }
-}
-
-__global__ void beam_commit_kernel(RowState rs, const int* __restrict__ hist_tmp, int* __restrict__ hist,
-                                   const int* __restrict__ anc_tmp, int* __restrict__ anc, int ld, RowState tmp,
-                                   const int* __restrict__ slot) {
-  const int r = blockIdx.x;
-  const int s = *slot;
-  for (int t = threadIdx.x; t <= s + 1; t += blockDim.x) {
+  __syncthreads();  // workgroup-scope fence: the tmp rows are visible to every thread of the block
+  const int n2 = s + 2;
+  for (int e = threadIdx.x; e < R * n2; e += kBeamUpdThreads) {
+    const int r = e / n2, t = e - r * n2;
     hist[(long)r * ld + t] = hist_tmp[(long)r * ld + t];
     anc[(long)r * ld + t] = anc_tmp[(long)r * ld + t];
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < R) {
+    const int r = threadIdx.x;
     rs.ns[r] = tmp.ns[r];
     rs.last[r] = tmp.last[r];
     rs.pen[r] = tmp.pen[r];
     rs.last_ts[r] = tmp.last_ts[r];
     rs.sum_lp[r] = tmp.sum_lp[r];
   }
+  __syncthreads();  // every thread has read *slot
+  if (threadIdx.x == 0) *slot = s + 1;
 }
-
-__global__ void advance_slot_kernel(int* slot) { *slot += 1; }
 
 // language detection: argmax over language tokens of the logits at <|startoftranscript|>; writes the token into
 // the prompt of every row of the window
@@ -803,10 +807,9 @@ void launch_beam_step(const RowPtrs& rp, const RowPtrs& tmp, const int* ctok, co
   const int R = nwin * K;
   hipLaunchKernelGGL(beam_select_kernel, dim3(nwin), dim3(64), 0, st, rs, ctok, clp, K, max_cand, eot, slot, hist, ld, bs,
                      n_done);
-  hipLaunchKernelGGL(beam_reorder_kernel, dim3(R), dim3(128), 0, st, rs, K, tb, slot, hist, hist_tmp, anc, anc_tmp, ld,
-                     bs, ts);
-  hipLaunchKernelGGL(beam_commit_kernel, dim3(R), dim3(128), 0, st, rs, hist_tmp, hist, anc_tmp, anc, ld, ts, slot);
-  hipLaunchKernelGGL(advance_slot_kernel, dim3(1), dim3(1), 0, st, slot);
+  WMX_CHECK(R <= kBeamUpdThreads, "beam update: rows");
+  hipLaunchKernelGGL(beam_update_kernel, dim3(1), dim3(kBeamUpdThreads), 0, st, rs, R, K, tb, slot, hist, hist_tmp,
+                     anc, anc_tmp, ld, bs, ts);
   WMX_HIP(hipGetLastError());
 }
 
