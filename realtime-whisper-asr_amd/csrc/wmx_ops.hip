@@ -270,6 +270,79 @@ void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const
   WMX_HIP(hipGetLastError());
 }
 
+// ---------------- decode step: token + position embedding and the first layer's LN1 in one launch ----------------
+// one wave per row (4 rows per workgroup); the same arithmetic as embed_kernel followed by layernorm_kernel
+template <DT T>
+__global__ __launch_bounds__(256) void embed_ln_kernel(const uint16_t* __restrict__ tok_emb,
+                                                       const uint16_t* __restrict__ pos_emb, const int* __restrict__ hist,
+                                                       long hist_ld, const int* __restrict__ pad,
+                                                       const int* __restrict__ slot0, const float* __restrict__ g,
+                                                       const float* __restrict__ bb, int rows, int d,
+                                                       float* __restrict__ x, uint16_t* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const int slot = *slot0;
+  const int tok = hist[(long)r * hist_ld + slot];
+  const int pos = max(slot - (pad ? pad[r] : 0), 0);
+  const int n4 = d >> 2;
+  float4 v[8];  // d <= 2048
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      // four consecutive k of one packed row are contiguous (packed_index keeps k & 7 innermost)
+      const u16x4 te = *reinterpret_cast<const u16x4*>(tok_emb + packed_index(tok, 4 * c, d));
+      const u16x4 pe = *reinterpret_cast<const u16x4*>(pos_emb + (long)pos * d + 4 * c);
+      v[i] = make_float4(to_f32<T>(te[0]) + to_f32<T>(pe[0]), to_f32<T>(te[1]) + to_f32<T>(pe[1]),
+                         to_f32<T>(te[2]) + to_f32<T>(pe[2]), to_f32<T>(te[3]) + to_f32<T>(pe[3]));
+      reinterpret_cast<float4*>(x + (long)r * d)[c] = v[i];
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+  }
+  const float mean = wave_sum(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, e = v[i].w - mean;
+      q += a * a + b * b + cc * cc + e * e;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / d + 1e-5f);
+  uint16_t* o = out + (long)r * d;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = lane + i * 64;
+    if (c < n4) {
+      const float4 gg = reinterpret_cast<const float4*>(g)[c];
+      const float4 be = reinterpret_cast<const float4*>(bb)[c];
+      u16x4 w;
+      w[0] = from_f32<T>((v[i].x - mean) * rstd * gg.x + be.x);
+      w[1] = from_f32<T>((v[i].y - mean) * rstd * gg.y + be.y);
+      w[2] = from_f32<T>((v[i].z - mean) * rstd * gg.z + be.z);
+      w[3] = from_f32<T>((v[i].w - mean) * rstd * gg.w + be.w);
+      reinterpret_cast<u16x4*>(o)[c] = w;
+    }
+  }
+}
+
+void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
+                     const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,
+                     hipStream_t st) {
+  WMX_CHECK(d % 32 == 0 && d <= 2048, "embed_ln: d");
+  dim3 grid(cdiv(R, 4));
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(embed_ln_kernel<DT::BF16>, grid, dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, pad, slot0,
+                       g, b, R, d, x, out);
+  else
+    hipLaunchKernelGGL(embed_ln_kernel<DT::F16>, grid, dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, pad, slot0,
+                       g, b, R, d, x, out);
+  WMX_HIP(hipGetLastError());
+}
+
 // ---------------- split-K reduction + residual + LayerNorm (decode step) ----------------
 // one 1024-thread workgroup per row: every partial slice of the thread's columns is loaded in one batch (slice
 // order kept in the sum), v = x + bias + sum_s part[s], x = v, out16 = LN(v) * g + b

@@ -817,15 +817,15 @@ struct FwdArgs {
 
 // Decode step (Tn == 1): every projection runs on packed weights with split-K partials, and the reductions are
 // fused into the consumers -- q/k/v into self attention (which also writes the KV cache), cross q into cross
-// attention, out-proj / fc2 into reduce_ln (residual add + the next LayerNorm).  10 launches per layer.
+// attention, out-proj / fc2 into reduce_ln (residual add + the next LayerNorm).  11 launches per layer.
 // Leaves LN_final(x) of every row in c.dhb.
 static void dec_step_fast(Ctx& c, const FwdArgs& f) {
   Model& m = *c.m;
   const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
   const int R = f.rows;
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
-  launch_embed(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, 1, f.pad_seq, c.slot, dt, c.dx, c.st);
-  launch_layernorm(c.dt, c.dx, m.dec[0].ln1g, m.dec[0].ln1b, c.dhb, R, dt, c.st);
+  launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, m.dec[0].ln1g, m.dec[0].ln1b, dt,
+                  c.dx, c.dhb, c.st);
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
     const bool last = l + 1 == Lt;
