@@ -348,12 +348,16 @@ __device__ inline void epi_from_image(const Epi& e, const float* img, int ldt, i
 // and rows r0, r0 + 8, ... (r0 = tid / 64): the bias is loaded once, and every row's loads (image, residual,
 // position) are issued before its stores, so the store tail is not a chain of dependent global round trips.
 template <DT T, int KIND>
-__device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid) {
+__device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
+                                  const float4* bpre = nullptr) {
   const int c4 = (tid & 63) * 4, r0 = tid >> 6;
   const int n = n0 + c4;
   if (n >= N) return;
   float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e.bias) b = *reinterpret_cast<const float4*>(e.bias + n);
+  if (bpre)  // loaded by the caller at tile start, so no round of the epilogue waits on it
+    b = *bpre;
+  else if (e.bias)
+    b = *reinterpret_cast<const float4*>(e.bias + n);
   float4 v[8], aux[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
@@ -394,10 +398,11 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
 }
 
 template <DT T, int KIND>
-__device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid) {
+__device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
+                                   const float4* bpre = nullptr) {
   if constexpr (KIND == EPI_CROSSKV) {  // specialised cross-K/V launch (host: d % 256 == 0, xt % 4 == 0)
     if (((n0 / e.d) & 1) == 0) {
-      epi_rows64<T, EPI_CROSSKV>(e, img, ldt, mb, n0, M, N, tid);
+      epi_rows64<T, EPI_CROSSKV>(e, img, ldt, mb, n0, M, N, tid, bpre);
     } else {  // V^T: 4 consecutive keys of one column per 8-byte store
       const int col = tid & 255, r4 = (tid >> 8) * 4, n = n0 + col;
       const float b = e.bias ? e.bias[n] : 0.f;
@@ -413,7 +418,7 @@ __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int 
     }
     return;
   } else if constexpr (KIND >= 0) {  // specialised launch: the host checked the vector conditions
-    epi_rows64<T, KIND>(e, img, ldt, mb, n0, M, N, tid);
+    epi_rows64<T, KIND>(e, img, ldt, mb, n0, M, N, tid, bpre);
     return;
   }
   const bool vec = (N & 3) == 0 && (e.ldc & 3) == 0;
@@ -498,7 +503,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   const int tilesN = (N + BN - 1) / BN;
   const int tilesM = (M + BM - 1) / BM;
   const int nwg = tilesN * tilesM;
-  int bid = blockIdx.x;
+  // persistent: a workgroup walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8, so a tile stays on
+  // the XCD the remap below assumes); the previous tile's epilogue stores drain while the next tile's first
+  // slices are in flight, and the workgroup's LDS is not released and re-acquired per tile
+  for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
+  int bid = tile;
   {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -514,6 +523,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int nk = K >> 5;
+  // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias, loaded now so its latency hides behind
+  // the main loop (the epilogue's column quads are the same in all four rounds)
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (KIND >= 0 && e.bias && n0 + 4 * (tid & 63) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (tid & 63));
 
   // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
   // Wave w issues pieces w, w + 8, w + 16, w + 24; lane l covers row l >> 2, 16-B column (l & 3).
@@ -625,6 +638,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
 
+#if WMX_G256_MODE == 3  // ablation: main loop only (keeps the accumulators live through an untaken store)
+  {
+    float sacc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sacc == 1234.5f) reinterpret_cast<float*>(e.out)[tid] = sacc;
+    continue;
+  }
+#endif
   // epilogue: 4 rounds of 64 rows through an fp32 LDS image [64][BN + 4]
   constexpr int LDT = BN + 4;
   float* img = reinterpret_cast<float*>(smem);
@@ -641,9 +665,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
       }
     }
     __syncthreads();
-    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid);
+    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
     __syncthreads();
   }
+  }  // tile loop
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1207,9 +1232,23 @@ static void g256_attr() {
   g256_attr_one<T, EPI_GELU_MX8>();
   g256_attr_one<T, EPI_CROSSKV>();
 }
+// persistent grid: one workgroup per CU (the 128 KiB ring allows no second one), a multiple of 8 workgroups
+static int g256_grid(int tiles) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      n = 256;
+    return std::max(8, n / 8 * 8);
+  }();
+  static const bool one_tile = getenv("WMX_G256_NONPERSIST") != nullptr;  // A/B switch: one tile per workgroup
+  return one_tile ? tiles : std::min(tiles, cus);
+}
+
 template <DT T>
 static void launch_g256(const GemmCall& g, hipStream_t st) {
-  const int tiles = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  const int ntile = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  const int tiles = g256_grid(ntile);
   const bool vec = (g.N & 3) == 0 && (g.epi.ldc & 3) == 0;
   const int kind = (vec || g.epi.kind == EPI_CROSSKV) ? g.epi.kind : -1;
 #define WMX_G256_LAUNCH(KD)                                                                                    \
