@@ -309,6 +309,10 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
 #else
 #define WMX_G256_MFMA(a, b, c) mfma16<T>(a, b, c)
 #endif
+#ifdef WMX_G256_STAMPS
+constexpr int kG256Stamps = 16384;
+__device__ unsigned long long g256_stamps[kG256Stamps][3];
+#endif
 constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
 constexpr int kG256Lds = 4 * kG256Slot;     // 128 KiB
 
@@ -507,6 +511,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   // the XCD the remap below assumes); the previous tile's epilogue stores drain while the next tile's first
   // slices are in flight, and the workgroup's LDS is not released and re-acquired per tile
   for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
+#ifdef WMX_G256_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
   int bid = tile;
   {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -637,6 +644,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   }
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
+#ifdef WMX_G256_STAMPS
+  const unsigned long long st1 = __builtin_amdgcn_s_memtime();
+#endif
 
 #if WMX_G256_MODE == 3  // ablation: main loop only (keeps the accumulators live through an untaken store)
   {
@@ -668,6 +678,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
     __syncthreads();
   }
+#ifdef WMX_G256_STAMPS  // diagnostic build only (tools/mb_gemm256 -DWMX_G256_STAMPS): per-tile phase clocks
+  if (tid == 0 && tile < kG256Stamps) {
+    g256_stamps[tile][0] = st0;
+    g256_stamps[tile][1] = st1;
+    g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   }  // tile loop
 }
 

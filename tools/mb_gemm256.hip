@@ -93,6 +93,19 @@ int main(int argc, char** argv) {
     h.tile = TILE_256;
     h.epi.out = C2;
     const float t2 = timeit([&] { launch_gemm(DT::BF16, h, 0); }, iters);
+#ifdef WMX_G256_STAMPS
+    {  // per-tile phase clocks of the last timed launch: main loop (incl. prologue) vs epilogue, in shader clocks
+      static unsigned long long stv[kG256Stamps][3];
+      hipMemcpyFromSymbol(stv, HIP_SYMBOL(g256_stamps), sizeof(stv));
+      const int nt = std::min(kG256Stamps, ((s.M + 255) / 256) * ((s.N + 255) / 256));
+      double mainc = 0, epic = 0;
+      for (int t = 0; t < nt; ++t) {
+        mainc += (double)(stv[t][1] - stv[t][0]);
+        epic += (double)(stv[t][2] - stv[t][1]);
+      }
+      printf("  stamps %s: main %.0f clk, epilogue %.0f clk per tile (%d tiles)\n", s.name, mainc / nt, epic / nt, nt);
+    }
+#endif
     hipDeviceSynchronize();
     const long n = (long)s.M * s.N;
     std::vector<uint16_t> a(n), b(n);
