@@ -313,6 +313,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
 constexpr int kG256Stamps = 16384;
 __device__ unsigned long long g256_stamps[kG256Stamps][3];
 #endif
+#ifndef WMX_G256_DIRECT
+#define WMX_G256_DIRECT 1  // LDS-free epilogue for the bf16-output kinds (0: the LDS-image epilogue for all)
+#endif
 constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
 constexpr int kG256Lds = 4 * kG256Slot;     // 128 KiB
 
@@ -532,8 +535,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   const int nk = K >> 5;
   // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias, loaded now so its latency hides behind
   // the main loop (the epilogue's column quads are the same in all four rounds)
+  // (direct epilogue kinds: the lane's column quad after the in-quad transpose, wn 64 + 16 (fr & 3) + 4 (fr >> 2))
+  constexpr bool kDirect = WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16);
+  const int bcol = kDirect ? (wave & 3) * 64 + 16 * (lane & 3) + 4 * ((lane >> 2) & 3) : 4 * (tid & 63);
   float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (KIND >= 0 && e.bias && n0 + 4 * (tid & 63) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (tid & 63));
+  if (KIND >= 0 && e.bias && n0 + bcol < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
 
   // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
   // Wave w issues pieces w, w + 8, w + 16, w + 24; lane l covers row l >> 2, 16-B column (l & 3).
@@ -659,6 +665,64 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     continue;
   }
 #endif
+  if constexpr (kDirect) {
+    // LDS-free epilogue: for every (fragment row i, register r) the 16 lanes of a row group hold columns
+    // 16 j + fr (j = 0..3) of one output row; a 4 x 4 transpose inside each lane quad (lane-dependent register
+    // rotation, three DPP quad rotations, rotation back) leaves lane (fr) with the 4 consecutive columns
+    // wn 64 + 16 (fr & 3) + 4 (fr >> 2) .. +3, stored as one 8-byte bf16 quad.  No image, no barriers.
+    const int q = lane & 3;
+    const int n = n0 + bcol;
+    {  // every lane takes part in the DPP exchanges; only the stores are guarded
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 128 + i * 16 + fq * 4 + r;
+          float v0 = acc[i][0][r], v1 = acc[i][1][r], v2 = acc[i][2][r], v3 = acc[i][3][r];
+          // u[k] = v[(q + k) & 3]
+          if (q & 1) {
+            const float t = v0;
+            v0 = v1, v1 = v2, v2 = v3, v3 = t;
+          }
+          if (q & 2) {
+            float t = v0;
+            v0 = v2, v2 = t;
+            t = v1, v1 = v3, v3 = t;
+          }
+          // u'[k] = u[k] of quad lane (q - k) & 3
+          v1 = dpp_mov<0x93>(v1);  // quad_perm [3,0,1,2]
+          v2 = dpp_mov<0x4E>(v2);  // quad_perm [2,3,0,1]
+          v3 = dpp_mov<0x39>(v3);  // quad_perm [1,2,3,0]
+          // w[m] = u'[(q - m) & 3] = x[(m - q) & 3] with x = (u'0, u'3, u'2, u'1)
+          float x0 = v0, x1 = v3, x2 = v2, x3 = v1;
+          if (q & 1) {
+            const float t = x3;
+            x3 = x2, x2 = x1, x1 = x0, x0 = t;
+          }
+          if (q & 2) {
+            float t = x0;
+            x0 = x2, x2 = t;
+            t = x1, x1 = x3, x3 = t;
+          }
+          float4 o = make_float4(x0 + bias4.x, x1 + bias4.y, x2 + bias4.z, x3 + bias4.w);
+          if (KIND == EPI_GELU16) o = make_float4(gelu_erf(o.x), gelu_erf(o.y), gelu_erf(o.z), gelu_erf(o.w));
+          if (m < M && n < N) {
+            const u16x4 h = {from_f32<T>(o.x), from_f32<T>(o.y), from_f32<T>(o.z), from_f32<T>(o.w)};
+            *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
+          }
+        }
+      }
+    }
+#ifdef WMX_G256_STAMPS
+    if (tid == 0 && tile < kG256Stamps) {
+      g256_stamps[tile][0] = st0;
+      g256_stamps[tile][1] = st1;
+      g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+    __syncthreads();  // the next tile's DMA must not overwrite the ring before every wave left this tile
+    continue;
+  }
   // epilogue: 4 rounds of 64 rows through an fp32 LDS image [64][BN + 4]
   constexpr int LDT = BN + 4;
   float* img = reinterpret_cast<float*>(smem);
