@@ -259,8 +259,18 @@ def main():
     e_ms, _, e_fl = ctx.bench_kernel("encoder", Bg, iters=3)
     e_tf = e_fl / (e_ms * 1e-3) / 1e12
     insitu_tf = G * e_fl / (stages[1] * 1e-3) / 1e12 if stages[1] > 0 else None
+    # the same pass over the whole per-GPU batch (B windows in one launch sequence), in a scratch context
+    e_ms_b, e_fl_b = e_ms, e_fl
+    if G > 1:
+        scratch = engine.Context(model, max_batch=B, beam_size=1, max_new_tokens=8, word_timestamps=False,
+                                 use_graph=False)
+        e_ms_b, _, e_fl_b = scratch.bench_kernel("encoder", B, iters=3)
+        scratch.close()
+    e_tf_b = e_fl_b / (e_ms_b * 1e-3) / 1e12
     encoder = {"windows": Bg, "gflop_per_window": round(e_fl / Bg / 1e9, 1), "isolated_ms": round(e_ms, 2),
                "isolated_tflops": round(e_tf, 1), "isolated_mfma_util": round(e_tf / MFMA_BF16_PEAK_TFLOPS, 4),
+               "isolated_gpu_batch": {"windows": B, "ms": round(e_ms_b, 2), "tflops": round(e_tf_b, 1),
+                                      "mfma_util": round(e_tf_b / MFMA_BF16_PEAK_TFLOPS, 4)},
                "insitu_stage_ms": round(stages[1], 2),
                "insitu_tflops": round(insitu_tf, 1) if insitu_tf else None,
                "insitu_mfma_util": round(insitu_tf / MFMA_BF16_PEAK_TFLOPS, 4) if insitu_tf else None,
