@@ -452,12 +452,16 @@ __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int 
 
 // 64-row x 128-column image, 512 threads: a thread owns column quad (tid & 31) and rows (tid >> 5) + 16u
 template <DT T, int KIND>
-__device__ inline void epi_rows64_n128(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid) {
+__device__ inline void epi_rows64_n128(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
+                                      const float4* bpre = nullptr) {
   const int c4 = (tid & 31) * 4, r0 = tid >> 5;
   const int n = n0 + c4;
   if (n >= N) return;
   float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (e.bias) b = *reinterpret_cast<const float4*>(e.bias + n);
+  if (bpre)
+    b = *bpre;
+  else if (e.bias)
+    b = *reinterpret_cast<const float4*>(e.bias + n);
   float4 v[4], aux[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -491,12 +495,12 @@ __device__ inline void epi_rows64_n128(const Epi& e, const float* img, int ldt, 
 
 template <DT T>
 __device__ inline void epi_image64_n128(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N,
-                                        int tid) {
+                                        int tid, const float4* bpre = nullptr) {
   switch (e.kind) {  // the host allows only these kinds, with N and ldc multiples of 4
-    case EPI_STORE16: epi_rows64_n128<T, EPI_STORE16>(e, img, ldt, mb, n0, M, N, tid); break;
-    case EPI_RESID32: epi_rows64_n128<T, EPI_RESID32>(e, img, ldt, mb, n0, M, N, tid); break;
-    case EPI_STORE32: epi_rows64_n128<T, EPI_STORE32>(e, img, ldt, mb, n0, M, N, tid); break;
-    case EPI_GELU_MX8: epi_rows64_n128<T, EPI_GELU_MX8>(e, img, ldt, mb, n0, M, N, tid); break;
+    case EPI_STORE16: epi_rows64_n128<T, EPI_STORE16>(e, img, ldt, mb, n0, M, N, tid, bpre); break;
+    case EPI_RESID32: epi_rows64_n128<T, EPI_RESID32>(e, img, ldt, mb, n0, M, N, tid, bpre); break;
+    case EPI_STORE32: epi_rows64_n128<T, EPI_STORE32>(e, img, ldt, mb, n0, M, N, tid, bpre); break;
+    case EPI_GELU_MX8: epi_rows64_n128<T, EPI_GELU_MX8>(e, img, ldt, mb, n0, M, N, tid, bpre); break;
     default: break;
   }
 }
@@ -781,7 +785,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
   const int tilesN = (N + BN - 1) / BN;
   const int tilesM = (M + BM - 1) / BM;
   const int nwg = tilesN * tilesM;
-  int bid = blockIdx.x;
+  // persistent over tiles, as gemm256_kernel (gridDim.x a multiple of 8)
+  for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
+  int bid = tile;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -792,6 +798,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
   const int gm = min(GM, tilesM - grp * GM);
   const int tm = grp * GM + gr % gm, tn = gr / gm;
   const int m0 = tm * BM, n0 = tn * BN;
+  // the epilogue's bias column quad (n0 + 4 (tid & 31)), loaded at tile start
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e.bias && n0 + 4 * (threadIdx.x & 31) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (threadIdx.x & 31));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int nk = K >> 7;
@@ -939,16 +948,19 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
           for (int r = 0; r < 4; ++r) img[(i * 16 + g * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
     }
     __syncthreads();
-    epi_image64_n128<T>(e, img, LDT, m0 + rd * 64, n0, M, N, tid);
+    epi_image64_n128<T>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
     __syncthreads();
   }
+  }  // tile loop
 }
+
+static int g256_grid(int tiles);
 
 template <DT T>
 static void launch_mx8_t(const Mx8Call& g, hipStream_t st) {
   const int tiles = ((g.M + 255) / 256) * ((g.N + 127) / 128);
-  hipLaunchKernelGGL((gemm_mx8_kernel<T>), dim3(tiles), dim3(512), kMx8Lds, st, g.A, g.lda, g.AS, g.ldas, g.W, g.ldw,
-                     g.WS, g.ldws, g.M, g.N, g.K, g.epi);
+  hipLaunchKernelGGL((gemm_mx8_kernel<T>), dim3(g256_grid(tiles)), dim3(512), kMx8Lds, st, g.A, g.lda, g.AS, g.ldas,
+                     g.W, g.ldw, g.WS, g.ldws, g.M, g.N, g.K, g.epi);
 }
 
 void launch_gemm_mx8(DT dt, const Mx8Call& g, hipStream_t st) {
