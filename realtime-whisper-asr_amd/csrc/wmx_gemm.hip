@@ -1249,9 +1249,9 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
 #define WMX_PACKED_LAUNCH(NWV)                                                                                \
   hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W, g.M, \
                      g.N, g.K, g.S, g.epi, g.part)
-  // the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] stays within 64 KiB of static LDS
-  constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 65536;
-  constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 65536;
+  // the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] stays within 80 KiB of LDS (two workgroups per CU)
+  constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
+  constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
   if (only4 || per4 <= 4 || !fit8) {
     WMX_PACKED_LAUNCH(4);
   } else if (per4 <= 8 || !fit16) {
