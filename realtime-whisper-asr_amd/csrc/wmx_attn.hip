@@ -891,7 +891,9 @@ static int cross_chunk(int Tk, int nq) {
   }();
   if (nq > 16) return Tk;  // prefill: many query tiles already fill the chip
   if (env) return env;
-  return 512;  // large-v3, 8 windows: 512-key chunks beat 256 by 5-10 % per decode step (bench.py sweep, r01)
+  // large-v3, 2 groups x 4 windows, 8 waves per workgroup: 1024-key chunks (2 per window-head) 600-602 ms per call,
+  // 768: 603-605, 512 with 4 waves: 610-625 (interleaved bench.py sweep, r01); 512 beat 256 with 4 waves
+  return 1024;
 }
 
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
@@ -909,10 +911,10 @@ static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
   WMX_CHECK(KS == 1 || chunk % 32 == 0, "cross attn: key chunks must be whole 32-key blocks");
   WMX_CHECK(KS == 1 || (ws != nullptr && a.xcnt != nullptr && nq <= 16), "cross attn: split workspace required");
   dim3 grid(a.H, nwin, KS * QT);
-  // WMX_XATTN_WAVES=8: 8 waves per workgroup (half the keys per wave), for tuning runs
+  // decode: 8 waves per workgroup (a 1024-key chunk is one 128-key batch per wave); WMX_XATTN_WAVES=4 for tuning
   static const int waves = [] {
     const char* v = getenv("WMX_XATTN_WAVES");
-    return v && atoi(v) == 8 ? 8 : 4;
+    return v && atoi(v) == 4 ? 4 : 8;
   }();
   if (waves == 8 && nq <= 16) {
     const int per_wave = ((chunk + 7) / 8 + 31) / 32;
