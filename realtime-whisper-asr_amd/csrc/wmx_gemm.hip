@@ -1229,7 +1229,11 @@ int packed_splits(int M, int N, int K, long cap_elems) {
   const int chunks = (M + mt * 16 - 1) / (mt * 16);
   const int nct = packed_nct(M, N, K);
   const long wgs = (long)((N + 16 * nct - 1) / (16 * nct)) * chunks;
-  long S = (480 + wgs - 1) / wgs;
+  static const long target = [] {  // workgroups a split aims for; WMX_PACKED_TARGET overrides (tuning runs)
+    const char* v = getenv("WMX_PACKED_TARGET");
+    return v ? std::max(1L, atol(v)) : 480L;
+  }();
+  long S = (target + wgs - 1) / wgs;
   S = std::min<long>(S, std::max(1, (K / 32) / 4));
   S = std::min<long>(S, K / (2L * std::max(M, 1)));
   S = std::min<long>(S, 8);  // the consumers load every slice of a value in one batch (reduce_ln: kRedMaxS)
