@@ -703,23 +703,40 @@ __global__ __launch_bounds__(256) void align_softmax_kernel(float* __restrict__ 
   }
 }
 
+// per (frame, alignment head, window): normalise the frame's column over the window's T tokens (mean, then centred
+// variance, as openai timing.find_alignment).  Workgroup = 64 frames x 4 token groups: each thread walks every 4th
+// token, 4 loads in flight, and the 4 partial sums meet in LDS (fixed order, so the result is deterministic).
 __global__ __launch_bounds__(256) void align_colnorm_kernel(float* __restrict__ scores, int rows_total, int Tk, int Tn,
                                                             const int* __restrict__ ntok,
                                                             const int* __restrict__ nframes) {
-  const int f = blockIdx.x * 256 + threadIdx.x, hh = blockIdx.y, w = blockIdx.z;
+  const int fl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + fl, hh = blockIdx.y, w = blockIdx.z;
   const int T = ntok[w], nf = nframes[w] / 2;
-  if (f >= nf || T <= 0) return;
-  float* s = scores + ((long)hh * rows_total + (long)w * Tn) * Tk + f;
-  float mean = 0.f;
-  for (int t = 0; t < T; ++t) mean += s[(long)t * Tk];
-  mean /= T;
-  float var = 0.f;
-  for (int t = 0; t < T; ++t) {
-    const float dlt = s[(long)t * Tk] - mean;
-    var += dlt * dlt;
-  }
-  const float inv = 1.0f / sqrtf(var / T);
-  for (int t = 0; t < T; ++t) s[(long)t * Tk] = (s[(long)t * Tk] - mean) * inv;
+  if (T <= 0 || blockIdx.x * 64 >= nf) return;  // whole-block exit: every thread of it agrees
+  const bool ok = f < nf;
+  float* s = scores + ((long)hh * rows_total + (long)w * Tn) * Tk + (ok ? f : 0);
+  __shared__ float red[4][64];
+  auto colsum = [&](auto&& term) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int t = g;
+    for (; t + 12 < T; t += 16) {
+      a0 += term(s[(long)t * Tk]);
+      a1 += term(s[(long)(t + 4) * Tk]);
+      a2 += term(s[(long)(t + 8) * Tk]);
+      a3 += term(s[(long)(t + 12) * Tk]);
+    }
+    for (; t < T; t += 4) a0 += term(s[(long)t * Tk]);
+    red[g][fl] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    const float tot = (red[0][fl] + red[1][fl]) + (red[2][fl] + red[3][fl]);
+    __syncthreads();
+    return tot;
+  };
+  const float mean = colsum([](float v) { return v; }) / T;
+  const float var = colsum([mean](float v) { return (v - mean) * (v - mean); }) / T;
+  const float inv = 1.0f / sqrtf(var);
+  if (ok)
+    for (int t = g; t < T; t += 4) s[(long)t * Tk] = (s[(long)t * Tk] - mean) * inv;
 }
 
 __global__ __launch_bounds__(256) void align_median_acc_kernel(const float* __restrict__ scores, int nh, int rows_total,
@@ -753,12 +770,14 @@ __global__ __launch_bounds__(256) void align_median_acc_kernel(const float* __re
   }
 }
 
+// one workgroup per (token row, window): the row's frames scaled in place
 __global__ void align_scale_kernel(float* __restrict__ out, int Tn, int Tk, const int* __restrict__ ntok,
                                    const int* __restrict__ nframes, float scale) {
-  const int w = blockIdx.x;
+  const int t = blockIdx.x, w = blockIdx.y;
   const int T = ntok[w], nf = nframes[w] / 2;
-  float* o = out + (long)w * Tn * Tk;
-  for (int i = threadIdx.x; i < T * nf; i += 256) o[(long)(i / nf) * Tk + i % nf] *= scale;
+  if (t >= T) return;
+  float* o = out + ((long)w * Tn + t) * Tk;
+  for (int f = threadIdx.x; f < nf; f += 256) o[f] *= scale;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -839,7 +858,7 @@ void launch_align_matrix_acc(float* scores, int nh, int rows_total, int Tk, int 
   WMX_CHECK(width <= 15 && width % 2 == 1 && Tk <= 1536, "alignment: median filter width / frames");
   hipLaunchKernelGGL(align_softmax_kernel, dim3(Tn, nh, nwin), dim3(256), 0, st, scores, rows_total, Tk, Tn, ntok,
                      nframes);
-  hipLaunchKernelGGL(align_colnorm_kernel, dim3((Tk + 255) / 256, nh, nwin), dim3(256), 0, st, scores, rows_total, Tk,
+  hipLaunchKernelGGL(align_colnorm_kernel, dim3((Tk + 63) / 64, nh, nwin), dim3(256), 0, st, scores, rows_total, Tk,
                      Tn, ntok, nframes);
   hipLaunchKernelGGL(align_median_acc_kernel, dim3(Tn, nwin), dim3(256), 0, st, scores, nh, rows_total, Tk, Tn, ntok,
                      nframes, width, out);
@@ -848,7 +867,7 @@ void launch_align_matrix_acc(float* scores, int nh, int rows_total, int Tk, int 
 
 void launch_align_matrix_scale(float* out, int nwin, int Tn, int Tk, const int* ntok, const int* nframes, float scale,
                                hipStream_t st) {
-  hipLaunchKernelGGL(align_scale_kernel, dim3(nwin), dim3(256), 0, st, out, Tn, Tk, ntok, nframes, scale);
+  hipLaunchKernelGGL(align_scale_kernel, dim3(Tn, nwin), dim3(256), 0, st, out, Tn, Tk, ntok, nframes, scale);
   WMX_HIP(hipGetLastError());
 }
 
