@@ -143,6 +143,8 @@ void launch_cvt16_to_f32(DT dt, const uint16_t* in, float* out, long n, hipStrea
 // tok_emb is packed (packed_index), pos_emb row-major
 void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R, int Tn,
                   const int* pad, const int* slot0, int d, float* x, hipStream_t st);
+// row-major [N][K] copy of a packed matrix
+void launch_unpack_packed(const uint16_t* packed, uint16_t* rowmajor, int N, int K, hipStream_t st);
 // decode step (Tn == 1): x = embed, out16 = LN(x) * g + b, in one launch
 void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
                      const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,

@@ -270,6 +270,23 @@ void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const
   WMX_HIP(hipGetLastError());
 }
 
+// ---------------- row-major copy of a packed [N][K] matrix (packed_index) ----------------
+__global__ __launch_bounds__(256) void unpack_packed_kernel(const uint16_t* __restrict__ p, uint16_t* __restrict__ rm,
+                                                            int N, int K) {
+  const long n8 = (long)N * K / 8;  // 8 consecutive k of a row are 8 consecutive packed elements (16 B)
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const long e = i * 8;
+    const long n = e / K, k = e - n * K;
+    *reinterpret_cast<u16x8*>(rm + e) = *reinterpret_cast<const u16x8*>(p + packed_index(n, k, K));
+  }
+}
+
+void launch_unpack_packed(const uint16_t* packed, uint16_t* rowmajor, int N, int K, hipStream_t st) {
+  WMX_CHECK(K % 32 == 0, "unpack: K must be a multiple of 32");
+  hipLaunchKernelGGL(unpack_packed_kernel, dim3(2048), dim3(256), 0, st, packed, rowmajor, N, K);
+  WMX_HIP(hipGetLastError());
+}
+
 // ---------------- decode step: token + position embedding and the first layer's LN1 in one launch ----------------
 // one wave per row (4 rows per workgroup); the same arithmetic as embed_kernel followed by layernorm_kernel
 template <DT T>

@@ -123,6 +123,9 @@ struct EncLayer {
 struct DecLayer {
   float *ln1g, *ln1b, *bqkv, *bo, *ln2g, *ln2b, *bcq, *bco, *ln3g, *ln3b, *bfc1, *bfc2;
   uint16_t *wqkv, *wo, *wcq, *wco, *wfc1, *wfc2;
+  // row-major [N][K] copies of the packed projections (derived after every weight load) for the many-row
+  // passes (prompt prefill, word-alignment forward), which run on the tiled MFMA GEMM instead of the packed one
+  uint16_t *rqkv, *ro, *rcq, *rco, *rfc1, *rfc2;
 };
 
 struct Model {
@@ -226,6 +229,14 @@ static void build_model(Model& m) {
     P.add(&L.bfc1, 4 * dt);
     P.add(&L.wfc2, (size_t)4 * dt * dt);
     P.add(&L.bfc2, dt);
+  }
+  for (auto& L : m.dec) {
+    P.add(&L.rqkv, (size_t)3 * dt * dt);
+    P.add(&L.ro, (size_t)dt * dt);
+    P.add(&L.rcq, (size_t)dt * dt);
+    P.add(&L.rco, (size_t)dt * dt);
+    P.add(&L.rfc1, (size_t)4 * dt * dt);
+    P.add(&L.rfc2, (size_t)4 * dt * dt);
   }
   P.add(&m.wckv, (size_t)d.n_text_layer * 2 * dt * dt);
   P.add(&m.bckv, (size_t)d.n_text_layer * 2 * dt);
@@ -344,6 +355,20 @@ static void build_model(Model& m) {
   WMX_HIP(hipMemcpyAsync(m.mel_count, count.data(), M * 4, hipMemcpyHostToDevice, m.st));
   WMX_HIP(hipMemcpyAsync(m.mel_off, off.data(), M * 4, hipMemcpyHostToDevice, m.st));
   WMX_HIP(hipMemcpyAsync(m.mel_w, wts.data(), wts.size() * 4, hipMemcpyHostToDevice, m.st));
+  WMX_HIP(hipStreamSynchronize(m.st));
+}
+
+// row-major copies of the packed decoder projections (after every weight load; deterministic)
+static void prepare_rowmajor(Model& m) {
+  const int dt = m.d.n_text_state;
+  for (auto& L : m.dec) {
+    launch_unpack_packed(L.wqkv, L.rqkv, 3 * dt, dt, m.st);
+    launch_unpack_packed(L.wo, L.ro, dt, dt, m.st);
+    launch_unpack_packed(L.wcq, L.rcq, dt, dt, m.st);
+    launch_unpack_packed(L.wco, L.rco, dt, dt, m.st);
+    launch_unpack_packed(L.wfc1, L.rfc1, 4 * dt, dt, m.st);
+    launch_unpack_packed(L.wfc2, L.rfc2, dt, 4 * dt, m.st);
+  }
   WMX_HIP(hipStreamSynchronize(m.st));
 }
 
@@ -627,8 +652,15 @@ static Epi epi(int kind, const float* bias, void* out, long ldc) {
   return e;
 }
 
-// decoder projection on packed weights, epilogue in-kernel (any M: row chunks on the grid's z axis)
-static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, const Epi& e) {
+// decoder projection: packed weights (decode, few rows), or the row-major copy on the tiled MFMA GEMM when there
+// are many rows (prompt prefill, word alignment: the packed kernel would re-read the weights per 64-row chunk)
+static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, const Epi& e,
+                   const uint16_t* Wrm = nullptr) {
+  static const bool packed_only = getenv("WMX_PREFILL_PACKED") != nullptr;  // A/B switch for tuning runs
+  if (Wrm && M > 256 && !packed_only) {
+    gemm(c, A, lda, Wrm, K, M, N, K, e);
+    return;
+  }
   PackedCall g;
   g.A = A;
   g.lda = lda;
@@ -905,7 +937,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
     eq.slot0 = c.slot;
     eq.kc = kcl;
     eq.vc = vcl;
-    gemm_p(c, c.dhb, dt, L.wqkv, rowsT, 3 * dt, dt, eq);
+    gemm_p(c, c.dhb, dt, L.wqkv, rowsT, 3 * dt, dt, eq, L.rqkv);
     if (f.prefill) {
       AttnArgs a{};
       a.q = c.dq;
@@ -942,9 +974,9 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.slot0 = c.slot;
       launch_self_attn(c.dt, a, c.st);
     }
-    gemm_p(c, c.dao, dt, L.wo, rowsT, dt, dt, epi(EPI_RESID32, L.bo, c.dx, dt));
+    gemm_p(c, c.dao, dt, L.wo, rowsT, dt, dt, epi(EPI_RESID32, L.bo, c.dx, dt), L.ro);
     launch_layernorm(c.dt, c.dx, L.ln2g, L.ln2b, c.dhb, rowsT, dt, c.st);
-    gemm_p(c, c.dhb, dt, L.wcq, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt));
+    gemm_p(c, c.dhb, dt, L.wcq, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt), L.rcq);
     const uint16_t* ckl = cross_k(c, l);
     const uint16_t* cvl = cross_v(c, l);
     {
@@ -993,10 +1025,10 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         sync(c);
       }
     }
-    gemm_p(c, c.dao, dt, L.wco, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt));
+    gemm_p(c, c.dao, dt, L.wco, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt), L.rco);
     launch_layernorm(c.dt, c.dx, L.ln3g, L.ln3b, c.dhb, rowsT, dt, c.st);
-    gemm_p(c, c.dhb, dt, L.wfc1, rowsT, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
-    gemm_p(c, c.df1, 4 * dt, L.wfc2, rowsT, dt, 4 * dt, epi(EPI_RESID32, L.bfc2, c.dx, dt));
+    gemm_p(c, c.dhb, dt, L.wfc1, rowsT, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), L.rfc1);
+    gemm_p(c, c.df1, 4 * dt, L.wfc2, rowsT, dt, 4 * dt, epi(EPI_RESID32, L.bfc2, c.dx, dt), L.rfc2);
   }
 }
 
@@ -1608,6 +1640,7 @@ wmx_status wmx_model_init_synthetic(wmx_model* w, uint64_t seed) {
     }
     WMX_HIP(hipStreamSynchronize(m.st));
     prepare_mx8(m);
+    prepare_rowmajor(m);
     m.initialized = true;
   });
 }
@@ -1706,6 +1739,7 @@ wmx_status wmx_model_arena_loaded(wmx_model* w) {
   return guard([&] {
     WMX_HIP(hipSetDevice(w->m.device));
     prepare_mx8(w->m);
+    prepare_rowmajor(w->m);
     w->m.initialized = true;
   });
 }
