@@ -64,7 +64,8 @@ template <DT T> __device__ inline float to_f32(uint16_t h);
 template <> __device__ inline float to_f32<DT::BF16>(uint16_t h) { return bf16_to_f32(h); }
 template <> __device__ inline float to_f32<DT::F16>(uint16_t h) { return f16_to_f32(h); }
 template <DT T> __device__ inline uint16_t from_f32(float f);
-template <> __device__ inline uint16_t from_f32<DT::BF16>(float f) { return f32_to_bf16(f); }
+// the hardware round-to-nearest-even convert (v_cvt_pk_bf16_f32): bit-identical to f32_to_bf16 for non-NaN input
+template <> __device__ inline uint16_t from_f32<DT::BF16>(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 template <> __device__ inline uint16_t from_f32<DT::F16>(float f) { return f32_to_f16(f); }
 
 // MFMA 16x16x32 on 8 x 16-bit operands held as u16x8
