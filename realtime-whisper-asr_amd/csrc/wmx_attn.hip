@@ -637,7 +637,7 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {
 // load per lane from the transposed V image.  Softmax statistics are per lane (q = l&15) plus two xor
 // shuffles across the four 16-lane groups; P goes to the MFMA as bf16/f16 hi + lo halves (two MFMAs), so
 // the probabilities keep ~16 mantissa bits.  No LDS until the 4-wave combine at the end.
-// KS > 1: each chunk writes a (max, sum, o[64]) record per query; dec_cross_combine merges them in order.
+// KS > 1: each chunk writes a (max, sum, o[64]) record per query; the last arriving chunk merges them in order.
 // ------------------------------------------------------------------------------------------------
 constexpr int kMaxTk = kXS, kMaxSplits = 16;
 #ifndef WMX_XATTN_OCC
@@ -696,8 +696,10 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   };
   if (kw0 < kw1) load_batch(kw0);
 
-  // ---- the tile's queries into LDS (bf16/f16, rounded like the stored path), one element per thread:
-  //      q = bias + sum of the split-K partials in slice order, or the stored q ----
+  // ---- the tile's queries into LDS (bf16/f16), one element per thread: q = bias + sum of the split-K partials in
+  //      slice order, or the stored q; pre-scaled by log2(e) / sqrt(64) so the scores come out of the MFMA in
+  //      log2 units (softmax on exp2, no per-score scaling) ----
+  constexpr float kQScale = 0.125f * 1.4426950408889634f;
   __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
   for (int t = tid; t < 16 * 64; t += NT) {
     const int q = t >> 6, e = t & 63;
@@ -713,9 +715,9 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         float p = 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u) p += tv[u];
-        v = from_f32<T>(p + (a.qbias ? a.qbias[col] : 0.f));
+        v = from_f32<T>((p + (a.qbias ? a.qbias[col] : 0.f)) * kQScale);
       } else {
-        v = a.q[row * a.q_ld + col];
+        v = from_f32<T>(to_f32<T>(a.q[row * a.q_ld + col]) * kQScale);
       }
     }
     qsh[q][e] = v;
@@ -734,6 +736,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   for (int kb0 = kw0; kb0 < kw1; kb0 += 32 * KPW) {
     if (kb0 != kw0) load_batch(kb0);  // (prefill only: decode chunks are one batch, loaded above)
     float sv[KPW][8];
+    const bool whole = kb0 + 32 * KPW <= kw1;  // (wave-uniform) no key of the batch past the range: no masking
 #pragma unroll
     for (int b = 0; b < KPW; ++b) {
 #pragma unroll
@@ -744,7 +747,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb0 + 32 * b + 8 * g + 4 * u + r;
-          sv[b][4 * u + r] = key < kw1 ? acc[r] * 0.125f : -INFINITY;
+          sv[b][4 * u + r] = (whole || key < kw1) ? acc[r] : -INFINITY;
         }
       }
     }
@@ -755,26 +758,30 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
       for (int j = 0; j < 8; ++j) mx = fmaxf(mx, sv[b][j]);
     mx = max_xor32(max_xor16(mx));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = __expf(m_run - m_new);  // 0 on the first batch (m_run = -inf)
     float ls = 0.f;
 #pragma unroll
     for (int b = 0; b < KPW; ++b)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float e = __expf(sv[b][j] - m_new);
+        const float e = __builtin_amdgcn_exp2f(sv[b][j] - m_new);
         sv[b][j] = e;
         ls += e;
       }
     ls = sum_xor32(sum_xor16(ls));
-    l_run = l_run * alpha + ls;
-    m_run = m_new;
-    // o rows are queries 4g + r: their alpha lives in lane (4g + r) of any group
+    if (kb0 == kw0) {  // first batch: o and l are still zero (the only batch of a decode chunk)
+      l_run = ls;
+    } else {
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      l_run = l_run * alpha + ls;
+      // o rows are queries 4g + r: their alpha lives in lane (4g + r) of any group
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float ar = __shfl(alpha, 4 * g + r);
+      for (int r = 0; r < 4; ++r) {
+        const float ar = __shfl(alpha, 4 * g + r);
 #pragma unroll
-      for (int db = 0; db < 4; ++db) o[db][r] *= ar;
+        for (int db = 0; db < 4; ++db) o[db][r] *= ar;
+      }
     }
+    m_run = m_new;
 #pragma unroll
     for (int b = 0; b < KPW; ++b) {
       u16x8 phi, plo;
@@ -812,7 +819,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     float L = 0.f, O = 0.f;
 #pragma unroll
     for (int wv = 0; wv < NWV; ++wv) {
-      const float f = sm[wv][q] == -INFINITY ? 0.f : __expf(sm[wv][q] - M);
+      const float f = sm[wv][q] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sm[wv][q] - M);
       L += sl[wv][q] * f;
       O += so[wv][q][e] * f;
     }
@@ -872,7 +879,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
-        const float sc2 = rec[k][0] == -INFINITY ? 0.f : __expf(rec[k][0] - M);
+        const float sc2 = rec[k][0] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(rec[k][0] - M);
         l += rec[k][1] * sc2;
         o2 += rec[k][2] * sc2;
       }
