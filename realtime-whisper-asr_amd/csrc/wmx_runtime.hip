@@ -618,7 +618,11 @@ static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ld
     launch_gemm(c.dt, g, c.st);
     return;
   }
-  if (M >= 1024) {
+  static const int m128 = [] {  // rows from which the 128x128 tile is used; WMX_GEMM_M128 overrides (tuning runs)
+    const char* v = getenv("WMX_GEMM_M128");
+    return v ? atoi(v) : 1024;
+  }();
+  if (M >= m128) {
     g.tile = TILE_128x128;
     bm = 128;
     bn = 128;

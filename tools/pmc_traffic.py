@@ -47,7 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kernels", nargs="+")
     ap.add_argument("--batch", type=int, nargs="+", default=[4, 8], help="windows per launch")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01e_pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01f_pmc_traffic.json"))
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     res = {}
