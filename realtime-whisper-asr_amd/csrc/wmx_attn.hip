@@ -899,7 +899,8 @@ static int cross_chunk(int Tk, int nq) {
   if (nq > 16) return Tk;  // prefill: many query tiles already fill the chip
   if (env) return env;
   // large-v3, 2 groups x 4 windows, 8 waves per workgroup: 1024-key chunks (2 per window-head) 600-602 ms per call,
-  // 768: 603-605, 512 with 4 waves: 610-625 (interleaved bench.py sweep, r01); 512 beat 256 with 4 waves
+  // 768: 603-605, 512 with 4 waves: 610-625 (interleaved bench.py sweep, r01); 512 beat 256 with 4 waves;
+  // unsplit (1504): 611-612 vs 591 (r01f)
   return 1024;
 }
 
