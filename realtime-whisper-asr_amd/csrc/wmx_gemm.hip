@@ -1122,15 +1122,123 @@ static void launch_skinny(const GemmCall& g, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// RedTail: split-K reduction + residual + LayerNorm inside the producing packed GEMM launch (the decode step's
+// out-projections and fc2).  The in-launch merge of cdna_hip_programming.md Guideline 16 in its sc1 form, twice:
+//   1. every workgroup drains its write-through partial stores and takes a ticket on its column group's counter;
+//      the one drawing S-1 sums the S slices in slice order, x = (x + bias) + sum (same order as
+//      reduce_ln4_kernel), stores x write-through and re-arms the counter;
+//   2. those reducers take a ticket on one launch counter; the last normalises every row, one wave per row
+//      group (4 rows x 5 column quads per lane in flight, wave-only reductions), and re-arms it.
+// Requires N % 4 == 0 and N <= 1280 (packed_tail_ok).
+// ------------------------------------------------------------------------------------------------
+constexpr int kTailQpl = 5, kTailRows = 4;
+typedef unsigned int tail_u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte write-through (sc1, aux 16) store / sc1 load through a buffer resource on a wave-uniform base
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tail_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void tail_st4(__amdgpu_buffer_rsrc_t r, long idx, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tail_u32x4, v), r, (int)(idx * 4), 0, 16);
+}
+__device__ __forceinline__ float4 tail_ld4(__amdgpu_buffer_rsrc_t r, long idx) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
+}
+template <DT T, int MT, int NCT, int NW>
+__device__ __forceinline__ void packed_red_tail(const RedTail& rt, const float* part, int M, int N, int S, int m0,
+                                                int t0) {
+  constexpr int NT = 64 * NW, C4 = 4 * NCT;
+  __shared__ int flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int cg = blockIdx.z * gridDim.x + blockIdx.x;
+  if (tid == 0) flag = __hip_atomic_fetch_add(rt.cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+  __syncthreads();
+  if (!flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const auto pr = tail_rsrc(part), xr = tail_rsrc(rt.x);
+  for (int idx = tid; idx < MT * 16 * C4; idx += NT) {
+    const int row = idx / C4, c = (idx - row * C4) * 4;
+    const int m = m0 + row, n = t0 * 16 + c;
+    if (m >= M || n >= N) continue;
+    float4 t[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      t[s] = s < S ? tail_ld4(pr, ((long)s * M + m) * N + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 xv = *reinterpret_cast<const float4*>(rt.x + (long)m * N + n);
+    const float4 bv = rt.bias ? *reinterpret_cast<const float4*>(rt.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) p = make_float4(p.x + t[s].x, p.y + t[s].y, p.z + t[s].z, p.w + t[s].w);
+    tail_st4(xr, (long)m * N + n,
+             make_float4((xv.x + bv.x) + p.x, (xv.y + bv.y) + p.y, (xv.z + bv.z) + p.z, (xv.w + bv.w) + p.w));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int ntask = gridDim.x * gridDim.z;
+  if (tid == 0) {
+    __hip_atomic_store(rt.cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = __hip_atomic_fetch_add(rt.cnt + ntask, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntask - 1;
+  }
+  __syncthreads();
+  if (!flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const int n4 = N >> 2;
+  for (int r0 = wave * kTailRows; r0 < M; r0 += NW * kTailRows) {
+    float4 v[kTailRows][kTailQpl];
+#pragma unroll
+    for (int r = 0; r < kTailRows; ++r)
+#pragma unroll
+      for (int j = 0; j < kTailQpl; ++j) {
+        const int q = lane + 64 * j, m = r0 + r;
+        const bool ok = m < M && q < n4;
+        v[r][j] = ok ? tail_ld4(xr, (long)m * N + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+    for (int r = 0; r < kTailRows; ++r) {
+      const int m = r0 + r;
+      if (m >= M) break;  // wave-uniform
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < kTailQpl; ++j) sum += (v[r][j].x + v[r][j].y) + (v[r][j].z + v[r][j].w);
+      const float mean = wave_sum(sum) / N;
+      float sq = 0.f;
+#pragma unroll
+      for (int j = 0; j < kTailQpl; ++j) {
+        if (lane + 64 * j < n4) {
+          const float4 d = make_float4(v[r][j].x - mean, v[r][j].y - mean, v[r][j].z - mean, v[r][j].w - mean);
+          sq += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        }
+      }
+      const float rstd = 1.0f / sqrtf(wave_sum(sq) / N + 1e-5f);
+#pragma unroll
+      for (int j = 0; j < kTailQpl; ++j) {
+        const int q = lane + 64 * j;
+        if (q < n4) {
+          const float4 gg = *reinterpret_cast<const float4*>(rt.g + 4 * q);
+          const float4 bb = *reinterpret_cast<const float4*>(rt.b + 4 * q);
+          const u16x4 h = {from_f32<T>((v[r][j].x - mean) * rstd * gg.x + bb.x),
+                           from_f32<T>((v[r][j].y - mean) * rstd * gg.y + bb.y),
+                           from_f32<T>((v[r][j].z - mean) * rstd * gg.z + bb.z),
+                           from_f32<T>((v[r][j].w - mean) * rstd * gg.w + bb.w)};
+          *reinterpret_cast<u16x4*>(rt.out + (long)m * N + 4 * q) = h;
+        }
+      }
+    }
+  }
+  if (tid == 0) __hip_atomic_store(rt.cnt + ntask, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------------
 // decode GEMM on packed weights (skinny M): workgroup = NCT 16-column tiles x one K slice x one 16*MT row chunk;
 // its 4 waves split the slice's k-steps, every wave issues KU k-steps of loads (NCT contiguous 1 KiB weight
 // fragments + MT activation fragments) before their MFMAs, partial tiles are summed through LDS.
 // Grid (col groups, S, row chunks).  S == 1: epilogue; S > 1: raw fp32 partials part[s][M][N].
 // ------------------------------------------------------------------------------------------------
-template <DT T, int MT, int NCT, int NW>
+template <DT T, int MT, int NCT, int NW, bool TAIL>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
-                                                              int S, Epi e, float* __restrict__ part) {
+                                                              int S, Epi e, float* __restrict__ part, RedTail rt) {
   constexpr int KU = (MT + NCT) <= 8 ? 2 : 1;
   constexpr int LDR = 16 * NCT + 1;
   constexpr int NT = 64 * NW;
@@ -1198,7 +1306,9 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
       for (int w = 1; w < NW; ++w) v += red[w][row][c + q];
       v4[q] = v;
     }
-    if (S > 1) {
+    if (TAIL) {  // write-through (sc1) so the last arriver on another XCD reads them without an L2 release
+      tail_st4(tail_rsrc(part), ((long)sp * M + m) * N + n, make_float4(v4[0], v4[1], v4[2], v4[3]));
+    } else if (S > 1) {
       float* dst = part + ((long)sp * M + m) * N + n;
       if (n + 3 < N && (N & 3) == 0) {
         *reinterpret_cast<float4*>(dst) = make_float4(v4[0], v4[1], v4[2], v4[3]);
@@ -1211,6 +1321,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
       for (int q = 0; q < 4 && n + q < N; ++q) epi_store<T>(e, m, n + q, v4[q]);
     }
   }
+  if constexpr (TAIL) packed_red_tail<T, MT, NCT, NW>(rt, part, M, N, S, m0, t0);
 }
 
 static int packed_mt(int M) {
@@ -1250,9 +1361,16 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ksteps = g.K / 32, kps = (ksteps + g.S - 1) / g.S;
   const int per4 = (kps + 3) / 4;
   static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
-#define WMX_PACKED_LAUNCH(NWV)                                                                                \
-  hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W, g.M, \
-                     g.N, g.K, g.S, g.epi, g.part)
+  const bool tail = g.tail.cnt != nullptr;
+#define WMX_PACKED_LAUNCH(NWV)                                                                                     \
+  do {                                                                                                             \
+    if (tail)                                                                                                      \
+      hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, true>), grid, dim3(64 * NWV), 0, st, g.A, g.lda,     \
+                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail);                                          \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, false>), grid, dim3(64 * NWV), 0, st, g.A, g.lda,    \
+                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail);                                          \
+  } while (0)
   // the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] stays within 80 KiB of LDS (two workgroups per CU)
   constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
   constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
@@ -1280,9 +1398,26 @@ static void launch_packed_mt(const PackedCall& g, hipStream_t st) {
   }
 }
 
+// the tail's reducers and its single normalising workgroup: S <= 8 slices, rows of <= 5 quads per lane, one
+// counter per column group plus one, at most 8 waves per workgroup
+bool packed_tail_ok(int M, int N, int K, int S) {
+  if (S < 2 || S > 8 || N % 4 != 0 || N > 256 * kTailQpl || K % 32 != 0 || M < 1) return false;
+  if ((long)S * M * N * 4 >= 0x7fffffffL) return false;  // 32-bit buffer offsets
+  const int mt = (std::min(M, 128) + 15) / 16;
+  const int mtc = mt <= 4 ? mt : (mt <= 6 ? 6 : 4);
+  const int nct = mt > 4 ? 2 : packed_nct(M, N, K);
+  const long groups = (long)((N + 16 * nct - 1) / (16 * nct)) * ((M + mtc * 16 - 1) / (mtc * 16));
+  if (groups + 1 > packed_tail_counters()) return false;
+  const int kps = (K / 32 + S - 1) / S, per4 = (kps + 3) / 4;
+  return per4 <= 8;
+}
+
 void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
   WMX_CHECK(g.M >= 1 && g.K % 32 == 0 && g.S >= 1, "packed gemm: shape");
   WMX_CHECK(g.S == 1 || g.part != nullptr, "packed gemm: partial buffer required for S > 1");
+  WMX_CHECK(g.tail.cnt == nullptr ||
+                (packed_tail_ok(g.M, g.N, g.K, g.S) && g.tail.x && g.tail.g && g.tail.b && g.tail.out),
+            "packed gemm: reduction tail shape");
   const int nct = packed_nct(g.M, g.N, g.K);
   if (dt == DT::BF16) {
     if (nct == 4) launch_packed_mt<DT::BF16, 4>(g, st); else launch_packed_mt<DT::BF16, 2>(g, st);

@@ -106,6 +106,17 @@ __host__ __device__ inline long packed_index(long n, long k, long K) {
 
 // C[M][N] = A[M][K] . Wp^T.  S == 1: epilogue applied in-kernel.  S > 1: K is split over S workgroup slices and
 // each writes raw fp32 partials part[s][M][N] (no bias); the consumer sums them in slice order (deterministic).
+// in-launch split-K reduction + residual + LayerNorm of a partial-output packed GEMM (decode step): the last
+// of a column group's S slices sums them into x (x += bias + sum_s part[s]); the last column group normalises
+// every row into out (LN(x) * g + b).  cnt: >= packed_tail_counters() zeroed ints, re-armed by the kernel.
+struct RedTail {
+  const float* bias = nullptr;
+  float* x = nullptr;
+  const float* g = nullptr;
+  const float* b = nullptr;
+  uint16_t* out = nullptr;
+  int* cnt = nullptr;
+};
 struct PackedCall {
   const uint16_t* A;
   long lda;
@@ -114,8 +125,12 @@ struct PackedCall {
   int S = 1;
   Epi epi;
   float* part = nullptr;
+  RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
 };
 void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st);
+// whether a partial-output launch of this shape can carry the RedTail; counters the tail needs
+bool packed_tail_ok(int M, int N, int K, int S);
+constexpr int packed_tail_counters() { return 4096; }
 int packed_nct(int M, int N, int K);
 // split count for a partial-output launch (<= cap_elems / (M*N) partial slices)
 int packed_splits(int M, int N, int K, long cap_elems);

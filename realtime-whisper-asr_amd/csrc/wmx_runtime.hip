@@ -443,6 +443,7 @@ struct Ctx {
   float* sel_ws = nullptr;
   float* xa_ws = nullptr;
   int* xa_cnt = nullptr;
+  int* red_cnt = nullptr;  // RedTail arrival counters (packed GEMM with in-launch reduce + LayerNorm)
   uint32_t* mask = nullptr;
   // alignment
   float *scores = nullptr, *align_out = nullptr, *tprob = nullptr;
@@ -564,6 +565,7 @@ static void alloc_ctx(Ctx& c) {
   // key-chunk records: chunked launches have <= 16 queries per window (more use one chunk, no records)
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
+  P.add(&c.red_cnt, (size_t)packed_tail_counters());
   P.add(&c.probe_buf, (size_t)2 * T);
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
@@ -694,6 +696,38 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
   }
   launch_gemm_packed(c.dt, g, c.st);
   return g.S;
+}
+
+// decoder projection whose split-K partials feed x += bias + sum; out16 = LN(x) (reduce_ln): one packed launch
+// carrying the reduction and the LayerNorm when the shape allows (RedTail), else the GEMM and reduce_ln
+static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K,
+                         const float* bias, const float* g, const float* b) {
+  // opt-in (WMX_REDLN_FUSED): measured slower than the separate reduce_ln launch, 798 vs 587 ms per call on the
+  // default bench -- the in-launch chain (sc1 partial loads, write-through x, a second arrival, the single
+  // normalising workgroup's row loads) costs ~10 us more than the kernel boundary it removes
+  static const bool fused = getenv("WMX_REDLN_FUSED") != nullptr;
+  const int S = packed_splits(M, N, K, c.part_elems);
+  if (fused && packed_tail_ok(M, N, K, S)) {
+    PackedCall p;
+    p.A = A;
+    p.lda = lda;
+    p.W = Wp;
+    p.M = M;
+    p.N = N;
+    p.K = K;
+    p.S = S;
+    p.part = c.part;
+    p.tail.bias = bias;
+    p.tail.x = c.dx;
+    p.tail.g = g;
+    p.tail.b = b;
+    p.tail.out = c.dhb;
+    p.tail.cnt = c.red_cnt;
+    launch_gemm_packed(c.dt, p, c.st);
+    return;
+  }
+  const int S2 = gemm_p_part(c, A, lda, Wp, M, N, K);
+  launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -886,8 +920,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     a.qpart_ld = 3 * dt;
     a.qbias = L.bqkv;
     launch_self_attn(c.dt, a, c.st);
-    S = gemm_p_part(c, c.dao, dt, L.wo, R, dt, dt);
-    launch_reduce_ln(c.dt, c.part, S, L.bo, c.dx, L.ln2g, L.ln2b, c.dhb, R, dt, c.st);
+    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b);
     // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3
     S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
     DecAttnArgs x{};
@@ -911,13 +944,11 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.slot0 = c.slot;
     if (l == c.probe_layer && c.probe_kernel == 0) x.tprobe = c.probe_buf;
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
-    S = gemm_p_part(c, c.dao, dt, L.wco, R, dt, dt);
-    launch_reduce_ln(c.dt, c.part, S, L.bco, c.dx, L.ln3g, L.ln3b, c.dhb, R, dt, c.st);
+    gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b);
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
     gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
-    S = gemm_p_part(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt);
-    launch_reduce_ln(c.dt, c.part, S, L.bfc2, c.dx, last ? m.lng : m.dec[l + 1].ln1g, last ? m.lnb : m.dec[l + 1].ln1b,
-                     c.dhb, R, dt, c.st);
+    gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
+                 last ? m.lnb : m.dec[l + 1].ln1b);
   }
 }
 
