@@ -243,13 +243,13 @@ def main():
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
     # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py) at this launch's batch
-    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01f_pmc_traffic.json")
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01g_pmc_traffic.json")
     if os.path.exists(pmc):
         rec = json.load(open(pmc)).get(f"{dom}@{Bg}")
         if rec and roof["unit"] == "GB/s":
             roof["traffic"] = round(rec["traffic_bytes"] / 1e9 / (ms * 1e-3), 1)
             roof["traffic_bytes_per_launch"] = rec["traffic_bytes"]
-            roof["traffic_source"] = "profiles/r01f_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
+            roof["traffic_source"] = "profiles/r01g_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
     roof["measured"] = measured
     roof["kernel"] = dom
     roof["launch_ms"] = round(ms, 4)
