@@ -34,6 +34,25 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+_JSON_OUT = None
+
+
+def emit(obj):
+    """The one JSON line, on the real stdout (native libraries' stdout chatter is redirected to stderr)."""
+    out = _JSON_OUT or sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
+def quiet_stdout():
+    """Point fd 1 at stderr so RCCL / gloo / HIP messages printed by native code cannot interleave with the JSON
+    line; keep a private handle on the original stdout for emit()."""
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -50,6 +69,8 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU rehearsal of the launch / rendezvous / broadcast / max-over-ranks plumbing (gloo, no GPU)")
     p.add_argument("--roofline-kernel", default="auto",
                    choices=["auto", "cross_attn", "enc_fc1", "enc_attn", "logmel", "dec_fc1", "self_attn"])
     return p.parse_args()
@@ -108,11 +129,66 @@ def cpu_baseline(model, args, steps_done):
                       f"{steps_done} steps; word alignment not included"}
 
 
+def dry_run(args):
+    """The multi-rank plumbing of main() without a GPU: gloo rendezvous, the arena broadcast, barrier-bracketed
+    timed steps, max over ranks, one JSON line from rank 0 (tests/test_bench_launch.py drives it at world 2)."""
+    from wmx import dist as D
+    import torch
+    world, rank, _ = D.env_rank()
+    if world > 1:
+        D.init("gloo")
+    arena = (torch.arange(1 << 16, dtype=torch.int32) % 251).to(torch.uint8)
+    if rank != 0:
+        arena.zero_()
+    if world > 1:
+        D.broadcast_arena(arena, src=0)
+    ok = bool(torch.equal(arena, (torch.arange(1 << 16, dtype=torch.int32) % 251).to(torch.uint8)))
+    x = np.random.default_rng(rank).standard_normal(480000).astype(np.float32)
+
+    def step():  # a fixed synthetic host workload standing in for one transcribe call
+        return float(np.abs(np.fft.rfft(x.reshape(-1, 400), axis=-1)).sum())
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        D.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = D.max_over_ranks(elapsed)
+        ranks = int(D.sum_over_ranks(1.0))
+        arena_ok = int(D.sum_over_ranks(float(ok))) == world
+    else:
+        ranks, arena_ok = 1, ok
+    if rank == 0:
+        value = 30.0 * args.batch * world * args.steps / elapsed
+        emit({"metric": METRIC, "value": round(value, 3), "unit": "x_realtime (audio s / wall s, all GPUs)",
+              "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+              "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
+              "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+              "data": "dry run: launch / rendezvous / broadcast plumbing only, host FFT stand-in step",
+              "config": {"workload": "dry-run", "parallelism": f"dp{world} (independent streams)"},
+              "ranks_reporting": ranks, "arena_broadcast_ok": arena_ok})
+    D.destroy()
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from wmx import dist as D
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` outside torch.distributed.run: start N rank processes here, before any torch / HIP
+        # call in this process, and relay rank 0's JSON line
+        sys.exit(D.launch_ranks(args.gpus, sys.argv[1:], os.path.abspath(__file__)))
+    quiet_stdout()
+    if args.dry_run:
+        return dry_run(args)
+    world, rank, local = D.env_rank()
+    if world != args.gpus:
+        log(f"[rank {rank}] note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)")
     dist = None
     # torch (plumbing only: RCCL + the resident input buffer) must bring up its HIP runtime before libwmx is
     # loaded, so the process holds ONE libamdhip64.so.7 and device pointers are shared.
@@ -120,8 +196,7 @@ def main():
     torch.cuda.set_device(local)
     torch.zeros(1, device=f"cuda:{local}")
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = D.init("nccl", torch.device("cuda", local))  # RCCL
     from wmx import engine, synth
 
     dt = {"bf16": "bfloat16", "f16": "float16", "fp8": "float8"}[args.dtype]
@@ -133,7 +208,7 @@ def main():
         ptr, nbytes = model.arena()
         view = torch.as_tensor(_ArenaView(ptr, nbytes), device=f"cuda:{local}")
         torch.cuda.synchronize()
-        dist.broadcast(view, src=0)  # RCCL over xGMI: the only collective of the job
+        D.broadcast_arena(view, src=0)  # RCCL over xGMI: the only collective of the job
         torch.cuda.synchronize()
         model.mark_loaded()
     else:
@@ -178,7 +253,7 @@ def main():
     for _ in range(args.warmup):
         step()
     if dist is not None:
-        dist.barrier()
+        D.barrier()
     torch.cuda.synchronize()
     lat = []
     t0 = time.perf_counter()
@@ -189,12 +264,10 @@ def main():
         lat.append(time.perf_counter() - ts)
     torch.cuda.synchronize()
     if dist is not None:
-        dist.barrier()
+        D.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        e = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed = D.max_over_ranks(elapsed, device=f"cuda:{local}")
     stages = ctx.stage_ms()
     steps_done = ctx.last_steps()
     n_tok = [len(r.tokens) for r in res]
@@ -313,9 +386,8 @@ def main():
             log(f"[cpu] baseline failed: {e!r}")
             out["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        emit(out)
+    D.destroy()
 
 
 if __name__ == "__main__":

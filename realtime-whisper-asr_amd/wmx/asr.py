@@ -7,7 +7,7 @@ OnlineASRProcessor.process_iter) — but the engine below is libwmx.so on MI355X
 faster-whisper/CTranslate2.
 
     from wmx.asr import MI355XWhisperASR
-    asr = MI355XWhisperASR(lan="auto", modelsize="large-v3", device="cuda", compute_type="bfloat16")
+    asr = MI355XWhisperASR(lan="auto", modelsize="large-v3", device="cuda", compute_type="float16")
     online = EnhancedOnlineASRProcessor(asr, ...)        # unchanged caller
 """
 from __future__ import annotations
@@ -20,7 +20,7 @@ from .transcribe import WhisperModel
 class MI355XWhisperASR:
     sep = ""  # whisper_online.FasterWhisperASR.sep (faster-whisper words carry their own leading space)
 
-    def __init__(self, lan, modelsize=None, cache_dir=None, model_dir=None, device="cuda", compute_type="bfloat16",
+    def __init__(self, lan, modelsize=None, cache_dir=None, model_dir=None, device="cuda", compute_type="float16",
                  device_index=0, num_workers=1, cpu_threads=None, logfile=sys.stderr, adaptive_params=None,
                  transcribe_kwargs=None, seed=1, max_new_tokens=None):
         # asr_components.py:195-230
@@ -46,9 +46,12 @@ class MI355XWhisperASR:
         else:
             raise ValueError("modelsize or model_dir parameter must be set")
         if self.device == "cpu":
-            raise ValueError("MI355XWhisperASR runs on the GPU only; use device='cuda'")
-        return WhisperModel(name, device="cuda", device_index=self.device_index, compute_type=self.compute_type,
-                            download_root=cache_dir, num_workers=self.num_workers, seed=self._seed,
+            # the app's CPU/int8 fallback (asr_components.py:256-258) has no MI355X engine: fail loudly
+            raise ValueError("MI355XWhisperASR runs on the GPU only (device='cuda'); there is no CPU/int8 path")
+        # the faster-whisper WhisperModel kwargs of asr_components.py:244-254, then the engine's own keys
+        model_kwargs = {"device": self.device, "compute_type": self.compute_type, "download_root": cache_dir,
+                        "num_workers": self.num_workers, "device_index": self.device_index}
+        return WhisperModel(name, **model_kwargs, seed=self._seed,
                             beam_size=self.transcribe_kargs.get("beam_size", 5), max_new_tokens=self._max_new_tokens)
 
     def transcribe(self, audio, init_prompt=""):

@@ -421,11 +421,12 @@ class DynamicVACOnlineASRProcessor(VACOnlineASRProcessor):
     """Reference asr_components.py:81-179 (DynamicVADIterator gate)."""
 
     def __init__(self, online_chunk_size, asr, tokenizer=None, logfile=sys.stderr, buffer_trimming=("segment", 15),
-                 initial_silence_ms=500, min_silence_ms=200, max_silence_ms=1000, vad_threshold=0.5, vad_model=None):
+                 initial_silence_ms=500, min_silence_ms=200, max_silence_ms=1000, vad_threshold=0.5, vad_model=None,
+                 online=None):
         vad = DynamicVADIterator(vad_model or EnergyVAD(), initial_silence_ms, min_silence_ms, max_silence_ms,
                                  vad_threshold)
         super().__init__(online_chunk_size, asr, tokenizer=tokenizer, buffer_trimming=buffer_trimming,
-                         logfile=logfile, vad=vad)
+                         logfile=logfile, vad=vad, online=online)
 
     def set_silence_duration(self, silence_ms):
         return self.vac.set_silence_duration(silence_ms)
@@ -649,7 +650,25 @@ class StreamBatcher:
                 outs[i] = (None, None, "")
         if due:
             reqs = [streams[i].online.prepare_iter() for i in due]
-            results = self.model.transcribe_batch([a for a, _ in reqs], [p for _, p in reqs])
+            # the ASR's own decoding options, as CustomFasterWhisperASR.transcribe would pass them
+            # (asr_components.py:279-288): language (None = detect), task (set_translate_task), beam size
+            kw = dict(getattr(self.asr, "transcribe_kargs", None) or {})
+            if float(kw.get("temperature", 0.0) or 0.0) > 0 or kw.get("vad_filter"):
+                raise NotImplementedError("StreamBatcher: temperature > 0 / vad_filter are not implemented")
+            results = self.model.transcribe_batch([a for a, _ in reqs], [p for _, p in reqs],
+                                                  language=getattr(self.asr, "original_language", None),
+                                                  task=kw.get("task", "transcribe"), beam_size=kw.get("beam_size"))
             for i, res in zip(due, results):
-                outs[i] = streams[i].online.complete_iter(res)
+                on = streams[i].online
+                try:
+                    if isinstance(res, Exception):
+                        raise res
+                    outs[i] = on.complete_iter(res)
+                except Exception as e:  # per stream, EnhancedOnlineASRProcessor.process_iter (:369-381)
+                    print(f"process_iter error: {e}", file=getattr(on, "logfile", sys.stderr))
+                    try:
+                        on.init(offset=on.buffer_time_offset)
+                    except Exception:
+                        pass
+                    outs[i] = (None, None, "")
         return outs

@@ -34,6 +34,18 @@ DEFAULT_SUPPRESS = [
 ]
 
 
+def suppressed_tokens(sp, suppress_tokens=(-1,)):
+    """faster-whisper 1.2.1 get_suppressed_tokens (openai decoding._get_suppress_tokens): -1 expands to the
+    non-speech symbols; the task / sot / prev / lm control tokens are always suppressed, and so is no_speech
+    (openai), so a sampled or beam-searched sequence can never emit a control token into the text or the prompt
+    history."""
+    toks = list(suppress_tokens or [])
+    if -1 in toks:
+        toks = [t for t in toks if t >= 0] + list(DEFAULT_SUPPRESS)
+    toks += [sp.transcribe, sp.translate, sp.sot, sp.sot_prev, sp.sot_lm, sp.no_speech]
+    return sorted(set(int(t) for t in toks))
+
+
 class SpecialTokens:
     def __init__(self, n_vocab: int):
         self.n_langs = 100 if n_vocab >= 51866 else 99

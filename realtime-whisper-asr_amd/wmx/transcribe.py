@@ -16,7 +16,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .engine import ALIGNMENT_HEADS, Context, Model
-from .tokenizer import DEFAULT_SUPPRESS, LANGUAGES, load_tokenizer
+from .tokenizer import LANGUAGES, load_tokenizer, suppressed_tokens
 
 SAMPLE_RATE = 16000
 HOP = 160
@@ -137,7 +137,8 @@ def words_from_jumps(tokenizer, text_tokens, jump_times, token_probs, language):
             for w, t, s, e, p in zip(words, word_tokens, starts, ends, wp)]
 
 
-def add_word_timestamps(subsegments, alignment, seek, last_speech_timestamp):
+def add_word_timestamps(subsegments, alignment, seek, last_speech_timestamp, prepended=PREPEND_PUNCT,
+                        appended=APPEND_PUNCT):
     """faster-whisper add_word_timestamps for one window (median-duration clamps, punctuation merge,
     segment-boundary fixes)."""
     durs = np.array([w["end"] - w["start"] for w in alignment])
@@ -152,7 +153,7 @@ def add_word_timestamps(subsegments, alignment, seek, last_speech_timestamp):
                     alignment[i]["end"] = alignment[i]["start"] + max_dur
                 elif alignment[i - 1]["word"] in marks:
                     alignment[i]["start"] = alignment[i]["end"] - max_dur
-    merge_punctuations(alignment, PREPEND_PUNCT, APPEND_PUNCT)
+    merge_punctuations(alignment, prepended, appended)
     time_offset = seek * HOP / SAMPLE_RATE
     wi = 0
     for sub in subsegments:
@@ -186,12 +187,56 @@ def add_word_timestamps(subsegments, alignment, seek, last_speech_timestamp):
     return last_speech_timestamp
 
 
+# faster-whisper 1.2.1 WhisperModel.transcribe keywords this engine does not implement, with the value that means
+# "off"; any other value raises NotImplementedError instead of being silently ignored
+_FW_UNSUPPORTED = {
+    "vad_filter": False,  # Silero VAD pre-filter: the network is remote-only (torch.hub), SURVEY §8f-1
+    "vad_parameters": None,
+    "prefix": None,
+    "hotwords": None,
+    "clip_timestamps": "0",
+    "hallucination_silence_threshold": None,
+    "multilingual": False,
+    "repetition_penalty": 1,
+    "no_repeat_ngram_size": 0,
+    "chunk_length": None,
+    "language_detection_segments": 1,
+}
+# accepted and without effect on this path (faster-whisper semantics preserved)
+_FW_NO_EFFECT = ("log_progress", "language_detection_threshold", "prompt_reset_on_temperature")
+
+
+def _check_kwargs(kw):
+    for k, v in kw.items():
+        if k in _FW_UNSUPPORTED:
+            off = _FW_UNSUPPORTED[k]
+            if v != off and not (k == "chunk_length" and v == 30) and not (k == "clip_timestamps" and v in ([], None)):
+                raise NotImplementedError(f"faster-whisper option {k}={v!r} is not implemented by the MI355X engine")
+        elif k not in _FW_NO_EFFECT:
+            raise TypeError(f"transcribe() got an unexpected keyword argument {k!r}")
+
+
+def _temperatures(temperature):
+    ts = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
+    if any(float(t) > 0 for t in ts):
+        # faster-whisper samples best_of candidates at T > 0 (and falls back through the list); only the
+        # deterministic T = 0 search (greedy / beam) runs on this engine
+        raise NotImplementedError(f"temperature={temperature!r}: sampling (T > 0) is not implemented; use 0.0")
+    return ts
+
+
+def get_end(segments):
+    """faster-whisper get_end: the last word's end, else the last segment's end."""
+    return next((w["end"] for s in reversed(segments) for w in reversed(s.get("words") or [])),
+                segments[-1]["end"] if segments else None)
+
+
 class WhisperModel:
     """MI355X stand-in for faster_whisper.WhisperModel (same constructor keywords the reference passes at
-    asr_components.py:251-264; `download_root`/`num_workers` are accepted and ignored — weights are either a
+    asr_components.py:244-262; `download_root`/`num_workers` are accepted and ignored — weights are either a
     local HF/openai-named checkpoint (safetensors) or the build-owned synthetic initialisation)."""
 
-    def __init__(self, model_size_or_path="large-v3", device="cuda", device_index=0, compute_type="bfloat16",
+    def __init__(self, model_size_or_path="large-v3", device="cuda", device_index=0, compute_type="float16",
                  cpu_threads=0, num_workers=1, download_root=None, local_files_only=True, seed=1, max_batch=1,
                  beam_size=5, max_new_tokens=None, suppress_tokens=None, use_graph=True):
         if device not in ("cuda", "auto", "gpu", "rocm"):
@@ -215,33 +260,51 @@ class WhisperModel:
         self.max_batch = max_batch
         self.default_beam = beam_size
         self.max_new_tokens = max_new_tokens
-        self.suppress = DEFAULT_SUPPRESS if suppress_tokens is None else list(suppress_tokens)
+        self.suppress_tokens = [-1] if suppress_tokens is None else list(suppress_tokens)
         self.use_graph = use_graph
         self._ctx = {}
 
-    def context(self, beam_size, language_token, task, word_timestamps, without_timestamps=False):
-        key = (beam_size, language_token, task, word_timestamps, without_timestamps)
+    def context(self, beam_size, language_token, task, word_timestamps, without_timestamps=False, patience=1.0,
+                length_penalty=1.0, suppress_blank=True, suppress_tokens=None, max_initial_timestamp=1.0,
+                max_new_tokens=None):
+        sup = tuple(suppressed_tokens(self.tokenizer.sp, self.suppress_tokens if suppress_tokens is None
+                                      else suppress_tokens))
+        mit = None if max_initial_timestamp is None else int(round(max_initial_timestamp / TIME_PRECISION))
+        mnt = max_new_tokens or self.max_new_tokens or 448
+        key = (beam_size, language_token, task, word_timestamps, without_timestamps, float(patience),
+               float(length_penalty), bool(suppress_blank), sup, mit, mnt)
         if key not in self._ctx:
-            self._ctx[key] = Context(self.model, max_batch=self.max_batch, beam_size=beam_size,
-                                     max_new_tokens=self.max_new_tokens or 448, task=task, language=language_token,
-                                     without_timestamps=without_timestamps, suppress_tokens=self.suppress,
-                                     word_timestamps=word_timestamps, alignment_heads=ALIGNMENT_HEADS.get(self.name),
-                                     use_graph=self.use_graph, max_audio_samples=2 * 480000)
+            self._ctx[key] = Context(self.model, max_batch=self.max_batch, beam_size=beam_size, patience=patience,
+                                     length_penalty=length_penalty, max_new_tokens=mnt, task=task,
+                                     language=language_token, without_timestamps=without_timestamps,
+                                     max_initial_timestamp_index=mit, suppress_blank=suppress_blank,
+                                     suppress_tokens=sup, word_timestamps=word_timestamps,
+                                     alignment_heads=ALIGNMENT_HEADS.get(self.name), use_graph=self.use_graph,
+                                     max_audio_samples=2 * 480000)
         return self._ctx[key]
 
     # ---- faster-whisper WhisperModel.transcribe ----
     def transcribe(self, audio, language=None, task="transcribe", beam_size=5, best_of=5, patience=1.0,
                    length_penalty=1.0, temperature=0.0, initial_prompt=None, word_timestamps=False,
                    condition_on_previous_text=True, no_speech_threshold=0.6, log_prob_threshold=-1.0,
-                   compression_ratio_threshold=2.4, without_timestamps=False, vad_filter=False, **_unused):
+                   compression_ratio_threshold=2.4, without_timestamps=False, suppress_blank=True,
+                   suppress_tokens=(-1,), max_initial_timestamp=1.0, max_new_tokens=None,
+                   prepend_punctuations=PREPEND_PUNCT, append_punctuations=APPEND_PUNCT, **kwargs):
+        """faster-whisper 1.2.1 transcribe + generate_segments over 30 s windows (seek loop).  Language detection
+        runs once, on the first window, and every later window decodes with that language; with word timestamps
+        a window that does not end on a single timestamp moves seek to its last word's end (round(end * 100))."""
+        _check_kwargs(kwargs)
+        _temperatures(temperature)  # T > 0 raises: only deterministic search runs here
         audio = np.asarray(audio, dtype=np.float32)
         tok = self.tokenizer
         sp = tok.sp
         lang_tok = None if language is None else sp.language_token(language)
-        ctx = self.context(beam_size, lang_tok, task, word_timestamps, without_timestamps)
+        ctx_kw = dict(without_timestamps=without_timestamps, patience=patience, length_penalty=length_penalty,
+                      suppress_blank=suppress_blank, suppress_tokens=list(suppress_tokens or []),
+                      max_initial_timestamp=max_initial_timestamp, max_new_tokens=max_new_tokens)
         all_tokens = []
         prompt_reset_since = 0
-        if initial_prompt:
+        if initial_prompt is not None:
             if isinstance(initial_prompt, str):
                 all_tokens.extend(tok.encode(" " + initial_prompt.strip()))
             else:
@@ -250,37 +313,50 @@ class WhisperModel:
         seek = 0
         segments, last_speech = [], 0.0
         detected, det_prob = language, 1.0
+        punct = (prepend_punctuations, append_punctuations)
         while seek < content_frames:
             segment_size = min(N_FRAMES, content_frames - seek)
             prompt = all_tokens[prompt_reset_since:] if condition_on_previous_text else []
+            ctx = self.context(beam_size, lang_tok, task, word_timestamps, **ctx_kw)
             # the window's features come from the whole buffer (global max normalisation) -> pass the full audio
             r = ctx.transcribe([audio], prompts=[prompt], seek=[seek])[0]
             if detected is None:
                 detected, det_prob = sp.language_code(r.language), r.language_prob
+            if lang_tok is None:
+                lang_tok = sp.lang0 + LANGUAGES.index(detected)  # detected once, fixed for later windows
             segs, toks, seek_new, last_speech = self._window_segments(
                 r, seek, segment_size, word_timestamps, detected, last_speech, len(segments),
-                no_speech_threshold, log_prob_threshold)
+                no_speech_threshold, log_prob_threshold, punct)
             segments.extend(segs)
             all_tokens.extend(toks)
+            if not condition_on_previous_text:
+                prompt_reset_since = len(all_tokens)
             seek = seek_new if seek_new > seek else seek + max(1, segment_size)
         info = TranscriptionInfo(detected or "en", det_prob, len(audio) / SAMPLE_RATE, len(audio) / SAMPLE_RATE)
         return iter(segments), info
 
     def _window_segments(self, r, seek, segment_size, word_timestamps, language, last_speech, first_id,
-                         no_speech_threshold=0.6, log_prob_threshold=-1.0):
+                         no_speech_threshold=0.6, log_prob_threshold=-1.0, punct=(PREPEND_PUNCT, APPEND_PUNCT)):
         """faster-whisper generate_segments body for one decoded window -> (segments, tokens, seek, last_speech)."""
         tok, sp = self.tokenizer, self.tokenizer.sp
         time_offset = seek * HOP / SAMPLE_RATE
         segment_duration = segment_size * HOP / SAMPLE_RATE
-        if no_speech_threshold is not None and r.no_speech_prob > no_speech_threshold and (
-                log_prob_threshold is None or r.avg_logprob < log_prob_threshold):
-            return [], [], seek + segment_size, last_speech
-        subs, seek_new, _ = split_segments_by_timestamps(sp.timestamp_begin, list(r.tokens), time_offset,
-                                                         segment_size, segment_duration, seek)
+        if no_speech_threshold is not None:
+            skip = r.no_speech_prob > no_speech_threshold
+            if log_prob_threshold is not None and r.avg_logprob > log_prob_threshold:
+                skip = False  # high enough log prob despite the no-speech probability
+            if skip:
+                return [], [], seek + segment_size, last_speech
+        subs, seek_new, single_ending = split_segments_by_timestamps(
+            sp.timestamp_begin, list(r.tokens), time_offset, segment_size, segment_duration, seek)
         if word_timestamps:
             text_tokens = [t for t in r.tokens if t < sp.eot]
             alignment = words_from_jumps(tok, text_tokens, r.jump_times, r.text_token_probs, language or "en")
-            last_speech = add_word_timestamps(subs, alignment, seek, last_speech)
+            last_speech = add_word_timestamps(subs, alignment, seek, last_speech, *punct)
+            if not single_ending:
+                last_word_end = get_end(subs)
+                if last_word_end is not None and last_word_end > time_offset:
+                    seek_new = round(last_word_end * (SAMPLE_RATE // HOP))
         out, toks = [], []
         for s in subs:
             text = tok.decode(s["tokens"])
@@ -295,27 +371,51 @@ class WhisperModel:
 
     def transcribe_batch(self, audios, prompts=None, language=None, task="transcribe", beam_size=None,
                          word_timestamps=True, no_speech_threshold=0.6, log_prob_threshold=-1.0):
-        """Many independent streams' buffers (each <= 30 s, one window) in ONE libwmx launch sequence.
-        prompts: per-stream previous text (str) or token lists.  Returns a list of segment lists."""
+        """Many independent streams' buffers in ONE libwmx launch sequence (one window each).  prompts: per-stream
+        previous text (str) or token lists.  Buffers longer than one 30 s window (a streaming buffer nothing has
+        committed from yet) go through the full seek loop of transcribe() instead.  Returns per stream a list of
+        segments, or the exception that stream's call raised (the caller decides, per stream, what to do)."""
         tok, sp = self.tokenizer, self.tokenizer.sp
         beam = beam_size or self.default_beam
         lang_tok = None if language is None else sp.language_token(language)
+        prompts = list(prompts) if prompts is not None else [None] * len(audios)
+        out = [None] * len(audios)
+        short = []
+        for i, a in enumerate(audios):
+            if len(a) > N_FRAMES * HOP:
+                p = prompts[i]
+                try:
+                    segs, _ = self.transcribe(a, language=language, task=task, beam_size=beam,
+                                              initial_prompt=p if p else None, word_timestamps=word_timestamps,
+                                              no_speech_threshold=no_speech_threshold,
+                                              log_prob_threshold=log_prob_threshold)
+                    out[i] = list(segs)
+                except Exception as e:  # per stream, like EnhancedOnlineASRProcessor.process_iter
+                    out[i] = e
+            else:
+                short.append(i)
         ctx = self.context(beam, lang_tok, task, word_timestamps)
-        out = []
-        for b0 in range(0, len(audios), self.max_batch):
-            chunk = [np.asarray(a, np.float32) for a in audios[b0: b0 + self.max_batch]]
+        for b0 in range(0, len(short), self.max_batch):
+            idx = short[b0: b0 + self.max_batch]
+            chunk = [np.asarray(audios[i], np.float32) for i in idx]
             pr = []
-            for p in (prompts or [None] * len(audios))[b0: b0 + self.max_batch]:
+            for i in idx:
+                p = prompts[i]
                 if isinstance(p, str):
-                    pr.append(tok.encode(" " + p.strip()) if p.strip() else [])
+                    pr.append(tok.encode(" " + p.strip()))
                 else:
                     pr.append(list(p or []))
-            res = ctx.transcribe(chunk, prompts=pr)
-            for a, r in zip(chunk, res):
+            try:
+                res = ctx.transcribe(chunk, prompts=pr)
+            except Exception as e:
+                for i in idx:
+                    out[i] = e
+                continue
+            for i, a, r in zip(idx, chunk, res):
                 lang = language or sp.language_code(r.language)
                 segs, _, _, _ = self._window_segments(r, 0, min(N_FRAMES, len(a) // HOP), word_timestamps, lang,
                                                       0.0, 0, no_speech_threshold, log_prob_threshold)
-                out.append(segs)
+                out[i] = segs
         return out
 
 
@@ -334,13 +434,16 @@ def _infer_name(model_dir):
 
 
 def _load_checkpoint(model, model_dir):
+    """HF Whisper safetensors (any of f32 / f16 / bf16 storage) -> wmx_model_set_tensor (rounds to the model
+    dtype, packs the decoder projections).  bf16 has no numpy dtype, so tensors are read through torch."""
     import glob
     import os
     files = sorted(glob.glob(os.path.join(model_dir, "*.safetensors")))
     if not files:
         raise FileNotFoundError(f"no *.safetensors in {model_dir} (CT2 model.bin conversion is not supported yet)")
-    from safetensors.numpy import load_file
+    from safetensors.torch import load_file
     sd = {}
     for f in files:
-        sd.update(load_file(f))
-    model.load_state_dict({k: v.astype(np.float32) for k, v in sd.items()})
+        for k, v in load_file(f).items():
+            sd[k] = v.float().numpy()
+    model.load_state_dict(sd)

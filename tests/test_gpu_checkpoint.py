@@ -1,0 +1,47 @@
+"""Checkpoint ingestion: HF-named safetensors -> wmx_model_set_tensor, bit-exact.
+
+The build-owned PRNG weights are written as a HF Whisper state dict ("model." prefix, tied proj_out) in f32 and in
+bf16 storage, loaded through wmx.transcribe._load_checkpoint into a fresh model, and every tensor must read back
+bit-identical to init_synthetic's (the set path rounds to the model dtype and packs the decoder projections;
+get_tensor unpacks).  The loaded model must then transcribe token-identically to the synthetic one."""
+import numpy as np
+import pytest
+
+from oracle import whisper_np as O
+from wmx import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("storage", ["f32", "bf16"])
+def test_safetensors_roundtrip_bit_exact(tmp_path, storage):
+    import torch
+    from safetensors.torch import save_file
+
+    from wmx import engine as E
+    from wmx.transcribe import _load_checkpoint
+    d = O.DIMS["micro"]
+    ref = E.Model("micro", 0, "bfloat16").init_synthetic(3)
+    sd = {}
+    for name, shape, _, _ in O.tensor_specs(d):
+        sd["model." + name] = torch.from_numpy(ref.get_tensor(name, shape).copy())
+    sd["model.encoder.embed_positions.weight"] = torch.from_numpy(
+        ref.get_tensor("encoder.embed_positions.weight", (1500, d.n_audio_state)).copy())
+    sd["proj_out.weight"] = sd["model.decoder.embed_tokens.weight"]
+    if storage == "bf16":
+        sd = {k: v.to(torch.bfloat16) for k, v in sd.items()}
+    sd = {k: v.contiguous().clone() for k, v in sd.items()}
+    save_file(sd, str(tmp_path / "model.safetensors"))
+    m = E.Model("micro", 0, "bfloat16")
+    _load_checkpoint(m, str(tmp_path))
+    n = 0
+    for name, shape, _, _ in O.tensor_specs(d):
+        np.testing.assert_array_equal(m.get_tensor(name, shape), ref.get_tensor(name, shape), err_msg=name)
+        n += 1
+    assert n == len(O.tensor_specs(d))
+    a = [synth.speech_like(91, 80000), synth.speech_like(92, 200000)]
+    c1 = E.Context(ref, max_batch=2, beam_size=2, max_new_tokens=12, word_timestamps=False)
+    c2 = E.Context(m, max_batch=2, beam_size=2, max_new_tokens=12, word_timestamps=False)
+    r1, r2 = c1.transcribe(a), c2.transcribe(a)
+    assert [r.tokens for r in r1] == [r.tokens for r in r2]
+    print(storage, "tensors", n, "tokens", [len(r.tokens) for r in r1])

@@ -1,0 +1,247 @@
+"""CPU tests of the faster-whisper host loop (wmx.transcribe.WhisperModel) over a fake decoding context:
+language detected once and then fixed, the word-timestamp seek rule, the no-speech skip, control-token
+suppression, keyword validation, and StreamBatcher's per-stream options and error handling.
+
+Rules restated from faster-whisper 1.2.1 transcribe.py (not in the container):
+  * generate_segments: `seek = round(last_word_end * frames_per_second)` when word_timestamps and the window does
+    not end on a single timestamp; detect_language once before the loop; initial_prompt " " + prompt.strip();
+  * get_suppressed_tokens: -1 -> non-speech set, + transcribe/translate/sot/sot_prev/sot_lm (+ no_speech, openai).
+"""
+import numpy as np
+import pytest
+
+from wmx import online as OL
+from wmx import transcribe as TR
+from wmx.engine import WindowResult
+from wmx.tokenizer import DEFAULT_SUPPRESS, SpecialTokens, SyntheticTokenizer, suppressed_tokens
+
+V = 51865
+SP = SpecialTokens(V)
+TB = SP.timestamp_begin
+
+
+class FakeCtx:
+    """Stands in for engine.Context: returns scripted windows and records what it was asked for."""
+
+    def __init__(self, log, key, windows):
+        self.log, self.key, self.windows = log, key, windows
+
+    def transcribe(self, audios, prompts=None, seek=None):
+        s = seek[0] if seek else 0
+        self.log.append({"key": self.key, "seek": s, "prompt": list(prompts[0]) if prompts else [],
+                         "n": len(audios)})
+        return [self.windows(s, i) for i in range(len(audios))]
+
+
+def make_model(windows, max_batch=1):
+    m = TR.WhisperModel.__new__(TR.WhisperModel)
+    m.tokenizer = SyntheticTokenizer(V)
+    m.name = "micro"
+    m.max_batch = max_batch
+    m.default_beam = 5
+    m.max_new_tokens = 32
+    m.suppress_tokens = [-1]
+    m.use_graph = False
+    m._ctx = {}
+    m.log = []
+
+    def context(beam_size, language_token, task, word_timestamps, **kw):
+        m.log.append({"context": (beam_size, language_token, task, word_timestamps, kw)})
+        return FakeCtx(m.log, (beam_size, language_token, task), windows)
+
+    m.context = context
+    return m
+
+
+def window(seek, i, lang=SP.lang0 + 1, no_speech=0.01, avg_lp=-0.3, single_ending=False):
+    """Two timestamped segments: [0.00 t1 t2 1.00][1.00 t3 t4 2.00] (+ a trailing timestamp pair unless
+    single_ending); DTW jump times put the last word's end at 1.87 s."""
+    toks = [TB + 0, 101, 102, TB + 50, TB + 50, 103, 104, TB + 100]
+    if not single_ending:
+        toks += [TB + 100]
+    jt = np.array([0.1, 0.5, 0.9, 1.3, 1.87], np.float32)
+    return WindowResult(toks, lang, 0.9, -2.0, avg_lp, no_speech, seek, jt, np.full(4, 0.8, np.float32))
+
+
+def test_language_detected_once_then_fixed():
+    m = make_model(window)
+    audio = np.zeros(16000 * 65, np.float32)  # 3 windows
+    segs, info = m.transcribe(audio, language=None, word_timestamps=False)
+    segs = list(segs)
+    keys = [e["key"] for e in m.log if "key" in e]
+    assert keys[0][1] is None  # first window: the engine detects
+    assert all(k[1] == SP.lang0 + 1 for k in keys[1:])  # later windows: the detected language, fixed
+    assert info.language == "zh" and len(keys) >= 3 and segs
+
+
+def test_word_timestamp_seek_rule():
+    m = make_model(window)
+    audio = np.zeros(16000 * 40, np.float32)
+    segs = list(m.transcribe(audio, word_timestamps=True)[0])
+    seeks = [e["seek"] for e in m.log if "seek" in e]
+    first_end = max(w.end for s in segs if s.seek == 0 for w in s.words)
+    # not single-ending -> seek = round(last word end * 100), not the timestamp-token position (200)
+    assert seeks[1] == round(first_end * 100) != 200
+    # without word timestamps the timestamp rule applies: last consecutive pair ends at <|2.00|> -> 100 * 2 frames
+    m2 = make_model(window)
+    list(m2.transcribe(audio, word_timestamps=False)[0])
+    assert [e["seek"] for e in m2.log if "seek" in e][1] == 200
+
+
+def test_single_ending_window_advances_full_segment():
+    m = make_model(lambda s, i: window(s, i, single_ending=True))
+    list(m.transcribe(np.zeros(16000 * 40, np.float32), word_timestamps=True)[0])
+    assert [e["seek"] for e in m.log if "seek" in e][:2] == [0, 3000]
+
+
+def test_no_speech_skip_rule():
+    # skipped: no_speech above threshold and avg_logprob not above log_prob_threshold
+    m = make_model(lambda s, i: window(s, i, no_speech=0.9, avg_lp=-1.0))
+    assert list(m.transcribe(np.zeros(16000 * 10, np.float32))[0]) == []
+    # kept: a high enough log probability overrides the no-speech probability
+    m = make_model(lambda s, i: window(s, i, no_speech=0.9, avg_lp=-0.5))
+    assert list(m.transcribe(np.zeros(16000 * 10, np.float32))[0])
+
+
+def test_initial_prompt_encoding_like_faster_whisper():
+    m = make_model(window)
+    list(m.transcribe(np.zeros(16000 * 5, np.float32), initial_prompt="  t12 t99 "))
+    assert [e["prompt"] for e in m.log if "prompt" in e][0] == [12, 99]
+    m = make_model(window)
+    list(m.transcribe(np.zeros(16000 * 5, np.float32), initial_prompt=[5, 6, 7]))
+    assert [e["prompt"] for e in m.log if "prompt" in e][0] == [5, 6, 7]
+
+
+@pytest.mark.parametrize("kw,exc", [({"vad_filter": True}, NotImplementedError),
+                                    ({"temperature": 0.2}, NotImplementedError),
+                                    ({"temperature": (0.0, 0.2, 0.4)}, NotImplementedError),
+                                    ({"hotwords": "abc"}, NotImplementedError),
+                                    ({"no_such_option": 1}, TypeError)])
+def test_unsupported_options_raise(kw, exc):
+    m = make_model(window)
+    with pytest.raises(exc):
+        m.transcribe(np.zeros(16000, np.float32), **kw)
+
+
+def test_supported_options_reach_the_context():
+    m = make_model(window)
+    list(m.transcribe(np.zeros(16000, np.float32), beam_size=3, patience=2.0, length_penalty=0.5,
+                      vad_filter=False, temperature=[0.0], log_progress=True)[0])
+    ctx = [e["context"] for e in m.log if "context" in e][0]
+    assert ctx[0] == 3 and ctx[4]["patience"] == 2.0 and ctx[4]["length_penalty"] == 0.5
+
+
+def test_suppressed_tokens_include_control_tokens():
+    s = suppressed_tokens(SP, [-1])
+    for t in (SP.transcribe, SP.translate, SP.sot, SP.sot_prev, SP.sot_lm, SP.no_speech):
+        assert t in s
+    assert set(DEFAULT_SUPPRESS) <= set(s)
+    assert SP.eot not in s and TB not in s and SP.lang0 not in s
+    s2 = suppressed_tokens(SP, [])
+    assert set(s2) == {SP.transcribe, SP.translate, SP.sot, SP.sot_prev, SP.sot_lm, SP.no_speech}
+
+
+class ASRView:
+    sep = ""
+
+    def __init__(self, lang=None, task=None):
+        self.original_language = lang
+        self.transcribe_kargs = {"beam_size": 5}
+        if task:
+            self.transcribe_kargs["task"] = task
+
+    def ts_words(self, segments):
+        return [(w.start, w.end, w.word) for s in segments for w in (s.words or [])]
+
+    def segments_end_ts(self, segments):
+        return [s.end for s in segments]
+
+
+class BatchModel:
+    def __init__(self, fail=()):
+        self.calls, self.fail = [], set(fail)
+
+    def transcribe_batch(self, audios, prompts, language=None, task="transcribe", beam_size=None):
+        self.calls.append({"n": len(audios), "language": language, "task": task, "beam": beam_size})
+        return [RuntimeError("boom") if i in self.fail else [] for i in range(len(audios))]
+
+
+def _streams(n):
+    out = []
+    for _ in range(n):
+        v = OL.VACOnlineASRProcessor(0.5, ASRView(), vad=OL.FixedVADIterator(OL.ScriptedVAD([0.9] * 400)))
+        v.insert_audio_chunk(np.zeros(16000, np.float32))  # speech starts (padded start inside this chunk)
+        v.insert_audio_chunk(np.zeros(16000, np.float32))  # voiced: the whole chunk reaches the processor
+        assert v.wants_iter()
+        out.append(v)
+    return out
+
+
+def test_stream_batcher_passes_language_and_task():
+    bm = BatchModel()
+    OL.StreamBatcher(bm, ASRView("zh", "translate")).step(_streams(3))
+    assert bm.calls == [{"n": 3, "language": "zh", "task": "translate", "beam": 5}]
+
+
+def test_stream_batcher_isolates_a_failing_stream():
+    bm = BatchModel(fail={1})
+    st = _streams(3)
+    st[1].online.buffer_time_offset = 7.0
+    outs = OL.StreamBatcher(bm, ASRView()).step(st)
+    assert outs[1] == (None, None, "")
+    assert st[1].online.buffer_time_offset == 7.0 and len(st[1].online.audio_buffer) == 0  # reset, offset kept
+    assert len(st[0].online.audio_buffer) > 0  # the other streams are untouched
+
+
+# ---- real-checkpoint host paths (SURVEY §8f-2 tokenizer, §8f-4 checkpoint config) ----
+def _tiny_tokenizer_dir(tmp_path):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    tk = Tokenizer(models.BPE())
+    tk.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tk.decoder = decoders.ByteLevel()
+    tr = trainers.BpeTrainer(vocab_size=400, initial_alphabet=pre_tokenizers.ByteLevel.alphabet())
+    corpus = ["hello world, this is a tiny whisper tokenizer test.", "the quick brown fox jumps over the lazy dog!",
+              "你好世界 speech recognition"] * 20
+    tk.train_from_iterator(corpus, tr)
+    tk.save(str(tmp_path / "tokenizer.json"))
+    return str(tmp_path)
+
+
+def test_hf_tokenizer_prompt_and_word_split(tmp_path):
+    from wmx.tokenizer import HFTokenizer, load_tokenizer
+    d = _tiny_tokenizer_dir(tmp_path)
+    tok = load_tokenizer(d, V)
+    assert isinstance(tok, HFTokenizer)
+    text = " hello world, the quick fox!"
+    ids = tok.encode(text)
+    assert ids and all(0 <= t < tok.eot for t in ids)
+    assert tok.decode(ids) == text
+    # timestamps render like openai's decode_with_timestamps; decode() drops them
+    assert tok.decode_with_timestamps([TB + 50] + ids[:2]).startswith("<|1.00|>")
+    assert tok.decode(ids + [TB + 3]) == text
+    # word grouping (split_tokens_on_spaces): words re-join to the text, punctuation is its own word
+    words, wt = tok.split_to_word_tokens(ids + [tok.eot], "en")
+    assert "".join(words[:-1]) == text
+    assert [w.strip() for w in words[:-1]] == ["hello", "world", ",", "the", "quick", "fox", "!"]
+    assert sum(len(t) for t in wt) == len(ids) + 1
+    # unicode splitting (zh): every word decodes to whole characters
+    zh = tok.encode("你好世界")
+    zw, zt = tok.split_to_word_tokens(zh + [tok.eot], "zh")
+    assert "".join(zw[:-1]) == "你好世界" and all("�" not in w for w in zw)
+    # the prompt path of WhisperModel.transcribe: " " + prompt.strip()
+    m = make_model(window)
+    m.tokenizer = tok
+    list(m.transcribe(np.zeros(16000 * 5, np.float32), initial_prompt="hello world ")[0])
+    assert [e["prompt"] for e in m.log if "prompt" in e][0] == tok.encode(" hello world")
+
+
+@pytest.mark.parametrize("cfg,name", [
+    ({"d_model": 1280, "num_mel_bins": 128, "decoder_layers": 32, "encoder_layers": 32}, "large-v3"),
+    ({"d_model": 1280, "num_mel_bins": 80, "decoder_layers": 32, "encoder_layers": 32}, "large-v2"),
+    ({"d_model": 1280, "num_mel_bins": 128, "decoder_layers": 4, "encoder_layers": 32}, "large-v3-turbo"),
+    ({"d_model": 384, "num_mel_bins": 80, "decoder_layers": 4, "encoder_layers": 4}, "tiny"),
+    ({"d_model": 512, "num_mel_bins": 80, "decoder_layers": 6, "encoder_layers": 6}, "base")])
+def test_checkpoint_config_names(tmp_path, cfg, name):
+    import json
+    (tmp_path / "config.json").write_text(json.dumps(cfg))
+    assert TR._infer_name(str(tmp_path)) == name
