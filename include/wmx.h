@@ -149,6 +149,20 @@ wmx_status wmx_encode_device(wmx_ctx* c, const float* mel_dev, int B);
 wmx_status wmx_decoder_logits(wmx_ctx* c, const int32_t* tokens, const int32_t* lens, int B, int T,
                               float* logits_out);
 
+/* parity hook for the decode-STEP kernels (the launches a transcribe step replays: packed split-K GEMMs,
+ * ancestry-gathered self attention, cross attention, reduce + LayerNorm, logits), teacher-forced: the B encoded
+ * windows' rows (R = B x beam_size, row r belongs to window r / beam_size) are prefilled with prefix [B][P]
+ * (window b's first prefix_lens[b] ids, left-padded to P as transcribe pads prompts; prefix_lens NULL = all P), then
+ * n_steps steps each append tokens[i][r] to the history of row parents[i][r] (a row of the same window; the
+ * beam reorder of a real step, ancestry rows only) and run one decode step.  Step 0 is the prefill's last position
+ * (shared by a window's rows).  top1 [(n_steps+1)][R] = argmax of the raw logits (lowest id on ties); logits
+ * (nullable) [(n_steps+1)/every rounded up][R][n_vocab] = the raw logits of steps 0, every, 2*every, ...
+ * Replaces nothing in the reference; tests only. */
+wmx_status wmx_ctx_forced_decode(wmx_ctx* c, const int32_t* prefix, const int32_t* prefix_lens, int P, int B,
+                                 int n_steps,
+                                 const int32_t* tokens, const int32_t* parents, int32_t* top1, float* logits,
+                                 int every);
+
 /* the hot path: pcm -> log-mel -> encoder -> [language detect] -> prompt prefill -> greedy/beam decode
  * (hipGraph) -> [alignment forward + DTW].  prompt_ids: concatenated previous-text token ids per window
  * (prompt_lens[b] each; faster-whisper keeps the last 223); NULL = no prompt. */
@@ -173,6 +187,15 @@ int wmx_ctx_last_steps(wmx_ctx* c);
  * 5 decoder self-attention (one layer, at the last decoded length), 6 the whole encoder over B windows. */
 wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float* avg_ms, double* bytes,
                                 double* flops);
+
+/* parity recorder of the decode SEARCH (tests only): with max_steps > 0 every following wmx_transcribe copies,
+ * per decode step i < max_steps (step 0 = the selection from the prompt prefill), the raw logits of each of its
+ * R = B x beam_size rows before the rules and selection, and the selection: greedy (row, token) of live rows, beam
+ * (parent row, token) of the rows of windows still searching, (-1, -1) otherwise.  max_steps = 0 turns it off.
+ * wmx_ctx_recorded: n_steps = min(steps of the last transcribe, max_steps), rows = its R; logits (nullable)
+ * [n_steps][R][n_vocab], sel (nullable) [n_steps][R][2]. */
+wmx_status wmx_ctx_record(wmx_ctx* c, int max_steps);
+wmx_status wmx_ctx_recorded(wmx_ctx* c, float* logits, int32_t* sel, int* n_steps, int* rows);
 
 /* ---- pre-ASR DSP of the microphone loop, batched over B streams ----
  * band-pass "vocal separation" (reference vocal_separation.py:335-358, SimpleFilterSeparator.separate):

@@ -560,6 +560,40 @@ def decode(W, d: Dims, enc: np.ndarray, opt: DecodeOptions, prompt_ids=(), force
     return _beam(W, d, sp, opt, base, logits[-1], no_speech, lang, max_new)
 
 
+def forced_rows(W, d: Dims, encs, prefix, tokens, parents, K: int, keep=None):
+    """Teacher-forced decoding of R = len(encs) x K rows (row r belongs to window r // K), the beam bookkeeping of
+    openai BeamSearchDecoder.update (decoding.py: each new row continues the KV cache of its source row):
+    every row starts from prefix[b]; step i appends tokens[i][r] to the sequence of row parents[i][r].
+    Returns (top1 [n+1][R], top-2 margin [n+1][R], {step: logits [R][V]} for the steps in `keep`), step 0 = the
+    prefix's last position."""
+    R = len(encs) * K
+    n = len(tokens)
+    keep = set(range(n + 1)) if keep is None else set(keep)
+    caches, last = [], []
+    for b, enc in enumerate(encs):
+        c = DecoderCache(W, d, enc)
+        lg = decoder_forward(W, d, list(prefix[b]), c)[-1]
+        for _ in range(K):
+            caches.append(c.copy())
+            last.append(lg)
+    top1 = np.zeros((n + 1, R), np.int64)
+    margin = np.zeros((n + 1, R), np.float32)
+    out = {}
+    for i in range(n + 1):
+        L = np.stack(last)
+        top1[i] = np.argmax(L, axis=-1)
+        t2 = np.partition(L, -2, axis=-1)[:, -2:]
+        margin[i] = t2[:, 1] - t2[:, 0]
+        if i in keep:
+            out[i] = L
+        if i == n:
+            break
+        new_c = [caches[int(parents[i][r])].copy() for r in range(R)]
+        last = [decoder_forward(W, d, [int(tokens[i][r])], new_c[r])[0] for r in range(R)]
+        caches = new_c
+    return top1, margin, out
+
+
 def _greedy(W, d, sp, opt, cache, last_logits, no_speech, lang, max_new, forced):
     sampled, total, trace = [], 0.0, []
     cur = last_logits
@@ -591,6 +625,7 @@ def _beam(W, d, sp, opt, cache0, last_logits, no_speech, lang, max_new):
     max_cand = int(round(K * opt.patience))
     beams = [([], 0.0, cache0.copy(), last_logits) for _ in range(K)]
     finished = {}
+    trace = []
     for step in range(max_new):
         cands = []
         seen = set()
@@ -606,13 +641,19 @@ def _beam(W, d, sp, opt, cache0, last_logits, no_speech, lang, max_new):
                 cands.append((score + float(lp[t]), j, int(t), s))
         cands.sort(key=lambda c: (-c[0], c[1], c[2]))
         new_beams, new_fin = [], []
+        used = 0
         for sc, j, t, s in cands:
+            used += 1
             if t == sp.eot:
                 new_fin.append((s, sc))
             else:
                 new_beams.append((list(s), sc, j))
                 if len(new_beams) == K:
                     break
+        # selection margin of this step: the smallest score gap among the candidates that decided it and the first
+        # one left out (a perturbation below it cannot change which hypotheses survive, nor their order)
+        sc_used = [c[0] for c in cands[: used + 1]]
+        trace.append(min([a - b for a, b in zip(sc_used, sc_used[1:])], default=np.inf))
         for s, sc in new_fin:
             if len(finished) >= max_cand:
                 break
@@ -635,14 +676,146 @@ def _beam(W, d, sp, opt, cache0, last_logits, no_speech, lang, max_new):
             if len(finished) >= K:
                 break
     best, best_score, best_sum = None, -np.inf, 0.0
+    norms = []
     for s, sc in finished.items():
         toks = [t for t in s if t != sp.eot]
         L = max(len(toks), 1)  # openai ranks the sequence trimmed at EOT (decoding.py DecodingTask.run)
         pen = L if opt.length_penalty is None else ((5 + L) / 6) ** opt.length_penalty
         norm = sc / pen
+        norms.append(norm)
         if norm > best_score:
             best, best_score, best_sum = toks, norm, sc
-    return DecodeResult(best, best_sum, best_sum / (len(best) + 1), no_speech, lang)
+    res = DecodeResult(best, best_sum, best_sum / (len(best) + 1), no_speech, lang)
+    res.trace = trace  # per step: selection margin (see above)
+    norms.sort(reverse=True)
+    res.final_margin = norms[0] - norms[1] if len(norms) > 1 else np.inf  # ranking margin of the chosen sequence
+    return res
+
+
+def topk_stable(lp, k: int):
+    """The k best ids by (value desc, id asc) -- np.lexsort((ids, -lp))[:k] -- via a partition (same result)."""
+    thr = np.partition(lp, -k)[-k]
+    c = np.nonzero(lp >= thr)[0]
+    return c[np.lexsort((c, -lp[c]))][:k]
+
+
+def _ts_rule_gap(x, sp: Special, opt: DecodeOptions) -> float:
+    """|logsumexp(timestamp log-probs) - max(text log-prob)| of apply_rules' last rule, on the logits it sees."""
+    if opt.without_timestamps:
+        return np.inf
+    lp = log_softmax(x)
+    tb = sp.timestamp_begin
+    a, b = logsumexp(lp[tb:]), np.max(lp[:tb])
+    if not (np.isfinite(a) and np.isfinite(b)):
+        return np.inf
+    return abs(a - b)
+
+
+def search_replay(logits, sel, K: int, sp: Special, opt: DecodeOptions, eps: float = 1e-3):
+    """The decode SEARCH of _greedy / _beam, replayed on recorded per-step logits (wmx_ctx_record: logits [n][R][V]
+    of the R = windows x K rows, the device's selection sel [n][R][2]) so the rules, top-k, beam bookkeeping and
+    finished-hypothesis handling are checked token-exactly over every recorded step, independent of the 16-bit
+    noise in the logits.  Per window the replay compares its own selection with the device's at every step; a
+    disagreement at a step whose deciding score gap (or timestamp-rule gap) is below `eps` is a legitimate
+    float tie (f32 device log-softmax vs f64 here) and ends that window's comparison.
+    Returns per window dict(steps=compared steps, ties=bool, mismatch=None or (step, ours, device),
+    finished=[(tokens, score)], alive=[(tokens, score)])."""
+    n, R, _ = logits.shape
+    B = R // K
+    out = []
+    for b in range(B):
+        rows = range(b * K, (b + 1) * K)
+        info = dict(steps=0, ties=False, mismatch=None, finished=[], alive=[])
+        if K == 1:
+            r, seq, total = b, [], 0.0
+            for i in range(n):
+                dev = tuple(sel[i][r])
+                if dev[0] < 0:
+                    break
+                x = apply_rules(logits[i][r], seq, sp, opt)
+                order = np.argsort(-x, kind="stable")
+                tok = int(order[0])
+                gap = min(float(x[order[0]] - x[order[1]]), _ts_rule_gap(logits[i][r], sp, opt))
+                if tok != dev[1]:
+                    if gap <= eps:
+                        info["ties"] = True
+                    else:
+                        info["mismatch"] = (i, tok, dev[1])
+                    break
+                info["steps"] += 1
+                total += float(log_softmax(x)[tok])
+                if tok == sp.eot:
+                    info["finished"].append((list(seq), total))
+                    break
+                seq.append(tok)
+            if not info["finished"]:
+                info["alive"].append((list(seq), total))
+            out.append(info)
+            continue
+        max_cand = int(round(K * opt.patience))
+        beams = [([], 0.0) for _ in range(K)]
+        finished = {}
+        for i in range(n):
+            dev = [tuple(sel[i][r]) for r in rows]
+            if dev[0][0] < 0:
+                break
+            cands = []
+            gap_rule = np.inf
+            for j, (seq, score) in enumerate(beams if i > 0 else beams[:1]):
+                lg = logits[i][b * K + j]
+                x = apply_rules(lg, seq, sp, opt)
+                gap_rule = min(gap_rule, _ts_rule_gap(lg, sp, opt))
+                lp = log_softmax(x)
+                cands += [(score + float(lp[t]), j, int(t)) for t in topk_stable(lp, K + 1)]
+            cands.sort(key=lambda c: (-c[0], c[1], c[2]))
+            new_beams, new_fin, used = [], [], 0
+            for sc, j, t in cands:
+                used += 1
+                if t == sp.eot:
+                    new_fin.append((beams[j][0], sc))
+                else:
+                    new_beams.append((beams[j][0] + [t], sc, j))
+                    if len(new_beams) == K:
+                        break
+            scs = [c[0] for c in cands[: used + 1]]
+            gap = min([gap_rule] + [a - c for a, c in zip(scs, scs[1:])])
+            ours = [(b * K + j, s[-1]) for s, _, j in new_beams]
+            if ours != dev[: len(ours)]:
+                if gap <= eps:
+                    info["ties"] = True
+                else:
+                    info["mismatch"] = (i, ours, dev)
+                break
+            info["steps"] += 1
+            for s, sc in new_fin:
+                if len(finished) >= max_cand:
+                    break
+                finished.setdefault(tuple(s), sc)
+            beams = [(s, sc) for s, sc, _ in new_beams]
+            if len(finished) >= max_cand:
+                break
+        info["finished"] = [(list(s), sc) for s, sc in finished.items()]
+        info["alive"] = [(list(s), sc) for s, sc in beams]
+        out.append(info)
+    return out
+
+
+def rank_final(finished, alive, K: int, length_penalty=None):
+    """openai BeamSearchDecoder.finalize (fill the finished list from the best alive beams) +
+    MaximumLikelihoodRanker; returns (tokens, sum_logprob, ranking margin to the runner-up)."""
+    fin = dict((tuple(s), sc) for s, sc in finished)
+    for s, sc in sorted(alive, key=lambda a: -a[1]):
+        if len(fin) >= K:
+            break
+        fin.setdefault(tuple(s), sc)
+    scored = []
+    for s, sc in fin.items():
+        L = max(len(s), 1)
+        pen = L if length_penalty is None else ((5 + L) / 6) ** length_penalty
+        scored.append((sc / pen, list(s), sc))
+    scored.sort(key=lambda a: -a[0])
+    margin = scored[0][0] - scored[1][0] if len(scored) > 1 else np.inf
+    return scored[0][1], scored[0][2], margin
 
 
 # ----------------------------------------------------------------------------------------------

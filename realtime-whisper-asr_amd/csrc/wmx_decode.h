@@ -47,6 +47,11 @@ void launch_lang_detect(const float* logits, int ldl, int lang0, int nlang, int 
                         const int* lang_slot, int* lang_out, float* prob_out, hipStream_t st);
 void launch_token_prob(const float* logits, int ldl, int V, int token, int rows, float* out, hipStream_t st);
 void launch_text_prob(const float* logits, int ldl, int eot, const int* target, int rows, float* out, hipStream_t st);
+// parity instrumentation (wmx_ctx_record)
+void launch_record_logits(const float* logits, int ldl, int V, int R, const int* row_map, const int* slot,
+                          const int* base, int cap, float* out, hipStream_t st);
+void launch_record_select(int R, int K, const int* ctok, const RowPtrs& rp, const BeamState& bs, const int* slot,
+                          const int* base, int after, int cap, int* out, hipStream_t st);
 // alignment matrix [nwin][Tn][Tk]: zero, accumulate heads (softmax over nframes/2, normalise over tokens, median
 // filter), scale by 1/n_heads
 void launch_align_matrix_zero(float* out, int nwin, int Tn, int Tk, hipStream_t st);

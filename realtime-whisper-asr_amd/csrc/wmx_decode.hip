@@ -809,6 +809,56 @@ void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const
   WMX_HIP(hipGetLastError());
 }
 
+// ---- parity instrumentation (wmx_ctx_record): per decode step, the raw logits of every row before selection and
+// the selection itself, at step index *slot - *base (- 1 after the update has advanced the slot) ----
+__global__ void record_logits_kernel(const float* __restrict__ logits, int ldl, int V, int R, const int* __restrict__ row_map,
+                                     const int* __restrict__ slot, const int* __restrict__ base, int cap,
+                                     float* __restrict__ out) {
+  const int r = blockIdx.y;
+  const int idx = *slot - *base;
+  if (idx < 0 || idx >= cap) return;
+  const float* src = logits + (long)(row_map ? row_map[r] : r) * ldl;
+  float* dst = out + ((long)idx * R + r) * V;
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) dst[v] = src[v];
+}
+
+// greedy (before the update): (row, first candidate) of live rows; beam (after the update): (parent, token) of the
+// rows of windows active this step; (-1, -1) otherwise
+__global__ void record_select_kernel(int R, int K, int KP, const int* __restrict__ ctok, const int* __restrict__ done,
+                                     const int* __restrict__ win_active, const int* __restrict__ new_parent,
+                                     const int* __restrict__ new_tok, const int* __restrict__ slot,
+                                     const int* __restrict__ base, int after, int cap, int* __restrict__ out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = *slot - *base - after;
+  if (r >= R || idx < 0 || idx >= cap) return;
+  int p = -1, t = -1;
+  if (K == 1) {
+    if (!done[r]) {
+      p = r;
+      t = ctok[r * KP];
+    }
+  } else if (win_active[r / K]) {
+    p = new_parent[r];
+    t = new_tok[r];
+  }
+  out[((long)idx * R + r) * 2] = p;
+  out[((long)idx * R + r) * 2 + 1] = t;
+}
+
+void launch_record_logits(const float* logits, int ldl, int V, int R, const int* row_map, const int* slot,
+                          const int* base, int cap, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(record_logits_kernel, dim3(32, R), dim3(256), 0, st, logits, ldl, V, R, row_map, slot, base, cap,
+                     out);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_record_select(int R, int K, const int* ctok, const RowPtrs& rp, const BeamState& bs, const int* slot,
+                          const int* base, int after, int cap, int* out, hipStream_t st) {
+  hipLaunchKernelGGL(record_select_kernel, dim3((R + 255) / 256), dim3(256), 0, st, R, K, K + (K > 1 ? 1 : 0), ctok,
+                     rp.done, bs.win_active, bs.new_parent, bs.new_tok, slot, base, after, cap, out);
+  WMX_HIP(hipGetLastError());
+}
+
 void launch_greedy_update(const RowPtrs& rp, const int* tok, const float* lp, int R, int tb, int eot, int* hist,
                           int hist_ld, int* slot, int* n_done, hipStream_t st) {
   WMX_CHECK(R <= 1024, "greedy: too many rows");

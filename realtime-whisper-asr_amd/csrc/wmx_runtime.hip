@@ -470,6 +470,11 @@ struct Ctx {
   int probe_n = 0;
   float stage_ms[7] = {0};
   int last_steps = 0;
+  // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
+  float* rec_logits = nullptr;
+  int* rec_sel = nullptr;
+  int* rec_base = nullptr;
+  int rec_cap = 0, rec_R = 0;
 };
 
 static void sync(Ctx& c) { WMX_HIP(hipStreamSynchronize(c.st)); }
@@ -1155,6 +1160,29 @@ static void logmel_dev(Ctx& c, const float* pcm_dev, long stride, const long* le
   sync(c);  // sk / lens host vectors
 }
 
+// rules + selection over c.logits (row_map: logits row of each decode row, NULL = identity) and the greedy / beam
+// update that appends the chosen tokens at *slot + 1; with the parity recorder on, the logits and the selection of
+// the step are copied out as well
+static void select_and_update(Ctx& c, int B, const int* row_map) {
+  Model& m = *c.m;
+  const int K = c.K, R = K * B;
+  const bool rec = c.rec_logits != nullptr;
+  if (rec)
+    launch_record_logits(c.logits, c.ldl, m.d.n_vocab, R, row_map, c.slot, c.rec_base, c.rec_cap, c.rec_logits, c.st);
+  RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
+              c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
+  launch_logits_select(c.logits, c.ldl, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, row_map, c.sel_ws, c.st);
+  if (K == 1) {
+    if (rec) launch_record_select(R, K, c.ctok, c.rp, c.bs, c.slot, c.rec_base, 0, c.rec_cap, c.rec_sel, c.st);
+    launch_greedy_update(c.rp, c.ctok, c.clp, R, c.sp.timestamp_begin, c.sp.eot, c.hist, c.Tctx, c.slot, c.n_done,
+                         c.st);
+  } else {
+    launch_beam_step(c.rp, c.rtmp, c.ctok, c.clp, B, K, c.max_cand, c.sp.timestamp_begin, c.sp.eot, c.slot, c.hist,
+                     c.hist_tmp, c.anc, c.anc_tmp, c.Tctx, c.bs, c.n_done, c.st);
+    if (rec) launch_record_select(R, K, c.ctok, c.rp, c.bs, c.slot, c.rec_base, 1, c.rec_cap, c.rec_sel, c.st);
+  }
+}
+
 static void run_step(Ctx& c, int B) {
   // one decode step: forward all rows at slot *slot, select, update (advances *slot)
   Model& m = *c.m;
@@ -1169,16 +1197,7 @@ static void run_step(Ctx& c, int B) {
   f.anc = c.K > 1 ? c.anc : nullptr;
   dec_step_fast(c, f);
   dec_logits(c, nullptr, f.rows, true);
-  RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
-              c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
-  launch_logits_select(c.logits, c.ldl, ro, c.rp, f.rows, c.K + (c.K > 1 ? 1 : 0), c.ctok, c.clp, nullptr,
-                       c.sel_ws, c.st);
-  if (c.K == 1)
-    launch_greedy_update(c.rp, c.ctok, c.clp, f.rows, c.sp.timestamp_begin, c.sp.eot, c.hist, c.Tctx, c.slot, c.n_done,
-                         c.st);
-  else
-    launch_beam_step(c.rp, c.rtmp, c.ctok, c.clp, B, c.K, c.max_cand, c.sp.timestamp_begin, c.sp.eot, c.slot, c.hist,
-                     c.hist_tmp, c.anc, c.anc_tmp, c.Tctx, c.bs, c.n_done, c.st);
+  select_and_update(c, B, nullptr);
 }
 
 // decode steps between n_done read-backs; the chunk is one graph launch
@@ -1202,6 +1221,7 @@ static void ensure_step_graphs(Ctx& c, int B) {
                                  c.o.max_initial_timestamp_index,
                                  c.o.without_timestamps,
                                  (long)(intptr_t)c.mask,
+                                 (long)(intptr_t)c.rec_logits,
                                  c.probe_kernel,
                                  c.probe_layer};
   if (c.graph[0] && c.graph[1] && key == c.graph_key) return;
@@ -1336,15 +1356,15 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   const int max_new = std::max(0, std::min(c.o.max_new_tokens, T - Pmax));
   set_slot(c, Pmax - 1);
   int steps = 0;
+  if (c.rec_logits) {  // recorder step 0 = this first selection (slot Pmax - 1)
+    c.rec_R = R;
+    c.pinned_i[1] = Pmax - 1;
+    WMX_HIP(hipMemcpyAsync(c.rec_base, c.pinned_i + 1, 4, hipMemcpyHostToDevice, c.st));
+    WMX_HIP(hipMemsetD32Async((hipDeviceptr_t)c.rec_sel, -1, (size_t)c.rec_cap * c.R * 2, c.st));
+    sync(c);
+  }
   if (max_new > 0) {
-    RuleOpts ro{V, sp.eot, sp.timestamp_begin, sp.no_timestamps, sp.blank, c.o.suppress_blank,
-                c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
-    launch_logits_select(c.logits, c.ldl, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, c.row_map, c.sel_ws, c.st);
-    if (K == 1)
-      launch_greedy_update(c.rp, c.ctok, c.clp, R, sp.timestamp_begin, sp.eot, c.hist, T, c.slot, c.n_done, c.st);
-    else
-      launch_beam_step(c.rp, c.rtmp, c.ctok, c.clp, B, K, c.max_cand, sp.timestamp_begin, sp.eot, c.slot, c.hist,
-                       c.hist_tmp, c.anc, c.anc_tmp, T, c.bs, c.n_done, c.st);
+    select_and_update(c, B, c.row_map);
     steps = 1;
   }
   rec(c, 5);
@@ -1590,6 +1610,15 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
 // C ABI
 // =================================================================================================
 using namespace wmx;
+
+static void free_recorder(Ctx& c) {
+  for (void* p : {(void*)c.rec_logits, (void*)c.rec_sel, (void*)c.rec_base})
+    if (p) (void)hipFree(p);
+  c.rec_logits = nullptr;
+  c.rec_sel = nullptr;
+  c.rec_base = nullptr;
+  c.rec_cap = 0;
+}
 
 struct wmx_model {
   Model m;
@@ -1856,6 +1885,7 @@ void wmx_ctx_destroy(wmx_ctx* x) {
   (void)hipSetDevice(c.m->device);
   (void)hipStreamSynchronize(c.st);
   drop_step_graphs(c);
+  free_recorder(c);
   if (c.buf) (void)hipFree(c.buf);
   if (c.pinned_i) (void)hipHostFree(c.pinned_i);
   for (auto& e : c.ev)
@@ -1958,6 +1988,137 @@ wmx_status wmx_decoder_logits(wmx_ctx* x, const int32_t* tokens, const int32_t* 
       sync(c);
     }
     (void)lens;
+  });
+}
+
+wmx_status wmx_ctx_forced_decode(wmx_ctx* x, const int32_t* prefix, const int32_t* prefix_lens, int P, int B,
+                                 int n_steps, const int32_t* tokens, const int32_t* parents, int32_t* top1,
+                                 float* logits, int every) {
+  return guard([&] {
+    Ctx& c = x->c;
+    Model& m = *c.m;
+    WMX_CHECK(m.initialized, "forced_decode: weights not initialised");
+    WMX_CHECK(B >= 1 && B <= c.maxB && P >= 1 && n_steps >= 0 && P + n_steps <= c.Tctx, "forced_decode: shape");
+    WMX_CHECK(prefix && top1 && (n_steps == 0 || (tokens && parents)) && (!logits || every >= 1),
+              "forced_decode: null argument");
+    WMX_HIP(hipSetDevice(m.device));
+    const int K = c.K, R = K * B, T = c.Tctx, V = m.d.n_vocab;
+    for (int i = 0; i < n_steps; ++i)
+      for (int r = 0; r < R; ++r) {
+        const int p = parents[(size_t)i * R + r], t = tokens[(size_t)i * R + r];
+        WMX_CHECK(p >= 0 && p < R && p / K == r / K, "forced_decode: parent outside the row's window");
+        WMX_CHECK(t >= 0 && t < V, "forced_decode: token id");
+      }
+    // the layout transcribe() sets up: window b's prefix (prefix_lens[b] ids) left-padded to P; row r of window b
+    // holds it, and its slots < P live in cache row b*K
+    std::vector<int> hist((size_t)R * T, 0), anc((size_t)R * T, 0), pad_row(R), pad_win(B);
+    for (int b = 0; b < B; ++b) {
+      const int n = prefix_lens ? prefix_lens[b] : P;
+      WMX_CHECK(n >= 1 && n <= P, "forced_decode: prefix length");
+      pad_win[b] = P - n;
+    }
+    for (int r = 0; r < R; ++r) {
+      const int b = r / K;
+      pad_row[r] = pad_win[b];
+      for (int i = pad_win[b]; i < P; ++i) hist[(size_t)r * T + i] = prefix[(size_t)b * P + i - pad_win[b]];
+      for (int s = 0; s < T; ++s) anc[(size_t)r * T + s] = s < P ? b * K : r;
+    }
+    WMX_HIP(hipMemcpyAsync(c.hist, hist.data(), hist.size() * 4, hipMemcpyHostToDevice, c.st));
+    WMX_HIP(hipMemcpyAsync(c.pad_row, pad_row.data(), R * 4, hipMemcpyHostToDevice, c.st));
+    WMX_HIP(hipMemcpyAsync(c.pad_win, pad_win.data(), B * 4, hipMemcpyHostToDevice, c.st));
+    set_slot(c, 0);
+    std::vector<float> lg((size_t)R * V);
+    auto collect = [&](int step, int nrows, int rep) {  // logits rows [0, nrows) -> top1 / logits of R rows
+      WMX_HIP(hipMemcpy2DAsync(lg.data(), (size_t)V * 4, c.logits, (size_t)c.ldl * 4, (size_t)V * 4, nrows,
+                               hipMemcpyDeviceToHost, c.st));
+      sync(c);
+      for (int r = 0; r < R; ++r) {
+        const float* row = lg.data() + (size_t)(r / rep) * V;
+        int best = 0;
+        for (int v = 1; v < V; ++v)
+          if (row[v] > row[best]) best = v;
+        top1[(size_t)step * R + r] = best;
+        if (logits && step % every == 0)
+          std::memcpy(logits + ((size_t)(step / every) * R + r) * V, row, (size_t)V * 4);
+      }
+    };
+    {  // prefill of the prefix, one sequence per window (cache rows b*K), logits of its last position
+      FwdArgs f;
+      f.rows = B;
+      f.Tn = P;
+      f.rmul = K;
+      f.tok = c.hist;
+      f.tok_ld = (long)K * T;
+      f.pad_seq = c.pad_win;
+      f.prefill = true;
+      f.anc = nullptr;
+      dec_forward(c, f);
+      std::vector<int> g(B);
+      for (int b = 0; b < B; ++b) g[b] = b * P + P - 1;
+      WMX_HIP(hipMemcpyAsync(c.gather, g.data(), B * 4, hipMemcpyHostToDevice, c.st));
+      dec_logits(c, c.gather, B);
+      collect(0, B, K);
+    }
+    std::vector<int> h2(hist.size()), a2(anc.size());
+    for (int i = 0; i < n_steps; ++i) {
+      const int s = P - 1 + i;  // slot of the last history token; the forced token goes to s + 1
+      for (int r = 0; r < R; ++r) {  // beam_update_kernel: parent history + ancestry, new token, own cache row
+        const int p = parents[(size_t)i * R + r];
+        std::memcpy(&h2[(size_t)r * T], &hist[(size_t)p * T], (size_t)T * 4);
+        std::memcpy(&a2[(size_t)r * T], &anc[(size_t)p * T], (size_t)T * 4);
+        h2[(size_t)r * T + s + 1] = tokens[(size_t)i * R + r];
+        a2[(size_t)r * T + s + 1] = r;
+      }
+      hist.swap(h2);
+      anc.swap(a2);
+      WMX_HIP(hipMemcpyAsync(c.hist, hist.data(), hist.size() * 4, hipMemcpyHostToDevice, c.st));
+      WMX_HIP(hipMemcpyAsync(c.anc, anc.data(), anc.size() * 4, hipMemcpyHostToDevice, c.st));
+      set_slot(c, s + 1);
+      // the launches of run_step() before its selection
+      FwdArgs f;
+      f.rows = R;
+      f.Tn = 1;
+      f.rmul = 1;
+      f.tok = c.hist;
+      f.tok_ld = T;
+      f.pad_seq = c.pad_row;
+      f.prefill = false;
+      f.anc = K > 1 ? c.anc : nullptr;
+      dec_step_fast(c, f);
+      dec_logits(c, nullptr, R, true);
+      collect(i + 1, R, 1);
+    }
+  });
+}
+
+wmx_status wmx_ctx_record(wmx_ctx* x, int max_steps) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(max_steps >= 0 && max_steps <= c.Tctx, "record: max_steps");
+    WMX_HIP(hipSetDevice(c.m->device));
+    sync(c);
+    drop_step_graphs(c);  // the captured steps carry (or lack) the record launches
+    free_recorder(c);
+    if (max_steps == 0) return;
+    WMX_HIP(hipMalloc(&c.rec_logits, (size_t)max_steps * c.R * c.m->d.n_vocab * 4));
+    WMX_HIP(hipMalloc(&c.rec_sel, (size_t)max_steps * c.R * 2 * 4));
+    WMX_HIP(hipMalloc(&c.rec_base, 4));
+    c.rec_cap = max_steps;
+  });
+}
+
+wmx_status wmx_ctx_recorded(wmx_ctx* x, float* logits, int32_t* sel, int* n_steps, int* rows) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(c.rec_logits, "recorded: the recorder is off (wmx_ctx_record)");
+    WMX_CHECK(n_steps && rows, "recorded: null argument");
+    WMX_HIP(hipSetDevice(c.m->device));
+    const int n = std::min(c.last_steps, c.rec_cap);
+    *n_steps = n;
+    *rows = c.rec_R;
+    if (logits)
+      WMX_HIP(hipMemcpy(logits, c.rec_logits, (size_t)n * c.rec_R * c.m->d.n_vocab * 4, hipMemcpyDeviceToHost));
+    if (sel) WMX_HIP(hipMemcpy(sel, c.rec_sel, (size_t)n * c.rec_R * 2 * 4, hipMemcpyDeviceToHost));
   });
 }
 

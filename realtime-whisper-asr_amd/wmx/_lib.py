@@ -55,7 +55,8 @@ EXPORTS = [
     "wmx_ctx_stream", "wmx_logmel", "wmx_logmel_device", "wmx_encode", "wmx_encode_device",
     "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device", "wmx_result_free",
     "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats",
-    "wmx_filtfilt", "wmx_filtfilt_device", "wmx_dedup_features",
+    "wmx_filtfilt", "wmx_filtfilt_device", "wmx_dedup_features", "wmx_ctx_forced_decode",
+    "wmx_ctx_record", "wmx_ctx_recorded",
 ]
 
 
@@ -86,6 +87,10 @@ def _load():
         "wmx_encode": (C.c_int, [VP, P(F), C.c_int, P(F)]),
         "wmx_encode_device": (C.c_int, [VP, VP, C.c_int]),
         "wmx_decoder_logits": (C.c_int, [VP, P(I32), P(I32), C.c_int, C.c_int, P(F)]),
+        "wmx_ctx_forced_decode": (C.c_int, [VP, P(I32), P(I32), C.c_int, C.c_int, C.c_int, P(I32), P(I32), P(I32), P(F),
+                                            C.c_int]),
+        "wmx_ctx_record": (C.c_int, [VP, C.c_int]),
+        "wmx_ctx_recorded": (C.c_int, [VP, P(F), P(I32), P(C.c_int), P(C.c_int)]),
         "wmx_transcribe": (C.c_int, [VP, P(F), I64, P(I64), P(I32), C.c_int, P(I32), P(I32), P(P(Result))]),
         "wmx_transcribe_device": (C.c_int, [VP, VP, I64, P(I64), P(I32), C.c_int, P(I32), P(I32), P(P(Result))]),
         "wmx_result_free": (None, [P(Result)]),

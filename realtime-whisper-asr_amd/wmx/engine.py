@@ -220,6 +220,41 @@ class Context:
         check(lib.wmx_decoder_logits(self._h, iptr(tokens), iptr(lens), B, T, fptr(out)))
         return out
 
+    def forced_decode(self, prefix, tokens: np.ndarray, parents: np.ndarray | None = None, logits_every: int = 0):
+        """Teacher-forced decode STEPS over the encoded windows (wmx_ctx_forced_decode): prefix = B token lists
+        (left-padded to the longest, as transcribe pads prompts);
+        tokens / parents [n_steps][R] with R = B x beam_size (parents None = every row extends itself).
+        Returns (top1 [n_steps+1][R], logits [ceil((n_steps+1)/every)][R][V] or None)."""
+        B, P = len(prefix), max(len(p) for p in prefix)
+        plens = np.array([len(p) for p in prefix], np.int32)
+        prefix = np.ascontiguousarray(np.array([list(p) + [0] * (P - len(p)) for p in prefix], np.int32))
+        R = B * self.opts.beam_size
+        tokens = np.ascontiguousarray(np.asarray(tokens, np.int32).reshape(-1, R))
+        n = tokens.shape[0]
+        if parents is None:
+            parents = np.tile(np.arange(R, dtype=np.int32), (n, 1))
+        parents = np.ascontiguousarray(np.asarray(parents, np.int32).reshape(n, R))
+        top1 = np.empty((n + 1, R), np.int32)
+        lg = None
+        if logits_every > 0:
+            lg = np.empty(((n + logits_every) // logits_every, R, self.model.dims.n_vocab), np.float32)
+        check(lib.wmx_ctx_forced_decode(self._h, iptr(prefix), iptr(plens) if plens is not None else None, P, B, n, iptr(tokens), iptr(parents), iptr(top1),
+                                        fptr(lg) if lg is not None else None, max(1, logits_every)))
+        return top1, lg
+
+    def record(self, max_steps: int):
+        """Parity recorder of the decode search (wmx_ctx_record); 0 turns it off."""
+        check(lib.wmx_ctx_record(self._h, int(max_steps)))
+
+    def recorded(self):
+        """(logits [n][R][V], selections [n][R][2]) of the last transcribe (wmx_ctx_recorded)."""
+        n, R = C.c_int(), C.c_int()
+        check(lib.wmx_ctx_recorded(self._h, None, None, C.byref(n), C.byref(R)))
+        lg = np.empty((n.value, R.value, self.model.dims.n_vocab), np.float32)
+        sel = np.empty((n.value, R.value, 2), np.int32)
+        check(lib.wmx_ctx_recorded(self._h, fptr(lg), iptr(sel), C.byref(n), C.byref(R)))
+        return lg, sel
+
     def _collect(self, res_ptr) -> list:
         r = res_ptr.contents
         out = []

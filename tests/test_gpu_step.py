@@ -1,0 +1,299 @@
+"""GPU parity of the decode STEP at the bench's shapes, and of the decode SEARCH over every step.
+
+What bench.py times per decode step (wmx_runtime.hip dec_step_fast + logits + select/update, replayed from a
+hipGraph) is checked here at the shapes it runs in, against the oracle, in two complementary ways:
+
+  * Step kernels, teacher-forced (wmx_ctx_forced_decode): the rows of B windows are fed a fixed token stream
+    (and, for beams, a fixed parent per row and step, i.e. the beam reorder of the ancestry rows) and the raw logits
+    of every step are compared with oracle.forced_rows (openai BeamSearchDecoder semantics: a new row continues its
+    parent's KV cache).  Shapes: large-v3 width (d = 1280, 20 heads, 128 mels, vocab 51866) with 20 rows -- the
+    per-group rows of the bench (4 windows x beam 5 and 20 windows greedy): packed split-K GEMMs with two 16-row
+    fragments (MT = 2), fc2 over K = 5120, the 16-wave fc1 -- and a micro model over 224 steps, so the
+    ancestry-gathered self attention runs past slot 200 with beams reordered every step.
+    Tolerances: relative L2 of each row's logits, bf16 <= 3e-2, f16 <= 5e-3 (tests/test_gpu_parity.py); and the
+    argmax must equal the oracle's wherever the oracle's top-2 margin exceeds twice the row's measured max abs
+    error (then no error of that size can flip it).  The number of steps compared this way is printed, and
+    f16 requires >= 16 per row.
+  * Search, token-exact (wmx_ctx_record + oracle.search_replay): a free-running transcribe records every step's
+    raw logits and the device's selection; the oracle replays the rules, top-k, beam bookkeeping and finished
+    handling on those same logits and must choose exactly the device's (parent, token) at every step (a step whose
+    deciding score gap is below 1e-3 is a legitimate f32-vs-f64 tie and ends that window's comparison), and the
+    final ranked sequence must equal the device's result.  This is what makes beam-5 parity testable at all with
+    random weights: free-running beams on random weights sit on near-ties (tools/ notes in DESIGN.md §4).
+"""
+import numpy as np
+import pytest
+
+from oracle import whisper_np as O
+from wmx import synth
+
+pytestmark = pytest.mark.gpu
+
+WIDE2 = O.Dims(128, 51866, 1280, 20, 1, 1280, 20, 2)  # large-v3 width, 1 encoder layer, 2 decoder layers
+REL = {"bf16": 3e-2, "f16": 5e-3}
+DT = {"bf16": "bfloat16", "f16": "float16"}
+EPS_TIE = 1e-3
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _edims(d):
+    from wmx import engine as E
+    return E.ModelDims(d.n_mels, d.n_vocab, d.n_audio_state, d.n_audio_head, d.n_audio_layer, d.n_text_state,
+                       d.n_text_head, d.n_text_layer)
+
+
+def _forced_stream(rng, n, R, K, V=50000):
+    tok = rng.integers(0, V, size=(n, R)).astype(np.int32)
+    par = np.tile(np.arange(R, dtype=np.int32), (n, 1))
+    if K > 1:
+        for i in range(n):
+            for b in range(R // K):
+                par[i, b * K:(b + 1) * K] = b * K + rng.integers(0, K, size=K)
+    return tok, par
+
+
+def _check_forced(tag, dt, top1, lg, every, ref_top1, ref_margin, ref_lg, min_cmp):
+    """rel-L2 at every snapshot step and argmax equality wherever the oracle margin > 2 x the row's max error."""
+    n1, R = top1.shape
+    err_row = np.zeros(R)
+    worst = 0.0
+    for si, step in enumerate(range(0, n1, every)):
+        for r in range(R):
+            e = rel_l2(lg[si, r], ref_lg[step][r])
+            worst = max(worst, e)
+            assert e <= REL[dt], (tag, step, r, e)
+            err_row[r] = max(err_row[r], float(np.max(np.abs(lg[si, r] - ref_lg[step][r]))))
+    cmp = np.zeros(R, int)
+    for r in range(R):
+        # steps without a logits snapshot use the row's worst snapshot error, x1.5
+        tau = 2 * err_row[r] * (1.0 if every == 1 else 1.5)
+        sel = ref_margin[:, r] > tau
+        np.testing.assert_array_equal(top1[sel, r], ref_top1[sel, r], err_msg=f"{tag} row {r}")
+        cmp[r] = int(sel.sum())
+    print(f"{tag} {dt}: {n1} steps x {R} rows, worst rel_l2 {worst:.2e}, argmax compared per row "
+          f"min {cmp.min()} mean {cmp.mean():.1f} of {n1}")
+    if dt == "f16":
+        assert cmp.min() >= min_cmp, cmp
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# large-v3 width fixture: 20 windows encoded once per dtype
+# ---------------------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module", params=["bf16", "f16"])
+def wide20(request):
+    from wmx import engine as E
+    dt = request.param
+    m = E.Model(_edims(WIDE2), 0, DT[dt]).init_synthetic(5)
+    W = O.make_weights(WIDE2, 5, dt)
+    lens = [480000, 150000, 320000, 16000, 240000] * 4
+    mels = np.stack([O.logmel_segment(synth.speech_like(100 + i, n), 128) for i, n in enumerate(lens)])
+    encs = [O.encoder(W, WIDE2, mel) for mel in mels]
+    return dt, m, W, mels, encs
+
+
+def test_forced_steps_wide_20rows_greedy(wide20):
+    """20 windows x greedy = 20 decode rows at d = 1280 (the bench's per-group row count), 32 forced steps."""
+    from wmx import engine as E
+    dt, m, W, mels, encs = wide20
+    sp = O.special_tokens(WIDE2.n_vocab)
+    ctx = E.Context(m, max_batch=20, beam_size=1, max_new_tokens=64, word_timestamps=False)
+    ctx.encode(mels, want_output=False)
+    n = 32
+    tok, par = _forced_stream(np.random.default_rng(1), n, 20, 1)
+    prefix = [[sp.sot, sp.lang0, sp.transcribe]] * 20
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, WIDE2, encs, prefix, tok, par, 1)
+    _check_forced("wide greedy R=20", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
+
+
+def test_forced_steps_wide_beam5_4windows(wide20):
+    """4 windows x beam 5 = 20 rows, parents re-drawn every step (ancestry-gathered self attention at width)."""
+    from wmx import engine as E
+    dt, m, W, mels, encs = wide20
+    sp = O.special_tokens(WIDE2.n_vocab)
+    ctx = E.Context(m, max_batch=4, beam_size=5, max_new_tokens=64, word_timestamps=False)
+    ctx.encode(mels[:4], want_output=False)
+    n = 32
+    tok, par = _forced_stream(np.random.default_rng(2), n, 20, 5)
+    # a prompted batch: previous-text prompts of different lengths, left-padded together (transcribe's layout)
+    prefix = [[sp.sot_prev] + list(range(1000, 1000 + L)) + [sp.sot, sp.lang0, sp.transcribe] for L in (0, 5, 11, 2)]
+    prefix[0] = [sp.sot, sp.lang0, sp.transcribe]
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, WIDE2, encs[:4], prefix, tok, par, 5)
+    _check_forced("wide beam5 B=4", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
+
+
+def test_forced_steps_micro_beam5_224():
+    """224 steps with beams reordered every step: self attention over up to 227 ancestry-gathered slots."""
+    from wmx import engine as E
+    d = O.DIMS["micro"]
+    sp = O.special_tokens(d.n_vocab)
+    dt = "f16"
+    m = E.Model("micro", 0, DT[dt]).init_synthetic(1)
+    W = O.make_weights(d, 1, dt)
+    mels = np.stack([O.logmel_segment(synth.speech_like(200 + i, n), 80)
+                     for i, n in enumerate((480000, 200000, 96000, 330000))])
+    encs = [O.encoder(W, d, mel) for mel in mels]
+    ctx = E.Context(m, max_batch=4, beam_size=5, max_new_tokens=224, word_timestamps=False)
+    ctx.encode(mels, want_output=False)
+    n, every = 224, 8
+    tok, par = _forced_stream(np.random.default_rng(3), n, 20, 5)
+    prefix = [[sp.sot, sp.lang0, sp.transcribe]] * 4
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=every)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, d, encs, prefix, tok, par, 5, keep=range(0, n + 1, every))
+    _check_forced("micro beam5 224 steps", dt, top1, lg, every, ref_top1, ref_margin, ref_lg, 150)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# search parity: free-running transcribe, recorded, replayed by the oracle
+# ---------------------------------------------------------------------------------------------------------------
+def _replay_and_compare(tag, ctx, res, K, opt, sp, min_steps):
+    lg, sel = ctx.recorded()
+    info = O.search_replay(lg, sel, K, sp, opt, eps=EPS_TIE)
+    steps = []
+    for b, (r, inf) in enumerate(zip(res, info)):
+        assert inf["mismatch"] is None, (tag, b, inf["mismatch"])
+        steps.append(inf["steps"])
+        if inf["ties"]:
+            continue
+        if K == 1:
+            ref = inf["finished"][0][0] if inf["finished"] else inf["alive"][0][0]
+            assert r.tokens == ref, (tag, b, r.tokens, ref)
+        else:
+            toks, sc, margin = O.rank_final(inf["finished"], inf["alive"], K)
+            if margin > EPS_TIE:
+                assert r.tokens == toks, (tag, b, r.tokens, toks)
+                assert abs(r.sum_logprob - sc) <= 1e-3 * max(1.0, abs(sc)), (tag, b, r.sum_logprob, sc)
+    ties = sum(i["ties"] for i in info)
+    ran = [int((sel[:, b * K, 0] >= 0).sum()) for b in range(len(res))]  # steps the device searched per window
+    print(f"{tag}: recorded {lg.shape[0]} steps x {lg.shape[1]} rows; replayed steps per window {steps} "
+          f"(device ran {ran}); windows ended by a float tie {ties}")
+    short = [b for b in range(len(res)) if not info[b]["ties"] and steps[b] < min(min_steps, ran[b])]
+    assert not short, (short, steps, ran)
+    return info
+
+
+def test_search_replay_wide_greedy_20windows(wide20):
+    from wmx import engine as E
+    dt, m, W, mels, encs = wide20
+    sp = O.special_tokens(WIDE2.n_vocab)
+    audios = [synth.speech_like(100 + i, n) for i, n in enumerate([480000, 150000, 320000, 16000, 240000] * 4)]
+    ctx = E.Context(m, max_batch=20, beam_size=1, max_new_tokens=32, word_timestamps=False)
+    ctx.record(33)
+    res = ctx.transcribe(audios)
+    langs = {r.language for r in res}
+    for b in (0, 3):  # language detection vs the oracle (the replay starts after it)
+        assert res[b].language == O.detect_language(W, WIDE2, encs[b])[0]
+    opt = O.DecodeOptions(beam_size=1, max_new_tokens=32)
+    _replay_and_compare(f"wide greedy B=20 {dt} (langs {sorted(langs)})", ctx, res, 1, opt, sp, 16)
+
+
+def test_search_replay_wide_beam5_4windows(wide20):
+    from wmx import engine as E
+    dt, m, W, mels, encs = wide20
+    sp = O.special_tokens(WIDE2.n_vocab)
+    audios = [synth.speech_like(100 + i, n) for i, n in enumerate([480000, 150000, 320000, 16000])]
+    ctx = E.Context(m, max_batch=4, beam_size=5, max_new_tokens=32, word_timestamps=False, language=sp.lang0)
+    ctx.record(33)
+    res = ctx.transcribe(audios, prompts=[[], [1000, 1001, 1002], [2000 + i for i in range(9)], [5]])
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=5, max_new_tokens=32)
+    _replay_and_compare(f"wide beam5 B=4 prompted {dt}", ctx, res, 5, opt, sp, 16)
+
+
+@pytest.mark.parametrize("K", [1, 5])
+def test_search_replay_micro_224_steps(K):
+    """The whole 224-step decode of the bench's max_new_tokens, greedy and beam 5, replayed exactly."""
+    from wmx import engine as E
+    d = O.DIMS["micro"]
+    sp = O.special_tokens(d.n_vocab)
+    m = E.Model("micro", 0, "bfloat16").init_synthetic(1)
+    ctx = E.Context(m, max_batch=2, beam_size=K, max_new_tokens=224, word_timestamps=False, language=sp.lang0)
+    ctx.record(224)
+    res = ctx.transcribe([synth.speech_like(301, 480000), synth.speech_like(302, 200000)])
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=K, max_new_tokens=224)
+    _replay_and_compare(f"micro K={K} 224 steps", ctx, res, K, opt, sp, 100)
+    ctx.record(0)
+
+
+def test_recorder_off_keeps_results():
+    """The recorder's launches change nothing: same tokens with it on and off (graph re-captured each way)."""
+    from wmx import engine as E
+    m = E.Model("micro", 0, "bfloat16").init_synthetic(1)
+    ctx = E.Context(m, max_batch=2, beam_size=5, max_new_tokens=40, word_timestamps=True)
+    audios = [synth.speech_like(401, 300000), synth.speech_like(402, 100000)]
+    a = ctx.transcribe(audios)
+    ctx.record(40)
+    b = ctx.transcribe(audios)
+    ctx.record(0)
+    c = ctx.transcribe(audios)
+    for x, y, z in zip(a, b, c):
+        assert x.tokens == y.tokens == z.tokens
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# full depth: the real large-v3 (32 + 32 layers), one window
+# ---------------------------------------------------------------------------------------------------------------
+def test_full_depth_large_v3_one_window():
+    """Encoder rel-L2 over all 32 layers and 8 forced decode steps through all 32 decoder layers (bf16), plus the
+    first free-running greedy steps replayed exactly."""
+    from wmx import engine as E
+    d = O.DIMS["large-v3"]
+    sp = O.special_tokens(d.n_vocab)
+    dt = "bf16"
+    m = E.Model("large-v3", 0, DT[dt]).init_synthetic(1)
+    # the oracle reads the device's weights back (bit-exact with O.make_weights: test_weights_bit_exact; the numpy
+    # PRNG over 1.55 B parameters would take a minute), as bench.py's cpu_baseline does
+    W = {name: m.get_tensor(name, shape) for name, shape, _, _ in O.tensor_specs(d)}
+    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
+    ref_small = O.make_weights(O.Dims(128, 51866, 1280, 20, 1, 1280, 20, 1), 1, dt)
+    np.testing.assert_array_equal(W["encoder.layers.0.fc1.weight"], ref_small["encoder.layers.0.fc1.weight"])
+    audio = synth.speech_like(501, 480000)
+    mel = O.logmel_segment(audio, d.n_mels)
+    enc = O.encoder(W, d, mel)
+    ctx = E.Context(m, max_batch=1, beam_size=1, max_new_tokens=8, word_timestamps=False, language=sp.lang0)
+    got = ctx.encode(mel[None])[0]
+    e = rel_l2(got, enc)
+    print("large-v3 full-depth encoder rel_l2", e)
+    assert e <= REL[dt], e
+    n = 8
+    tok, par = _forced_stream(np.random.default_rng(4), n, 1, 1)
+    prefix = [[sp.sot, sp.lang0, sp.transcribe]]
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, d, [enc], prefix, tok, par, 1)
+    _check_forced("large-v3 full depth", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 0)
+    ctx.record(8)
+    res = ctx.transcribe([audio])
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=1, max_new_tokens=8)
+    _replay_and_compare("large-v3 full depth greedy", ctx, res, 1, opt, sp, 1)
+
+
+def test_control_tokens_suppressed_with_boosted_logits():
+    """faster-whisper / openai always suppress the task / sot / prev / lm / no_speech ids (tokenizer.suppressed_tokens).
+    Their embedding rows are boosted so they would win every step; with the adapter's suppress list they are never
+    chosen (and the replay checks the device's mask step by step); without it they are (so the test has teeth)."""
+    from wmx import engine as E
+    from wmx.tokenizer import SpecialTokens, suppressed_tokens
+    d = O.DIMS["micro"]
+    sp = O.special_tokens(d.n_vocab)
+    ctrl = [sp.transcribe, sp.translate, sp.sot, sp.sot_prev, sp.sot_lm, sp.no_speech]
+    m = E.Model("micro", 0, "bfloat16").init_synthetic(1)
+    emb = m.get_tensor("decoder.embed_tokens.weight", (d.n_vocab, d.n_text_state))
+    emb[ctrl] *= 40.0
+    m.set_tensor("decoder.embed_tokens.weight", emb)
+    sup = suppressed_tokens(SpecialTokens(d.n_vocab))
+    assert set(ctrl) <= set(sup)
+    audios = [synth.speech_like(601, 240000), synth.speech_like(602, 90000)]
+    for K in (1, 5):
+        ctx = E.Context(m, max_batch=2, beam_size=K, max_new_tokens=24, word_timestamps=False, language=sp.lang0,
+                        suppress_tokens=sup)
+        ctx.record(24)
+        res = ctx.transcribe(audios)
+        for r in res:
+            assert not set(r.tokens) & set(ctrl), r.tokens
+        opt = O.DecodeOptions(language=sp.lang0, beam_size=K, max_new_tokens=24, suppress_tokens=tuple(sup))
+        _replay_and_compare(f"suppressed control tokens K={K}", ctx, res, K, opt, sp, 16)
+        bare = E.Context(m, max_batch=2, beam_size=K, max_new_tokens=24, word_timestamps=False, language=sp.lang0)
+        assert any(set(r.tokens) & set(ctrl) for r in bare.transcribe(audios))
