@@ -197,6 +197,13 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float*
 wmx_status wmx_ctx_record(wmx_ctx* c, int max_steps);
 wmx_status wmx_ctx_recorded(wmx_ctx* c, float* logits, int32_t* sel, int* n_steps, int* rows);
 
+/* host-only check of the decode GEMM's addressing (no GPU needed; tests only): for a packed-weight launch of
+ * M rows x N columns x K (lda = A's row stride), split = 0 as the epilogue launches (S = 1) or 1 as the split-K
+ * partial launches with a part_cap-element partial buffer, out9 = {S, MT, NCT, NW, KU, weight elements touched
+ * (end offset), A elements touched (end offset), partial elements written (end offset), k-steps loaded outside the
+ * wave's slice}, computed by walking the launch through the kernel's own index helpers (wmx_kernels.h). */
+wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int split, int64_t lda, int64_t* out9);
+
 /* ---- pre-ASR DSP of the microphone loop, batched over B streams ----
  * band-pass "vocal separation" (reference vocal_separation.py:335-358, SimpleFilterSeparator.separate):
  * y = scipy.signal.filtfilt(b, a, x) with the caller's normalised coefficients (a[0] = 1, ntaps = len(b) = len(a)

@@ -1235,11 +1235,16 @@ __device__ __forceinline__ void packed_red_tail(const RedTail& rt, const float* 
 // fragments + MT activation fragments) before their MFMAs, partial tiles are summed through LDS.
 // Grid (col groups, S, row chunks).  S == 1: epilogue; S > 1: raw fp32 partials part[s][M][N].
 // ------------------------------------------------------------------------------------------------
+template <int MT, int NCT>
+constexpr int packed_ku() {
+  return (MT + NCT) <= 8 ? 2 : 1;
+}
+
 template <DT T, int MT, int NCT, int NW, bool TAIL>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
                                                               int S, Epi e, float* __restrict__ part, RedTail rt) {
-  constexpr int KU = (MT + NCT) <= 8 ? 2 : 1;
+  constexpr int KU = packed_ku<MT, NCT>();
   constexpr int LDR = 16 * NCT + 1;
   constexpr int NT = 64 * NW;
   __shared__ float red[NW][MT * 16][LDR];
@@ -1250,10 +1255,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   const int sp = blockIdx.y;
   const int m0 = blockIdx.z * MT * 16;
   const int ksteps = K >> 5;
-  const int kps = (ksteps + S - 1) / S;
-  const int kb = sp * kps, ke = min(ksteps, kb + kps);
-  const int per = (max(0, ke - kb) + NW - 1) / NW;
-  const int ks0 = kb + wave * per, ks1 = min(ke, ks0 + per);
+  int ks0, ks1;
+  packed_wave_ksteps(K, S, NW, sp, wave, ks0, ks1);
   f32x4 acc[MT][NCT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -1261,11 +1264,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     for (int j = 0; j < NCT; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
   const uint16_t* wt[NCT];
 #pragma unroll
-  for (int j = 0; j < NCT; ++j) wt[j] = Wp + ((long)min(t0 + j, ntiles - 1) * ksteps << 9) + lane * 8;
+  for (int j = 0; j < NCT; ++j) wt[j] = Wp + packed_w_elem(t0 + j, ntiles, ksteps, 0, lane);
   // rows >= M are clamped to M-1: they only feed output rows that are never stored
   const uint16_t* ar[MT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) ar[i] = A + (long)min(m0 + i * 16 + fr, M - 1) * lda + 8 * fq;
+  for (int i = 0; i < MT; ++i) ar[i] = A + packed_a_elem(m0 + i * 16 + fr, M, lda, 0, lane);
   for (int kk = ks0; kk < ks1; kk += KU) {
     u16x8 b[KU][NCT], av[KU][MT];
 #pragma unroll
@@ -1354,13 +1357,24 @@ int packed_splits(int M, int N, int K, long cap_elems) {
 
 // waves per workgroup: enough that each wave's share of its K slice is at most ~4 k-steps (two dependent load
 // batches), so long unsplit slices (fc1, whose GELU epilogue needs S = 1) are not a chain of five round trips
+template <int MT, int NCT>
+static int packed_nw(int K, int S) {
+  const int ksteps = K / 32, kps = (ksteps + S - 1) / S;
+  const int per4 = (kps + 3) / 4;
+  static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
+  // the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] stays within 80 KiB of LDS (two workgroups per CU)
+  constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
+  constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
+  if (only4 || per4 <= 4 || !fit8) return 4;
+  if (per4 <= 8 || !fit16) return 8;
+  return 16;
+}
+
 template <DT T, int MT, int NCT>
 static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ntiles = (g.N + 15) / 16;
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
-  const int ksteps = g.K / 32, kps = (ksteps + g.S - 1) / g.S;
-  const int per4 = (kps + 3) / 4;
-  static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
+  const int nw = packed_nw<MT, NCT>(g.K, g.S);
   const bool tail = g.tail.cnt != nullptr;
 #define WMX_PACKED_LAUNCH(NWV)                                                                                     \
   do {                                                                                                             \
@@ -1371,17 +1385,74 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
       hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, false>), grid, dim3(64 * NWV), 0, st, g.A, g.lda,    \
                          g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail);                                          \
   } while (0)
-  // the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] stays within 80 KiB of LDS (two workgroups per CU)
   constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
   constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
-  if (only4 || per4 <= 4 || !fit8) {
+  if (nw == 4) {
     WMX_PACKED_LAUNCH(4);
-  } else if (per4 <= 8 || !fit16) {
+  } else if (nw == 8) {
     if constexpr (fit8) WMX_PACKED_LAUNCH(8);
   } else {
     if constexpr (fit16) WMX_PACKED_LAUNCH(16);
   }
 #undef WMX_PACKED_LAUNCH
+}
+
+template <int MT, int NCT>
+static PackedPlan plan_cfg(int M, int N, int K, int S) {
+  return PackedPlan{MT, NCT, packed_nw<MT, NCT>(K, S), packed_ku<MT, NCT>(), ((N + 15) / 16 + NCT - 1) / NCT,
+                    (M + MT * 16 - 1) / (MT * 16)};
+}
+
+template <int NCT>
+static PackedPlan plan_mt(int M, int N, int K, int S) {
+  switch ((std::min(M, 128) + 15) / 16) {  // launch_packed_mt's dispatch
+    case 1: return plan_cfg<1, NCT>(M, N, K, S);
+    case 2: return plan_cfg<2, NCT>(M, N, K, S);
+    case 3: return plan_cfg<3, NCT>(M, N, K, S);
+    case 4: return plan_cfg<4, NCT>(M, N, K, S);
+    case 5:
+    case 6: return plan_cfg<6, 2>(M, N, K, S);
+    default: return plan_cfg<4, 2>(M, N, K, S);
+  }
+}
+
+PackedPlan packed_plan(int M, int N, int K, int S) {
+  return packed_nct(M, N, K) == 4 ? plan_mt<4>(M, N, K, S) : plan_mt<2>(M, N, K, S);
+}
+
+// walks every lane of every wave of every workgroup of the launch through the kernel's own index helpers
+PackedExtent packed_extent(int M, int N, int K, int S, long lda) {
+  const PackedPlan p = packed_plan(M, N, K, S);
+  const int ntiles = (N + 15) / 16, ksteps = K / 32;
+  PackedExtent e{0, 0, 0, 0};
+  for (int bx = 0; bx < p.gx; ++bx)
+    for (int sp = 0; sp < S; ++sp)
+      for (int bz = 0; bz < p.gz; ++bz)
+        for (int wave = 0; wave < p.NW; ++wave) {
+          int ks0, ks1;
+          packed_wave_ksteps(K, S, p.NW, sp, wave, ks0, ks1);
+          for (int kk = ks0; kk < ks1; kk += p.KU)
+            for (int u = 0; u < p.KU; ++u) {
+              const int k = kk + u;
+              if (!(k < ks1)) continue;  // the kernel's load guard
+              if (k < 0 || k >= ksteps) ++e.stray_ksteps;
+              // both offsets grow with the lane index (lane * 8; row lane & 15 and column 8 * (lane >> 4)), so
+              // lane 63 bounds the wave
+              for (int lane = 63; lane < 64; lane += 1) {
+                for (int j = 0; j < p.NCT; ++j)
+                  e.w_end = std::max(e.w_end, packed_w_elem(bx * p.NCT + j, ntiles, ksteps, k, lane) + 8);
+                for (int i = 0; i < p.MT; ++i)
+                  e.a_end = std::max(e.a_end, packed_a_elem(bz * p.MT * 16 + i * 16 + (lane & 15), M, lda, k, lane) + 8);
+              }
+            }
+          if (S > 1)  // partial stores: rows < M, column quads < N
+            for (int row = 0; row < p.MT * 16; ++row)
+              for (int c = 0; c < 16 * p.NCT; c += 4) {
+                const int m = bz * p.MT * 16 + row, n = bx * p.NCT * 16 + c;
+                if (m < M && n < N) e.part_end = std::max(e.part_end, ((long)sp * M + m) * N + std::min(n + 4, N));
+              }
+        }
+  return e;
 }
 
 template <DT T, int NCT>

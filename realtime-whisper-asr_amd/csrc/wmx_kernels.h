@@ -128,6 +128,35 @@ struct PackedCall {
   RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
 };
 void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st);
+// the launch geometry launch_gemm_packed chooses: MT 16-row fragments x NCT 16-column tiles per workgroup, NW waves,
+// KU k-steps of loads per batch; grid (gx column groups, S slices, gz row chunks)
+struct PackedPlan {
+  int MT, NCT, NW, KU, gx, gz;
+};
+PackedPlan packed_plan(int M, int N, int K, int S);
+// the element offsets a packed-GEMM lane reads, shared by gemm_packed_kernel and the host-side extent check
+// (packed_extent): k-step range of one wave, the B fragment of column tile t (clamped to the last tile) and the A
+// fragment of row `row` (clamped to the last row)
+__host__ __device__ inline void packed_wave_ksteps(int K, int S, int NW, int sp, int wave, int& ks0, int& ks1) {
+  const int ksteps = K >> 5;
+  const int kps = (ksteps + S - 1) / S;
+  const int kb = sp * kps, ke = min(ksteps, kb + kps);
+  const int per = (max(0, ke - kb) + NW - 1) / NW;
+  ks0 = kb + wave * per;
+  ks1 = min(ke, ks0 + per);
+}
+__host__ __device__ inline long packed_w_elem(int t, int ntiles, int ksteps, int kstep, int lane) {
+  return ((long)min(t, ntiles - 1) * ksteps << 9) + ((long)kstep << 9) + lane * 8;
+}
+__host__ __device__ inline long packed_a_elem(int row, int M, long lda, int kstep, int lane) {
+  return (long)min(row, M - 1) * lda + 8 * (lane >> 4) + kstep * 32;
+}
+// max element offsets + 1 a launch of this shape touches: B fragments (weights), A fragments, and (S > 1) the
+// fp32 partials part[s][M][N]; the k-steps any wave loads beyond its slice (must be 0)
+struct PackedExtent {
+  long w_end, a_end, part_end, stray_ksteps;
+};
+PackedExtent packed_extent(int M, int N, int K, int S, long lda);
 // whether a partial-output launch of this shape can carry the RedTail; counters the tail needs
 bool packed_tail_ok(int M, int N, int K, int S);
 constexpr int packed_tail_counters() { return 4096; }

@@ -2091,6 +2091,22 @@ wmx_status wmx_ctx_forced_decode(wmx_ctx* x, const int32_t* prefix, const int32_
   });
 }
 
+wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int split, int64_t lda, int64_t* out9) {
+  return guard([&] {
+    WMX_CHECK(out9 && M >= 1 && N >= 1 && K >= 32 && K % 32 == 0, "debug_packed_launch: arguments");
+    // the split count the runtime's callers use: gemm_p (S = 1, epilogue) or gemm_p_part (partials, S >= 2)
+    int S = 1;
+    if (split) {
+      S = packed_splits(M, N, K, part_cap);
+      if (S == 1) S = 2;
+    }
+    const PackedPlan p = packed_plan(M, N, K, S);
+    const PackedExtent e = packed_extent(M, N, K, S, lda);
+    const int64_t v[9] = {S, p.MT, p.NCT, p.NW, p.KU, e.w_end, e.a_end, e.part_end, e.stray_ksteps};
+    std::memcpy(out9, v, sizeof(v));
+  });
+}
+
 wmx_status wmx_ctx_record(wmx_ctx* x, int max_steps) {
   return guard([&] {
     Ctx& c = x->c;
