@@ -71,8 +71,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU rehearsal of the launch / rendezvous / broadcast / max-over-ranks plumbing (gloo, no GPU)")
-    p.add_argument("--roofline-kernel", default="auto",
-                   choices=["auto", "cross_attn", "enc_fc1", "enc_attn", "logmel", "dec_fc1", "self_attn"])
+    p.add_argument("--no-stream", action="store_true", help="skip the per-stream process_iter latency lines")
     return p.parse_args()
 
 
@@ -83,50 +82,112 @@ class _ArenaView:
         self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}
 
 
-def cpu_baseline(model, args, steps_done):
-    """The oracle (numpy fp32 restatement, oracle/whisper_np.py) timed on this host on a bounded sample:
-    one 30 s window: log-mel + encoder + language detection + prompt prefill + 4 beam decode steps; the per-step
-    time is extrapolated to the same number of decode steps the GPU run executed."""
+def _cpu_sample(W, d, args, steps_done, n_text):
+    """One bounded sample of the oracle on this host: one 30 s window, log-mel + encoder + language detection +
+    prompt prefill + 4 beam decode steps (per-step time extrapolated to the GPU run's step count) + the word
+    alignment pass (alignment forward over n_text tokens + DTW).  Returns (seconds per window, stage log)."""
     from oracle import whisper_np as O
     from wmx import synth
-
-    d = O.DIMS[args.model] if args.model in O.DIMS else None
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    t0 = time.perf_counter()
-    W = {}
-    for name, shape, _, _ in O.tensor_specs(d):
-        W[name] = model.get_tensor(name, shape)
-    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
-    t_load = time.perf_counter() - t0
     audio = synth.speech_like(10_000, 480000)
+    tm = {}
     t = time.perf_counter()
     mel = O.logmel_segment(audio, d.n_mels)
-    t_mel = time.perf_counter() - t
+    tm["mel"] = time.perf_counter() - t
     t = time.perf_counter()
     enc = O.encoder(W, d, mel)
-    t_enc = time.perf_counter() - t
+    tm["enc"] = time.perf_counter() - t
     t = time.perf_counter()
     lang, _ = O.detect_language(W, d, enc)
-    t_lang = time.perf_counter() - t
+    tm["lang"] = time.perf_counter() - t
     sp = O.special_tokens(d.n_vocab)
     t = time.perf_counter()
     cache = O.DecoderCache(W, d, enc)
     O.decoder_forward(W, d, O.sot_sequence(sp, lang, "transcribe"), cache)
-    t_pre = time.perf_counter() - t
+    tm["prefill"] = time.perf_counter() - t
     caches = [cache.copy() for _ in range(args.beam)]
     n_dec = 4
     t = time.perf_counter()
     for s in range(n_dec):
         for c in caches:
             O.decoder_forward(W, d, [sp.timestamp_begin + s], c)
-    t_step = (time.perf_counter() - t) / n_dec
-    total = t_mel + t_enc + t_lang + t_pre + t_step * max(steps_done, 1)
-    log(f"[cpu] load {t_load:.1f}s mel {t_mel:.3f}s enc {t_enc:.2f}s lang {t_lang:.2f}s prefill {t_pre:.2f}s "
-        f"step {t_step:.3f}s x {steps_done} -> {total:.1f}s per 30 s window")
-    return {"value": round(30.0 / total, 4), "unit": "x_realtime", "cores": cores, "kind": "port",
-            "sample": f"1 x 30 s window of {args.model} (numpy fp32 oracle): log-mel + encoder + language detect + "
-                      f"prefill + {n_dec} beam-{args.beam} decode steps timed, per-step time extrapolated to "
-                      f"{steps_done} steps; word alignment not included"}
+    tm["step"] = (time.perf_counter() - t) / n_dec
+    t = time.perf_counter()
+    O.find_alignment(W, d, enc, lang, "transcribe", [1000 + (i % 5000) for i in range(n_text)], 3000)
+    tm["align"] = time.perf_counter() - t
+    total = tm["mel"] + tm["enc"] + tm["lang"] + tm["prefill"] + tm["step"] * max(steps_done, 1) + tm["align"]
+    return total, tm
+
+
+def cpu_baseline(model, args, steps_done, n_text):
+    """The oracle (numpy fp32 restatement, oracle/whisper_np.py) timed on this host's cores as the proxy for the
+    reference CPU path (faster-whisper / CT2 int8 is not installed: SURVEY §8d), at CT2's default 4 intra-op
+    threads and at every core of the affinity mask (BLAS threads set with threadpoolctl)."""
+    from oracle import whisper_np as O
+    from threadpoolctl import threadpool_limits
+
+    d = O.DIMS[args.model] if args.model in O.DIMS else None
+    cores = len(os.sched_getaffinity(0))
+    t0 = time.perf_counter()
+    W = {}
+    for name, shape, _, _ in O.tensor_specs(d):
+        W[name] = model.get_tensor(name, shape)
+    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
+    log(f"[cpu] weights read back in {time.perf_counter() - t0:.1f}s")
+    out = {}
+    for threads in (4, cores):
+        with threadpool_limits(limits=threads):
+            total, tm = _cpu_sample(W, d, args, steps_done, n_text)
+        log(f"[cpu] {threads} threads: " + " ".join(f"{k} {v:.3f}s" for k, v in tm.items()) +
+            f" (step x {steps_done}) -> {total:.1f}s per 30 s window")
+        out[threads] = (total, tm)
+    total4 = out[4][0]
+    totalc = out[cores][0]
+    return {"value": round(30.0 / total4, 4), "unit": "x_realtime", "cores": 4, "kind": "proxy",
+            "all_cores": {"value": round(30.0 / totalc, 4), "cores": cores},
+            "sample": f"1 x 30 s window of {args.model} through the numpy fp32 oracle (faster-whisper/CT2 absent: "
+                      f"proxy): log-mel + encoder + language detect + prefill + 4 beam-{args.beam} decode steps "
+                      f"(per-step time extrapolated to the GPU run's {steps_done} steps) + word alignment over "
+                      f"{n_text} tokens; value at 4 BLAS threads (CT2's default), all_cores at {cores}"}
+
+
+def stream_latency(name, dtype, seconds, cadence_s, max_new_tokens, vac):
+    """Per-stream p50 of one process_iter -> transcribe call, through the drop-in adapter and the
+    streaming processors: `vac` = config 2 (DynamicVACOnlineASRProcessor, 1 s online chunks, 640-sample feed,
+    scripted VAD track), else EnhancedOnlineASRProcessor with process_iter every `cadence_s` (一键.py:1510)."""
+    from wmx import synth
+    from wmx.asr import MI355XWhisperASR
+    from wmx.online import DynamicVACOnlineASRProcessor, EnhancedOnlineASRProcessor, ScriptedVAD
+    asr = MI355XWhisperASR(lan="auto", modelsize=name, device="cuda", compute_type=dtype,
+                           transcribe_kwargs={"beam_size": 5}, max_new_tokens=max_new_tokens)
+    lat = []
+    inner = asr.transcribe
+
+    def timed(audio, init_prompt=""):
+        t0 = time.perf_counter()
+        out = inner(audio, init_prompt=init_prompt)
+        lat.append(time.perf_counter() - t0)
+        return out
+
+    asr.transcribe = timed
+    audio = synth.speech_like(77, int(seconds * 16000))
+    if vac:
+        n_win = len(audio) // 512
+        proc = DynamicVACOnlineASRProcessor(1.0, asr, vad_model=ScriptedVAD([0.0] * 30 + [0.95] * (n_win - 30)))
+        feed, every = 640, 1
+    else:
+        proc = EnhancedOnlineASRProcessor(asr, buffer_trimming=("segment", 15), agreement_n=3)
+        feed, every = int(cadence_s * 16000), 1
+    for i in range(0, len(audio), feed):
+        proc.insert_audio_chunk(audio[i: i + feed])
+        if (i // feed) % every == 0:
+            proc.process_iter()
+    lat = lat[1:] if len(lat) > 2 else lat  # the first call captures the decode graph
+    return {"model": f"whisper-{name}", "dtype": dtype, "calls": len(lat),
+            "p50_ms": round(1000 * float(np.median(lat)), 2) if lat else None,
+            "p90_ms": round(1000 * float(np.percentile(lat, 90)), 2) if lat else None,
+            "feed": "VAC, 640-sample chunks, 1 s online chunks, scripted VAD" if vac else
+                    f"process_iter every {cadence_s} s", "audio_s": seconds,
+            "max_new_tokens": max_new_tokens, "beam": 5}
 
 
 def dry_run(args):
@@ -246,10 +307,11 @@ def main():
             out.extend(f.result())
         return out
 
-    # in-situ probe: HIP events captured into each context's decode-step graph around the cross-attention launch
-    # of the middle decoder layer, sampled once per 8-step replay chunk during the timed decode loops
+    # in-situ probes captured into each context's decode-step graph: device-clock start / end of the six packed
+    # projection GEMMs and the cross attention of the middle decoder layer, at every step of the timed decode loops
+    probe_layer = model.dims.n_text_layer // 2
     for c in ctxs:
-        c.set_probe("cross_attn", model.dims.n_text_layer // 2)
+        c.set_probe(True, probe_layer)
     for _ in range(args.warmup):
         step()
     if dist is not None:
@@ -279,54 +341,60 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     p50 = 1000.0 * float(np.median(lat))
 
-    # roofline of the dominant kernel, measured live with HIP events on the context stream
-    per_step_ms = {}
-    kern_stats = {}
-    R = B * args.beam
-    counts = {  # launches per transcribe step (each context group launches its own, over Bg windows)
-        "cross_attn": G * steps_done * model.dims.n_text_layer,
-        "self_attn": G * steps_done * model.dims.n_text_layer,
-        "dec_fc1": G * steps_done * model.dims.n_text_layer,
-        "enc_fc1": G * model.dims.n_audio_layer,
-        "enc_attn": G * model.dims.n_audio_layer,
-        "logmel": G,
-    }
-    for k in counts:
-        log(f"[rank {rank}] timing kernel {k}")
-        ms, by, fl = ctx.bench_kernel(k, Bg, iters=20)
-        kern_stats[k] = (ms, by, fl)
-        per_step_ms[k] = ms * counts[k]
-    dom = max(per_step_ms, key=per_step_ms.get) if args.roofline_kernel == "auto" else args.roofline_kernel
-    ms, by, fl = kern_stats[dom]
-    measured = "isolated replay (wmx_ctx_bench_kernel, HIP events, 20 launches)"
-    if dom == "cross_attn":
-        # the in-situ launches of the timed region (all context groups running concurrently)
-        st = [c.probe_stats() for c in ctxs]
-        n = sum(x[1] for x in st)
-        if n:
-            ms = sum(x[0] * x[1] for x in st) / n
-            by = st[0][2]
-            measured = f"in-situ, timed region: {n} sampled launches (layer {model.dims.n_text_layer // 2})"
-    if dom in ("enc_fc1", "enc_attn"):
-        ach = fl / (ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None}
-    else:
-        ach = by / (ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
-    # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py) at this launch's batch
-    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01g_pmc_traffic.json")
-    if os.path.exists(pmc):
-        rec = json.load(open(pmc)).get(f"{dom}@{Bg}")
-        if rec and roof["unit"] == "GB/s":
-            roof["traffic"] = round(rec["traffic_bytes"] / 1e9 / (ms * 1e-3), 1)
-            roof["traffic_bytes_per_launch"] = rec["traffic_bytes"]
-            roof["traffic_source"] = "profiles/r01g_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
-    roof["measured"] = measured
+    # roofline of the dominant kernel family, measured in situ over the timed region (device-clock probes inside
+    # the replayed decode graphs, every step, both context groups) -- rocprofv3's top kernel is gemm_packed_kernel
+    # (the decoder projections), then the cross attention (profiles/, tools/roofline_from_profile.py)
+    agg = {}
+    for c in ctxs:
+        for k, (ms_k, n_k, by_k) in c.probe_launches().items():
+            a = agg.setdefault(k, [0.0, 0, by_k])
+            a[0] += ms_k * n_k
+            a[1] += n_k
+    launch = {k: (v[0] / v[1] if v[1] else 0.0, v[1], v[2]) for k, v in agg.items()}
+    fams = {"gemm_packed_kernel": [k for k in launch if k.startswith("dec_")], "dec_cross_attn_kernel": ["cross_attn"]}
+    fam_ms = {f: sum(launch[k][0] for k in ks) for f, ks in fams.items()}  # per layer-step, one group
+    dom = max(fam_ms, key=fam_ms.get)
+    ms = fam_ms[dom]
+    by = sum(launch[k][2] for k in fams[dom])
+    ach = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py: FETCH_SIZE x2 +
+    # WRITE_SIZE, separate passes) of the same launches replayed alone at this context's batch
+    pmc_map = {"dec_qkv": "dec_qkv", "dec_out": "dec_proj", "dec_cross_q": "dec_proj", "dec_cross_out": "dec_proj",
+               "dec_fc1": "dec_fc1", "dec_fc2": "dec_fc2", "cross_attn": "cross_attn"}
+    for tag in ("r02", "r01g"):
+        pmc = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")
+        if not os.path.exists(pmc):
+            continue
+        recs = json.load(open(pmc))
+        got = [recs.get(f"{pmc_map[k]}@{Bg}") for k in fams[dom]]
+        if all(got):
+            tb = sum(g["traffic_bytes"] for g in got)
+            roof["traffic"] = round(tb / 1e9 / (ms * 1e-3), 1)
+            roof["traffic_bytes_per_layer_step"] = tb
+            roof["traffic_source"] = f"profiles/{tag}_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
+            break
     roof["kernel"] = dom
-    roof["launch_ms"] = round(ms, 4)
-    roof["algorithmic_per_launch"] = {"bytes": by, "flops": fl}
+    roof["measured"] = (f"in-situ over the timed region: device-clock probes of layer {probe_layer}'s launches in "
+                        f"every decode step, {sum(launch[k][1] for k in fams[dom])} launch samples")
+    roof["launches"] = {k: {"us": round(1000 * launch[k][0], 2), "bytes": launch[k][2],
+                            "gbs": round(launch[k][2] / (launch[k][0] * 1e-3) / 1e9, 1) if launch[k][0] else None}
+                        for k in fams[dom]}
+    roof["algorithmic_bytes_per_layer_step"] = by
+    roof["layer_step_ms"] = round(ms, 4)
+    roof["family_ms_per_layer_step"] = {f: round(v, 4) for f, v in fam_ms.items()}
+    # the other named stages: the log-mel front end (north_star: HBM GB/s of the mel path) and the self attention,
+    # replayed alone with HIP events on the context stream
+    kern_stats = {}
+    for k in ("logmel", "self_attn", "reduce_ln"):
+        kern_stats[k] = ctx.bench_kernel(k, Bg, iters=20)
+    lm_ms, lm_by, lm_fl = kern_stats["logmel"]
+    logmel = {"windows": Bg, "us": round(1000 * lm_ms, 1), "bytes": lm_by,
+              "achieved_gbs": round(lm_by / (lm_ms * 1e-3) / 1e9, 1),
+              "frac_hbm": round(lm_by / (lm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "tflops_f32": round(lm_fl / (lm_ms * 1e-3) / 1e12, 2),
+              "note": "isolated replay, HIP events; DFT-as-GEMM on the f32 MFMA"}
     # encoder MFMA utilisation (north_star: >= 40 % in the encoder): one whole encoder pass over a context's
     # windows, isolated (HIP events), and the in-situ encoder stage of the timed region (all groups concurrent)
     e_ms, _, e_fl = ctx.bench_kernel("encoder", Bg, iters=3)
@@ -351,8 +419,9 @@ def main():
                "note": ("fp8: the projections run on the MX-fp8 MFMA (5 PF dense peak), attention and convs bf16; "
                         "utilisation quoted against the bf16 peak" if args.dtype == "fp8" else "bf16 MFMA")}
     log(f"[rank {rank}] encoder: {encoder}")
-    log(f"[rank {rank}] kernel ms/launch: " + ", ".join(f"{k}={v[0]:.4f}" for k, v in kern_stats.items()))
-    log(f"[rank {rank}] est. ms per transcribe step: " + ", ".join(f"{k}={v:.1f}" for k, v in per_step_ms.items()))
+    log(f"[rank {rank}] in-situ us/launch (layer {probe_layer}): " +
+        ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in launch.items() if v[1]))
+    log(f"[rank {rank}] replayed kernel us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in kern_stats.items()))
 
     out = {
         "metric": METRIC,
@@ -378,10 +447,23 @@ def main():
         "stage_ms": [round(s, 2) for s in stages],
         "roofline": roof,
         "encoder": encoder,
+        "logmel": logmel,
+        "self_attn_us": round(1000 * kern_stats["self_attn"][0], 2),
+        "reduce_ln_us": round(1000 * kern_stats["reduce_ln"][0], 2),
     }
+    if rank == 0 and world == 1 and not args.no_stream:
+        # per-stream p50 of process_iter -> transcribe, next to the batched call's latency above
+        out["stream_latency"] = []
+        for cfg in ((args.model, dt, 8.0, 0.5, args.max_new_tokens, False), ("base", "float16", 12.0, 1.0, 64, True)):
+            try:
+                out["stream_latency"].append(stream_latency(*cfg))
+            except Exception as e:  # reported, never the target
+                log(f"[stream] {cfg[0]} failed: {e!r}")
+        log(f"[rank {rank}] stream latency: {out['stream_latency']}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(model, args, steps_done)
+            n_text = max(1, int(np.mean([sum(t < 50257 for t in r.tokens) for r in res])))
+            out["cpu_baseline"] = cpu_baseline(model, args, steps_done, n_text)
         except Exception as e:  # the baseline is reported, never the target
             log(f"[cpu] baseline failed: {e!r}")
             out["cpu_baseline"] = None

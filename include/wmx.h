@@ -184,7 +184,9 @@ int wmx_ctx_last_steps(wmx_ctx* c);
  * the last wmx_transcribe, B windows) between two HIP events; returns the average launch duration and the
  * ALGORITHMIC bytes / flops of one launch.  kernel: 0 decoder cross-attention (one layer, decode step),
  * 1 encoder fc1 GEMM, 2 encoder self-attention (one layer), 3 log-mel (raw pass), 4 decoder fc1 GEMM (step),
- * 5 decoder self-attention (one layer, at the last decoded length), 6 the whole encoder over B windows. */
+ * 5 decoder self-attention (one layer, at the last decoded length), 6 the whole encoder over B windows,
+ * 7 / 8 / 9 decoder qkv / d x d / fc2 projection (split-K partial launch of a step), 10 reduce_ln of a d x d
+ * projection's partials (residual add + LayerNorm). */
 wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float* avg_ms, double* bytes,
                                 double* flops);
 
@@ -219,12 +221,15 @@ wmx_status wmx_filtfilt_device(wmx_ctx* c, const float* x_dev, int64_t stride, c
 wmx_status wmx_dedup_features(wmx_ctx* c, const float* x, int64_t stride, const int64_t* lens, int B, float sr,
                               float* out);
 
-/* in-situ roofline probe: the launch of `kernel` (0 = decoder cross-attention) at decoder layer `layer` records
- * its first workgroup start and last workgroup end (device wall clock, hipDeviceAttributeWallClockRate) at every
- * decode step of the timed wmx_transcribe.  kernel < 0 disables the probe.  Stats of the last transcribe:
- * average launch duration (ms), number of steps sampled, ALGORITHMIC bytes of one launch. */
+/* in-situ roofline probes: with kernel = 0, the decode-step launches of decoder layer `layer` -- the six packed
+ * projection GEMMs (0 qkv, 1 out, 2 cross-q, 3 cross-out, 4 fc1, 5 fc2) and the cross attention (6) -- record their
+ * first workgroup start and last workgroup end (device wall clock, hipDeviceAttributeWallClockRate) at every
+ * decode step of the timed wmx_transcribe; kernel < 0 disables the probes.  wmx_ctx_probe_stats: the cross
+ * attention's average launch duration (ms), steps sampled and ALGORITHMIC bytes of one launch;
+ * wmx_ctx_probe_launches: the same for all eight launch ids (avg_ms8 / bytes8 / n8 [8]; id 7 unused). */
 wmx_status wmx_ctx_set_probe(wmx_ctx* c, int kernel, int layer);
 wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
+wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* avg_ms8, double* bytes8, int* n8);
 
 #ifdef __cplusplus
 }

@@ -1243,13 +1243,18 @@ constexpr int packed_ku() {
 template <DT T, int MT, int NCT, int NW, bool TAIL>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
-                                                              int S, Epi e, float* __restrict__ part, RedTail rt) {
+                                                              int S, Epi e, float* __restrict__ part, RedTail rt,
+                                                              unsigned long long* __restrict__ tprobe,
+                                                              const int* __restrict__ pslot) {
   constexpr int KU = packed_ku<MT, NCT>();
   constexpr int LDR = 16 * NCT + 1;
   constexpr int NT = 64 * NW;
   __shared__ float red[NW][MT * 16][LDR];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
+  // in-situ probe (bench roofline): earliest workgroup start / latest workgroup end, wall-clock ticks
+  unsigned long long* probe = tprobe ? tprobe + 2 * (*pslot) : nullptr;
+  if (probe && tid == 0) atomicMin(probe, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   const int ntiles = (N + 15) >> 4;
   const int t0 = blockIdx.x * NCT;
   const int sp = blockIdx.y;
@@ -1325,6 +1330,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     }
   }
   if constexpr (TAIL) packed_red_tail<T, MT, NCT, NW>(rt, part, M, N, S, m0, t0);
+  if (probe && tid == 0) atomicMax(probe + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 static int packed_mt(int M) {
@@ -1380,10 +1386,10 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   do {                                                                                                             \
     if (tail)                                                                                                      \
       hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, true>), grid, dim3(64 * NWV), 0, st, g.A, g.lda,     \
-                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail);                                          \
+                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot);                      \
     else                                                                                                           \
       hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, false>), grid, dim3(64 * NWV), 0, st, g.A, g.lda,    \
-                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail);                                          \
+                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot);                      \
   } while (0)
   constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
   constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;

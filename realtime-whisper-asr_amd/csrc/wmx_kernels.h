@@ -126,6 +126,9 @@ struct PackedCall {
   Epi epi;
   float* part = nullptr;
   RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
+  // in-situ probe: [slot][start, end] wall-clock ticks of this launch (atomic min / max) at slot *pslot, or null
+  unsigned long long* tprobe = nullptr;
+  const int* pslot = nullptr;
 };
 void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st);
 // the launch geometry launch_gemm_packed chooses: MT 16-row fragments x NCT 16-column tiles per workgroup, NW waves,

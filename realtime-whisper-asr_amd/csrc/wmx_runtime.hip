@@ -399,6 +399,9 @@ struct ResultHolder {
   std::vector<WindowOut> data;
 };
 
+// in-situ probe launch ids (one decoder layer of a decode step)
+enum { kProbeQKV = 0, kProbeOut, kProbeCrossQ, kProbeCrossOut, kProbeFc1, kProbeFc2, kProbeCross, kProbeLaunches = 8 };
+
 struct Ctx {
   Model* m = nullptr;
   wmx_opts o{};
@@ -463,11 +466,13 @@ struct Ctx {
   size_t dsp_io_elems = 0;
   long* dsp_lens = nullptr;
   int dsp_lens_cap = 0;
-  // in-situ probe (wmx_ctx_set_probe): [slot][start, end] wall-clock ticks of the probed launch
+  // in-situ probe (wmx_ctx_set_probe): [launch][slot][start, end] wall-clock ticks of the probed launches of one
+  // decoder layer (kProbe* ids); cur_probe = the buffer of the packed-GEMM launch being issued, or null
   int probe_kernel = -1, probe_layer = 0;
   unsigned long long* probe_buf = nullptr;
-  double probe_sum_ms = 0, probe_bytes = 0, wall_khz = 0;
-  int probe_n = 0;
+  unsigned long long* cur_probe = nullptr;
+  double probe_ms[8] = {0}, probe_bytes[8] = {0}, wall_khz = 0;
+  int probe_cnt[8] = {0};
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -571,7 +576,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
   P.add(&c.red_cnt, (size_t)packed_tail_counters());
-  P.add(&c.probe_buf, (size_t)2 * T);
+  P.add(&c.probe_buf, (size_t)kProbeLaunches * 2 * T);
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
   P.add(&c.align_out, (size_t)B * T * 1500);
@@ -681,6 +686,8 @@ static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int 
   g.K = K;
   g.S = 1;
   g.epi = e;
+  g.tprobe = c.cur_probe;
+  g.pslot = c.slot;
   launch_gemm_packed(c.dt, g, c.st);
 }
 
@@ -695,6 +702,8 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
   g.K = K;
   g.S = packed_splits(M, N, K, c.part_elems);
   g.part = c.part;
+  g.tprobe = c.cur_probe;
+  g.pslot = c.slot;
   if (g.S == 1) {  // nothing to split: a single slice is still written as raw partials
     g.S = 2;
     WMX_CHECK(2L * M * N <= c.part_elems, "decode gemm: partial buffer too small");
@@ -901,11 +910,16 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
   launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, m.dec[0].ln1g, m.dec[0].ln1b, dt,
                   c.dx, c.dhb, c.st);
+  const size_t probe_stride = (size_t)2 * c.Tctx;
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
     const bool last = l + 1 == Lt;
+    const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
+    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
     // self attention: QKV partials -> (reduce, cache write, attention) -> out-proj partials -> +x, LN2
+    probe(kProbeQKV);
     int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt);
+    c.cur_probe = nullptr;
     DecAttnArgs a{};
     a.o = c.dao;
     a.R = R;
@@ -925,9 +939,12 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     a.qpart_ld = 3 * dt;
     a.qbias = L.bqkv;
     launch_self_attn(c.dt, a, c.st);
+    probe(kProbeOut);
     gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b);
     // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3
+    probe(kProbeCrossQ);
     S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
+    c.cur_probe = nullptr;
     DecAttnArgs x{};
     x.o = c.dao;
     x.R = R;
@@ -947,13 +964,17 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.qbias = L.bcq;
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
-    if (l == c.probe_layer && c.probe_kernel == 0) x.tprobe = c.probe_buf;
+    if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    probe(kProbeCrossOut);
     gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b);
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
+    probe(kProbeFc1);
     gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
+    probe(kProbeFc2);
     gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
                  last ? m.lnb : m.dec[l + 1].ln1b);
+    c.cur_probe = nullptr;
   }
 }
 
@@ -1370,23 +1391,25 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   rec(c, 5);
   // ---- decode loop: one hipGraph replay per step ----
   const int need_done = K == 1 ? R : B;
-  c.probe_sum_ms = 0;
-  c.probe_n = 0;
+  for (int k = 0; k < kProbeLaunches; ++k) {
+    c.probe_ms[k] = 0;
+    c.probe_cnt[k] = 0;
+  }
   if (c.probe_kernel >= 0) {  // start ticks = all ones (atomic min), end ticks = 0 (atomic max)
-    std::vector<unsigned long long> init((size_t)2 * T);
-    for (int i = 0; i < T; ++i) {
-      init[2 * i] = ~0ull;
-      init[2 * i + 1] = 0ull;
+    std::vector<unsigned long long> init((size_t)kProbeLaunches * 2 * T);
+    for (size_t i = 0; i < init.size(); i += 2) {
+      init[i] = ~0ull;
+      init[i + 1] = 0ull;
     }
     WMX_HIP(hipMemcpyAsync(c.probe_buf, init.data(), init.size() * 8, hipMemcpyHostToDevice, c.st));
     sync(c);
   }
-  {
-    const double dtm = m.d.n_text_state, mean_slot = 0.5 * (steps + max_new);
-    c.probe_bytes = c.probe_kernel == 0   ? (double)B * 1500 * 2 * dtm * 2 + 2.0 * R * dtm * 2
-                    : c.probe_kernel == 4 ? 4.0 * dtm * dtm * 2 + (double)R * dtm * 2 + (double)R * 4 * dtm * 2
-                    : c.probe_kernel == 5 ? (double)R * mean_slot * dtm * 2 * 2
-                                          : 0.0;
+  {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
+    const double d = m.d.n_text_state, w2 = 2.0, r = R;
+    auto proj = [&](double n, double k) { return n * k * w2 + r * k * w2 + r * n * w2; };
+    const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), proj(d, d), proj(d, d), proj(4 * d, d),
+                                      proj(d, 4 * d), (double)B * 1500 * 2 * d * w2 + 2.0 * r * d * w2, 0.0};
+    for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
   if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
   while (steps < max_new) {
@@ -1407,12 +1430,15 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   c.last_steps = steps;
   rec(c, 6);
   if (c.probe_kernel >= 0) {
-    std::vector<unsigned long long> tk((size_t)2 * T);
+    std::vector<unsigned long long> tk((size_t)kProbeLaunches * 2 * T);
     WMX_HIP(hipMemcpy(tk.data(), c.probe_buf, tk.size() * 8, hipMemcpyDeviceToHost));
-    for (int i = 0; i < T; ++i)
-      if (tk[2 * i + 1] > tk[2 * i] && tk[2 * i] != ~0ull) {
-        c.probe_sum_ms += (double)(tk[2 * i + 1] - tk[2 * i]) / c.wall_khz;
-        c.probe_n += 1;
+    for (int k = 0; k < kProbeLaunches; ++k)
+      for (int i = 0; i < T; ++i) {
+        const unsigned long long t0 = tk[((size_t)k * T + i) * 2], t1 = tk[((size_t)k * T + i) * 2 + 1];
+        if (t1 > t0 && t0 != ~0ull) {
+          c.probe_ms[k] += (double)(t1 - t0) / c.wall_khz;
+          c.probe_cnt[k] += 1;
+        }
       }
   }
 
@@ -2267,7 +2293,7 @@ wmx_status wmx_dedup_features(wmx_ctx* x, const float* xh, int64_t stride, const
 
 wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
   return guard([&] {
-    WMX_CHECK(kernel < 0 || kernel == 0, "probe: only the decoder cross-attention (0) carries a probe");
+    WMX_CHECK(kernel < 1, "probe: 0 enables the decode-step probes, < 0 disables them");
     WMX_CHECK(layer >= 0 && layer < x->c.m->d.n_text_layer, "probe: layer");
     x->c.probe_kernel = kernel;
     x->c.probe_layer = layer;
@@ -2276,10 +2302,21 @@ wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
 
 wmx_status wmx_ctx_probe_stats(wmx_ctx* x, float* avg_ms, int* n, double* bytes) {
   return guard([&] {
-    const Ctx& c = x->c;
-    *n = c.probe_n;
-    *avg_ms = c.probe_n ? (float)(c.probe_sum_ms / c.probe_n) : 0.f;
-    *bytes = c.probe_bytes;
+    Ctx& c = x->c;
+    *n = c.probe_cnt[kProbeCross];
+    *avg_ms = *n ? (float)(c.probe_ms[kProbeCross] / *n) : 0.f;
+    *bytes = c.probe_bytes[kProbeCross];
+  });
+}
+
+wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* avg_ms8, double* bytes8, int* n8) {
+  return guard([&] {
+    Ctx& c = x->c;
+    for (int k = 0; k < kProbeLaunches; ++k) {
+      n8[k] = c.probe_cnt[k];
+      avg_ms8[k] = n8[k] ? (float)(c.probe_ms[k] / n8[k]) : 0.f;
+      bytes8[k] = c.probe_bytes[k];
+    }
   });
 }
 
@@ -2380,6 +2417,23 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
                 La * (2.0 * T * da * 3 * da + 4.0 * Ha * T * T * 64 + 2.0 * T * da * da + 4.0 * T * da * 4 * da));
       by = (double)La * 12 * da * da * 2;
       fn = [&c, B] { encode(c, B); };
+    } else if (kernel >= 7 && kernel <= 9) {
+      // decode-step projections on packed weights, split-K partial launches: 7 qkv, 8 a d x d projection, 9 fc2
+      const int N = kernel == 7 ? 3 * dt : dt, K = kernel == 9 ? 4 * dt : dt;
+      const uint16_t* W = kernel == 7 ? m.dec[0].wqkv : kernel == 8 ? m.dec[0].wo : m.dec[0].wfc2;
+      const uint16_t* A = kernel == 9 ? c.df1 : c.dhb;
+      by = (double)N * K * 2 + (double)R * K * 2 + (double)R * N * 2;
+      fl = 2.0 * R * N * K;
+      fn = [&c, A, W, R, N, K] { gemm_p_part(c, A, K, W, R, N, K); };
+    } else if (kernel == 10) {
+      // reduce_ln after a d x d projection: x += bias + sum of its split-K partials; LN(x) -> 16-bit
+      const int S = packed_splits(R, dt, dt, c.part_elems);
+      const int S2 = S == 1 ? 2 : S;
+      by = (double)S2 * R * dt * 4 + 2.0 * R * dt * 4 + (double)R * dt * 2;
+      fl = 0;
+      fn = [&c, &m, S2, R, dt] {
+        launch_reduce_ln(c.dt, c.part, S2, m.dec[0].bo, c.dx, m.dec[0].ln2g, m.dec[0].ln2b, c.dhb, R, dt, c.st);
+      };
     } else {
       WMX_CHECK(false, "bench_kernel: unknown kernel");
     }

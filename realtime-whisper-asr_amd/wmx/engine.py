@@ -307,13 +307,24 @@ class Context:
     def last_steps(self) -> int:
         return int(lib.wmx_ctx_last_steps(self._h))
 
-    KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5, "encoder": 6}
+    KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5, "encoder": 6,
+               "dec_qkv": 7, "dec_proj": 8, "dec_fc2": 9, "reduce_ln": 10}
 
-    def set_probe(self, kernel: str | None, layer: int = 0):
-        """Capture HIP events around one decode-step launch of `kernel` (cross_attn, dec_fc1, self_attn) at decoder
-        layer `layer`; every transcribe then samples that launch once per replay chunk inside its decode loop."""
-        k = -1 if kernel is None else self.KERNELS[kernel]
-        check(lib.wmx_ctx_set_probe(self._h, k, layer))
+    PROBE_LAUNCHES = ("dec_qkv", "dec_out", "dec_cross_q", "dec_cross_out", "dec_fc1", "dec_fc2", "cross_attn")
+
+    def set_probe(self, on: bool, layer: int = 0):
+        """In-situ probes on the decode-step launches of decoder layer `layer` (the six packed projection GEMMs and
+        the cross attention): every step of every following transcribe records their first-workgroup start and
+        last-workgroup end on the device clock."""
+        check(lib.wmx_ctx_set_probe(self._h, 0 if on else -1, layer))
+
+    def probe_launches(self) -> dict:
+        """{launch: (average in-situ duration ms, samples, algorithmic bytes of one launch)} of the last transcribe."""
+        ms = np.zeros(8, np.float32)
+        by = np.zeros(8, np.float64)
+        n = np.zeros(8, np.int32)
+        check(lib.wmx_ctx_probe_launches(self._h, fptr(ms), by.ctypes.data_as(C.POINTER(C.c_double)), iptr(n)))
+        return {k: (float(ms[i]), int(n[i]), float(by[i])) for i, k in enumerate(self.PROBE_LAUNCHES)}
 
     def probe_stats(self):
         """(average in-situ launch duration ms, samples, algorithmic bytes of one launch) of the last transcribe."""

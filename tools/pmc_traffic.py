@@ -24,6 +24,10 @@ MATCH = {
     "enc_fc1": "gemm256_kernel",
     "enc_attn": "enc_attn_kernel",
     "logmel": "logmel_raw_kernel",
+    "dec_qkv": "gemm_packed_kernel",
+    "dec_proj": "gemm_packed_kernel",
+    "dec_fc2": "gemm_packed_kernel",
+    "reduce_ln": "reduce_ln",
 }
 
 
