@@ -126,7 +126,9 @@ def cpu_baseline(model, args, steps_done, n_text):
     from threadpoolctl import threadpool_limits
 
     d = O.DIMS[args.model] if args.model in O.DIMS else None
-    cores = len(os.sched_getaffinity(0))
+    # the host share this process may use: the box's OMP_NUM_THREADS (its CPU share; the affinity mask lists the
+    # whole machine there), else the affinity mask
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     t0 = time.perf_counter()
     W = {}
     for name, shape, _, _ in O.tensor_specs(d):

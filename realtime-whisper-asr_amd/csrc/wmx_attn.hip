@@ -655,11 +655,10 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
   const int nq = a.rows_per_win * a.Tn;
-  // in-situ probe: earliest workgroup start / latest workgroup end of this launch, wall-clock ticks
-  unsigned long long* probe = a.tprobe ? a.tprobe + 2 * (*a.slot0) : nullptr;
-  if (probe && tid == 0) atomicMin(probe, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  // in-situ probe: this workgroup's start / end, device wall-clock ticks
+  const unsigned long long probe_t0 = (a.tprobe && tid == 0) ? probe_clock() : 0ull;
   auto probe_end = [&] {
-    if (probe && tid == 0) atomicMax(probe + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (a.tprobe && tid == 0) probe_record(a.tprobe, *a.slot0, probe_t0);
   };
   const int i0 = qt * 16;  // first query (within the window) of this tile
   const int nqt = min(16, nq - i0);

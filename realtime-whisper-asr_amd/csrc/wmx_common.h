@@ -181,4 +181,17 @@ __device__ inline float max8_lanes(float v) {
   return v;
 }
 
+// in-situ launch probe (bench roofline): every workgroup of a probed launch stores its own [start, end] device
+// wall-clock ticks at [slot][workgroup] with one plain 16-byte store (no shared counter to contend on); the host
+// takes the min start / max end over the workgroups of a slot after the timed region
+constexpr int kProbeWG = 512;
+__device__ inline unsigned long long probe_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ inline void probe_record(unsigned long long* base, int slot, unsigned long long t0) {
+  const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (wg < kProbeWG) {
+    const unsigned long long t1 = probe_clock();
+    *reinterpret_cast<ulonglong2*>(base + 2 * ((long)slot * kProbeWG + wg)) = make_ulonglong2(t0, t1);
+  }
+}
+
 }  // namespace wmx

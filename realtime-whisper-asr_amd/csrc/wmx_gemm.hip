@@ -1252,9 +1252,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   __shared__ float red[NW][MT * 16][LDR];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  // in-situ probe (bench roofline): earliest workgroup start / latest workgroup end, wall-clock ticks
-  unsigned long long* probe = tprobe ? tprobe + 2 * (*pslot) : nullptr;
-  if (probe && tid == 0) atomicMin(probe, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  // in-situ probe (bench roofline): this workgroup's start / end, device wall-clock ticks
+  const unsigned long long probe_t0 = (tprobe && tid == 0) ? probe_clock() : 0ull;
   const int ntiles = (N + 15) >> 4;
   const int t0 = blockIdx.x * NCT;
   const int sp = blockIdx.y;
@@ -1330,7 +1329,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     }
   }
   if constexpr (TAIL) packed_red_tail<T, MT, NCT, NW>(rt, part, M, N, S, m0, t0);
-  if (probe && tid == 0) atomicMax(probe + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (tprobe && tid == 0) probe_record(tprobe, *pslot, probe_t0);
 }
 
 static int packed_mt(int M) {

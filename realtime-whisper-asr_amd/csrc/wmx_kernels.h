@@ -126,7 +126,7 @@ struct PackedCall {
   Epi epi;
   float* part = nullptr;
   RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
-  // in-situ probe: [slot][start, end] wall-clock ticks of this launch (atomic min / max) at slot *pslot, or null
+  // in-situ probe: [slot][workgroup][start, end] wall-clock ticks (probe_record) at slot *pslot, or null
   unsigned long long* tprobe = nullptr;
   const int* pslot = nullptr;
 };
@@ -246,7 +246,7 @@ struct DecAttnArgs {
   int Tk;
   int rows_per_win;    // rows sharing one encoder window (beam)
   int* xcnt = nullptr; // key-chunked launches: one arrival counter per (window, head), zero between launches
-  unsigned long long* tprobe = nullptr;  // [slot][start, end] wall-clock ticks (atomic min / max), or null
+  unsigned long long* tprobe = nullptr;  // [slot][workgroup][start, end] wall-clock ticks (probe_record), or null
   // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
   // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
   const float* qpart = nullptr;

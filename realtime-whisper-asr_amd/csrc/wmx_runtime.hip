@@ -471,8 +471,8 @@ struct Ctx {
   int probe_kernel = -1, probe_layer = 0;
   unsigned long long* probe_buf = nullptr;
   unsigned long long* cur_probe = nullptr;
-  double probe_ms[8] = {0}, probe_bytes[8] = {0}, wall_khz = 0;
-  int probe_cnt[8] = {0};
+  double probe_bytes[8] = {0}, wall_khz = 0;
+  int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -576,7 +576,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
   P.add(&c.red_cnt, (size_t)packed_tail_counters());
-  P.add(&c.probe_buf, (size_t)kProbeLaunches * 2 * T);
+  P.add(&c.probe_buf, (size_t)kProbeLaunches * T * kProbeWG * 2);
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
   P.add(&c.align_out, (size_t)B * T * 1500);
@@ -910,7 +910,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
   launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, m.dec[0].ln1g, m.dec[0].ln1b, dt,
                   c.dx, c.dhb, c.st);
-  const size_t probe_stride = (size_t)2 * c.Tctx;
+  const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
     const bool last = l + 1 == Lt;
@@ -1391,19 +1391,9 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   rec(c, 5);
   // ---- decode loop: one hipGraph replay per step ----
   const int need_done = K == 1 ? R : B;
-  for (int k = 0; k < kProbeLaunches; ++k) {
-    c.probe_ms[k] = 0;
-    c.probe_cnt[k] = 0;
-  }
-  if (c.probe_kernel >= 0) {  // start ticks = all ones (atomic min), end ticks = 0 (atomic max)
-    std::vector<unsigned long long> init((size_t)kProbeLaunches * 2 * T);
-    for (size_t i = 0; i < init.size(); i += 2) {
-      init[i] = ~0ull;
-      init[i + 1] = 0ull;
-    }
-    WMX_HIP(hipMemcpyAsync(c.probe_buf, init.data(), init.size() * 8, hipMemcpyHostToDevice, c.st));
-    sync(c);
-  }
+  c.probe_slots[0] = steps > 0 ? Pmax : 0;  // slots of the graph-replayed steps of this call
+  if (c.probe_kernel >= 0)  // per-workgroup records of this call only (read after the timed region)
+    WMX_HIP(hipMemsetAsync(c.probe_buf, 0, (size_t)kProbeLaunches * T * kProbeWG * 2 * 8, c.st));
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
     const double d = m.d.n_text_state, w2 = 2.0, r = R;
     auto proj = [&](double n, double k) { return n * k * w2 + r * k * w2 + r * n * w2; };
@@ -1429,18 +1419,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   }
   c.last_steps = steps;
   rec(c, 6);
-  if (c.probe_kernel >= 0) {
-    std::vector<unsigned long long> tk((size_t)kProbeLaunches * 2 * T);
-    WMX_HIP(hipMemcpy(tk.data(), c.probe_buf, tk.size() * 8, hipMemcpyDeviceToHost));
-    for (int k = 0; k < kProbeLaunches; ++k)
-      for (int i = 0; i < T; ++i) {
-        const unsigned long long t0 = tk[((size_t)k * T + i) * 2], t1 = tk[((size_t)k * T + i) * 2 + 1];
-        if (t1 > t0 && t0 != ~0ull) {
-          c.probe_ms[k] += (double)(t1 - t0) / c.wall_khz;
-          c.probe_cnt[k] += 1;
-        }
-      }
-  }
+  c.probe_slots[1] = Pmax - 1 + steps;
 
   // ---- read back and finalise (openai BeamSearchDecoder.finalize + MaximumLikelihoodRanker) ----
   std::vector<int> h((size_t)R * T), ns(R), done(R);
@@ -2300,11 +2279,41 @@ wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
   });
 }
 
+// per probed launch id: average over the decode steps of the last transcribe of (latest workgroup end - earliest
+// workgroup start), from the per-workgroup records
+static void probe_collect(Ctx& c, double* ms, int* n) {
+  const int T = c.Tctx;
+  std::vector<unsigned long long> tk((size_t)kProbeLaunches * T * kProbeWG * 2);
+  WMX_HIP(hipStreamSynchronize(c.st));
+  WMX_HIP(hipMemcpy(tk.data(), c.probe_buf, tk.size() * 8, hipMemcpyDeviceToHost));
+  for (int k = 0; k < kProbeLaunches; ++k) {
+    ms[k] = 0;
+    n[k] = 0;
+    for (int sl = c.probe_slots[0]; sl < c.probe_slots[1] && sl < T; ++sl) {
+      unsigned long long lo = ~0ull, hi = 0;
+      const unsigned long long* r = tk.data() + ((size_t)k * T + sl) * kProbeWG * 2;
+      for (int w = 0; w < kProbeWG; ++w)
+        if (r[2 * w + 1] > r[2 * w] && r[2 * w] != 0) {
+          lo = std::min(lo, r[2 * w]);
+          hi = std::max(hi, r[2 * w + 1]);
+        }
+      if (hi > lo) {
+        ms[k] += (double)(hi - lo) / c.wall_khz;
+        n[k] += 1;
+      }
+    }
+    if (n[k]) ms[k] /= n[k];
+  }
+}
+
 wmx_status wmx_ctx_probe_stats(wmx_ctx* x, float* avg_ms, int* n, double* bytes) {
   return guard([&] {
     Ctx& c = x->c;
-    *n = c.probe_cnt[kProbeCross];
-    *avg_ms = *n ? (float)(c.probe_ms[kProbeCross] / *n) : 0.f;
+    double ms[kProbeLaunches];
+    int cnt[kProbeLaunches];
+    probe_collect(c, ms, cnt);
+    *n = cnt[kProbeCross];
+    *avg_ms = (float)ms[kProbeCross];
     *bytes = c.probe_bytes[kProbeCross];
   });
 }
@@ -2312,9 +2321,10 @@ wmx_status wmx_ctx_probe_stats(wmx_ctx* x, float* avg_ms, int* n, double* bytes)
 wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* avg_ms8, double* bytes8, int* n8) {
   return guard([&] {
     Ctx& c = x->c;
+    double ms[kProbeLaunches];
+    probe_collect(c, ms, n8);
     for (int k = 0; k < kProbeLaunches; ++k) {
-      n8[k] = c.probe_cnt[k];
-      avg_ms8[k] = n8[k] ? (float)(c.probe_ms[k] / n8[k]) : 0.f;
+      avg_ms8[k] = (float)ms[k];
       bytes8[k] = c.probe_bytes[k];
     }
   });
