@@ -505,17 +505,29 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
 
   // ---- this step's q / k / v of (row, head): from the QKV split-K partials or the stored q + cache slot ----
   if (a.qS > 0) {
+    __shared__ float2 lnrow;
+    const int part = tid >> 6, e = tid & 63;
+    const int col = part * a.d + h * 64 + e;
+    float p = 0.f;
     if (tid < 192) {
-      const int part = tid >> 6, e = tid & 63;
-      const int col = part * a.d + h * 64 + e;
       const float* src = a.qpart + (long)m * a.qpart_ld + col;
       float t[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) t[u] = u < a.qS ? src[u * a.qpart_stride] : 0.f;  // qS <= 8: one batch
-      float p = 0.f;
 #pragma unroll
       for (int u = 0; u < 8; ++u) p += t[u];
-      const uint16_t hv = from_f32<T>(p + (a.qbias ? a.qbias[col] : 0.f));
+    }
+    if (a.ln_c1) {  // LN1 folded into the QKV weights: this row's statistics, merged by the fourth wave
+      if (wave == 3) {
+        const float2 st = row_ln_from_stats(a.ln_stats + m, a.ln_ld, a.d >> 4);
+        if (lane == 0) lnrow = st;
+      }
+      __syncthreads();
+    }
+    if (tid < 192) {
+      const float val = a.ln_c1 ? lnrow.y * (p - lnrow.x * a.ln_c1[col]) + a.ln_c2[col]
+                                : p + (a.qbias ? a.qbias[col] : 0.f);
+      const uint16_t hv = from_f32<T>(val);
       const float f = to_f32<T>(hv);
       if (part == 0) {
         qs[e] = f * 0.125f;
@@ -700,6 +712,14 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   //      log2 units (softmax on exp2, no per-score scaling) ----
   constexpr float kQScale = 0.125f * 1.4426950408889634f;
   __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
+  __shared__ float2 qln[16];
+  if (a.qS > 0 && a.ln_c1) {  // LN2 folded into the cross-q weights: the tile's row statistics, one wave per row
+    for (int q = wave; q < nqt; q += NWV) {
+      const float2 st = row_ln_from_stats(a.ln_stats + (long)w * nq + i0 + q, a.ln_ld, a.d >> 4);
+      if (lane == 0) qln[q] = st;
+    }
+    __syncthreads();
+  }
   for (int t = tid; t < 16 * 64; t += NT) {
     const int q = t >> 6, e = t & 63;
     uint16_t v = 0;
@@ -714,7 +734,9 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         float p = 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u) p += tv[u];
-        v = from_f32<T>((p + (a.qbias ? a.qbias[col] : 0.f)) * kQScale);
+        const float val = a.ln_c1 ? qln[q].y * (p - qln[q].x * a.ln_c1[col]) + a.ln_c2[col]
+                                  : p + (a.qbias ? a.qbias[col] : 0.f);
+        v = from_f32<T>(val * kQScale);
       } else {
         v = from_f32<T>(to_f32<T>(a.q[row * a.q_ld + col]) * kQScale);
       }

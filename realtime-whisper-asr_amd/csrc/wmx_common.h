@@ -25,7 +25,8 @@ struct Error : std::runtime_error {
   do {                                                                                         \
     hipError_t e_ = (expr);                                                                    \
     if (e_ != hipSuccess)                                                                      \
-      throw ::wmx::Error(2, std::string(#expr) + ": " + hipGetErrorString(e_) + " @" __FILE__); \
+      throw ::wmx::Error(2, std::string(#expr) + ": " + hipGetErrorString(e_) + " @" __FILE__ ":" + \
+                         std::to_string(__LINE__));                                             \
   } while (0)
 
 #define WMX_CHECK(cond, msg)                                 \
@@ -139,6 +140,11 @@ __device__ inline float sum8_lanes(float v) {
   v += dpp_mov<kDppXor2>(v);
   return v + dpp_mov<kDppHalfMirror>(v);
 }
+// sum over each aligned group of 4 lanes
+__device__ inline float sum4_lanes(float v) {
+  v += dpp_mov<kDppXor1>(v);
+  return v + dpp_mov<kDppXor2>(v);
+}
 __device__ inline float wave_sum(float v) {
   v = sum8_lanes(v);
   v += dpp_mov<kDppMirror>(v);
@@ -153,6 +159,23 @@ __device__ inline float wave_max(float v) {
 }
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---- LayerNorm folded into the following projection (decode step) ----
+// The producer of a residual row x (embedding, an unsplit projection epilogue) stores, per aligned group of 16
+// columns g, (mean_g, M2_g = sum (x - mean_g)^2) at stats[g * ld + row].  The consumer merges the d / 16 groups
+// (Chan et al.'s pairwise update for equal counts: mean = avg mean_g, M2 = sum M2_g + 16 sum (mean_g - mean)^2,
+// i.e. sum (x - mean)^2 exactly) and applies LN through the folded weights:
+//   LN(x) W^T + bias = rstd (x W'^T - mean c1) + c2,  W' = W diag(g),  c1 = W' 1,  c2 = bias + W b.
+// One wave per row, every lane active; G = d / 16 <= 128.  Returns (mean, rstd).
+__device__ inline float2 row_ln_from_stats(const float2* __restrict__ st, long ld, int G) {
+  const int lane = threadIdx.x & 63;
+  const float2 a = lane < G ? st[lane * ld] : make_float2(0.f, 0.f);
+  const float2 b = lane + 64 < G ? st[(lane + 64) * ld] : make_float2(0.f, 0.f);
+  const float mean = wave_sum(a.x + b.x) / G;
+  const float da = lane < G ? a.x - mean : 0.f, db = lane + 64 < G ? b.x - mean : 0.f;
+  const float m2 = wave_sum((a.y + b.y) + 16.f * (da * da + db * db));
+  return make_float2(mean, 1.0f / sqrtf(m2 / (16.f * G) + 1e-5f));
+}
 
 // ---- OCP MX-fp8: e4m3 elements (OCP "fn", max 448), one e8m0 scale 2^e per 32 consecutive K elements ----
 // e = the smallest power of two with amax / 2^e <= 448, taken from the f32 bits of amax (amax = m 2^k with

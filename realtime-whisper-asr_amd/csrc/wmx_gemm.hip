@@ -1235,9 +1235,69 @@ __device__ __forceinline__ void packed_red_tail(const RedTail& rt, const float* 
 // fragments + MT activation fragments) before their MFMAs, partial tiles are summed through LDS.
 // Grid (col groups, S, row chunks).  S == 1: epilogue; S > 1: raw fp32 partials part[s][M][N].
 // ------------------------------------------------------------------------------------------------
+// k-steps per load batch.  The loads of a batch are unconditional (k-step index clamped to the wave's last one;
+// only the MFMAs are guarded): with per-step guarded loads, 4 k-steps per batch faulted with an illegal address in
+// the micro decode although every guarded address is in bounds (tests/test_packed_extent.py) -- the clamped form
+// is straight-line code.  The unsplit residual producers (MT + NCT <= 3, fc2: 10 k-steps per wave) take 5 per batch.
 template <int MT, int NCT>
 constexpr int packed_ku() {
-  return (MT + NCT) <= 8 ? 2 : 1;
+  return (MT + NCT) <= 3 ? 5 : (MT + NCT) <= 8 ? 2 : 1;
+}
+
+// S == 1 epilogues of the LayerNorm-folded decode step (wmx_common.h row_ln_from_stats): the residual producer
+// (x += acc + bias, its 16-bit copy and per-16-column statistics) and the folded-LN + GELU consumer (fc1).
+// Trip counts are whole waves (MT * 16 * 4 NCT is a multiple of 64), so the 4-lane DPP sums see every lane.
+template <DT T, int MT, int NCT, int NW>
+__device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT * 16][16 * NCT + 1], const Epi& e,
+                                                     int M, int N, int K, int m0, int t0) {
+  constexpr int NT = 64 * NW, C4 = 4 * NCT;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  __shared__ float2 rln[MT * 16];
+  const bool fold = e.kind == EPI_LNFOLD_GELU16;
+  if (fold) {
+    for (int r = wave; r < MT * 16; r += NW) {
+      const float2 st = row_ln_from_stats(e.stats + min(m0 + r, M - 1), e.stats_ld, K >> 4);
+      if ((tid & 63) == 0) rln[r] = st;
+    }
+    __syncthreads();
+  }
+  for (int idx = tid; idx < MT * 16 * C4; idx += NT) {
+    const int row = idx / C4, c = (idx - row * C4) * 4;
+    const int m = m0 + row, n = t0 * 16 + c;
+    const bool ok = m < M && n < N;
+    float v4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = red[0][row][c + q];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += red[w][row][c + q];
+      v4[q] = v;
+    }
+    if (!fold) {
+      float* xp = reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n;
+      const float4 x0 = ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 b = ok && e.bias ? *reinterpret_cast<const float4*>(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      // the order of the split-K path: x + bias + sum (reduce_ln4_kernel)
+      const float4 x = make_float4(x0.x + b.x + v4[0], x0.y + b.y + v4[1], x0.z + b.z + v4[2], x0.w + b.w + v4[3]);
+      const float mean = sum4_lanes((x.x + x.y) + (x.z + x.w)) * (1.f / 16.f);
+      const float dx = x.x - mean, dy = x.y - mean, dz = x.z - mean, dw = x.w - mean;
+      const float m2 = sum4_lanes((dx * dx + dy * dy) + (dz * dz + dw * dw));
+      if (ok) {
+        *reinterpret_cast<float4*>(xp) = x;
+        const u16x4 h = {from_f32<T>(x.x), from_f32<T>(x.y), from_f32<T>(x.z), from_f32<T>(x.w)};
+        *reinterpret_cast<u16x4*>(e.out16 + (long)m * e.ldc + n) = h;
+        if ((n & 15) == 0) e.stats[(long)(n >> 4) * e.stats_ld + m] = make_float2(mean, m2);
+      }
+    } else if (ok) {
+      const float2 ln = rln[row];
+      const float4 a = *reinterpret_cast<const float4*>(e.c1 + n), b = *reinterpret_cast<const float4*>(e.c2 + n);
+      const u16x4 h = {from_f32<T>(gelu_erf(ln.y * (v4[0] - ln.x * a.x) + b.x)),
+                       from_f32<T>(gelu_erf(ln.y * (v4[1] - ln.x * a.y) + b.y)),
+                       from_f32<T>(gelu_erf(ln.y * (v4[2] - ln.x * a.z) + b.z)),
+                       from_f32<T>(gelu_erf(ln.y * (v4[3] - ln.x * a.w) + b.w))};
+      *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
+    }
+  }
 }
 
 template <DT T, int MT, int NCT, int NW, bool TAIL>
@@ -1277,12 +1337,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     u16x8 b[KU][NCT], av[KU][MT];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
-      if (kk + u < ks1) {
+      const int k = min(kk + u, ks1 - 1);  // clamped: a duplicate load of the wave's last k-step, MFMA skipped
 #pragma unroll
-        for (int j = 0; j < NCT; ++j) b[u][j] = *reinterpret_cast<const u16x8*>(wt[j] + ((long)(kk + u) << 9));
+      for (int j = 0; j < NCT; ++j) b[u][j] = *reinterpret_cast<const u16x8*>(wt[j] + ((long)k << 9));
 #pragma unroll
-        for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + (kk + u) * 32);
-      }
+      for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + k * 32);
     }
 #pragma unroll
     for (int u = 0; u < KU; ++u)
@@ -1301,7 +1360,9 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   __syncthreads();
   // 4 consecutive columns per thread
   constexpr int C4 = 4 * NCT;  // column quads per row
-  for (int idx = tid; idx < MT * 16 * C4; idx += NT) {
+  const bool fold_epi = !TAIL && S == 1 && (e.kind == EPI_RESID_STATS || e.kind == EPI_LNFOLD_GELU16);
+  if (fold_epi) packed_fold_epilogue<T, MT, NCT, NW>(red, e, M, N, K, m0, t0);
+  for (int idx = tid; !fold_epi && idx < MT * 16 * C4; idx += NT) {
     const int row = idx / C4, c = (idx - row * C4) * 4;
     const int m = m0 + row, n = t0 * 16 + c;
     if (m >= M || n >= N) continue;
@@ -1421,13 +1482,14 @@ static PackedPlan plan_mt(int M, int N, int K, int S) {
   }
 }
 
-PackedPlan packed_plan(int M, int N, int K, int S) {
-  return packed_nct(M, N, K) == 4 ? plan_mt<4>(M, N, K, S) : plan_mt<2>(M, N, K, S);
+PackedPlan packed_plan(int M, int N, int K, int S, int nct) {
+  const int c = nct ? nct : packed_nct(M, N, K);
+  return c == 4 ? plan_mt<4>(M, N, K, S) : c == 1 ? plan_mt<1>(M, N, K, S) : plan_mt<2>(M, N, K, S);
 }
 
 // walks every lane of every wave of every workgroup of the launch through the kernel's own index helpers
-PackedExtent packed_extent(int M, int N, int K, int S, long lda) {
-  const PackedPlan p = packed_plan(M, N, K, S);
+PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct) {
+  const PackedPlan p = packed_plan(M, N, K, S, nct);
   const int ntiles = (N + 15) / 16, ksteps = K / 32;
   PackedExtent e{0, 0, 0, 0};
   for (int bx = 0; bx < p.gx; ++bx)
@@ -1438,8 +1500,7 @@ PackedExtent packed_extent(int M, int N, int K, int S, long lda) {
           packed_wave_ksteps(K, S, p.NW, sp, wave, ks0, ks1);
           for (int kk = ks0; kk < ks1; kk += p.KU)
             for (int u = 0; u < p.KU; ++u) {
-              const int k = kk + u;
-              if (!(k < ks1)) continue;  // the kernel's load guard
+              const int k = std::min(kk + u, ks1 - 1);  // the kernel's clamped load index
               if (k < 0 || k >= ksteps) ++e.stray_ksteps;
               // both offsets grow with the lane index (lane * 8; row lane & 15 and column 8 * (lane >> 4)), so
               // lane 63 bounds the wave
@@ -1494,11 +1555,21 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
   WMX_CHECK(g.tail.cnt == nullptr ||
                 (packed_tail_ok(g.M, g.N, g.K, g.S) && g.tail.x && g.tail.g && g.tail.b && g.tail.out),
             "packed gemm: reduction tail shape");
-  const int nct = packed_nct(g.M, g.N, g.K);
+  WMX_CHECK(g.nct == 0 || g.nct == 1 || g.nct == 2 || g.nct == 4, "packed gemm: column tiles per workgroup");
+  WMX_CHECK((g.epi.kind != EPI_RESID_STATS && g.epi.kind != EPI_LNFOLD_GELU16) ||
+                (g.S == 1 && g.N % 16 == 0 && g.epi.stats && g.epi.ldc % 4 == 0 &&
+                 (g.epi.kind == EPI_LNFOLD_GELU16 ? (g.epi.c1 && g.epi.c2 && g.K % 16 == 0 && g.K <= 2048)
+                                                  : (g.epi.out16 != nullptr && g.N <= 2048))),
+            "packed gemm: folded-LayerNorm epilogue arguments");
+  const int nct = g.nct ? g.nct : packed_nct(g.M, g.N, g.K);
   if (dt == DT::BF16) {
-    if (nct == 4) launch_packed_mt<DT::BF16, 4>(g, st); else launch_packed_mt<DT::BF16, 2>(g, st);
+    if (nct == 4) launch_packed_mt<DT::BF16, 4>(g, st);
+    else if (nct == 1) launch_packed_mt<DT::BF16, 1>(g, st);
+    else launch_packed_mt<DT::BF16, 2>(g, st);
   } else {
-    if (nct == 4) launch_packed_mt<DT::F16, 4>(g, st); else launch_packed_mt<DT::F16, 2>(g, st);
+    if (nct == 4) launch_packed_mt<DT::F16, 4>(g, st);
+    else if (nct == 1) launch_packed_mt<DT::F16, 1>(g, st);
+    else launch_packed_mt<DT::F16, 2>(g, st);
   }
   WMX_HIP(hipGetLastError());
 }

@@ -13,6 +13,9 @@ enum EpiKind {
   EPI_QKV_CACHE = 5,   // decoder self-attn: q -> out16, k/v -> KV cache at slot *slot0 + (m % Tn)
   EPI_CROSSKV = 6,     // cross K/V of all decoder layers, head-major: K [L][xw][H][kXS][64], V^T [L][xw][H][64][kXS]
   EPI_GELU_MX8 = 7,    // out8 = MX-fp8(gelu(acc + bias)): e4m3 bytes at out (ldc bytes / row), e8m0 scales at out2
+  // decode step, LayerNorm folded into the projections (packed GEMM, S == 1; row_ln_from_stats):
+  EPI_RESID_STATS = 8,  // x32 = out += acc + bias; out16 = 16-bit(x32); stats[n / 16][m] = (mean, M2) of x32
+  EPI_LNFOLD_GELU16 = 9,  // out16 = gelu(rstd_m (acc - mean_m c1[n]) + c2[n]), (mean, rstd) from stats
 };
 
 struct Epi {
@@ -32,6 +35,12 @@ struct Epi {
   // EPI_GELU_MX8: the block scales (one byte per 32 columns, ldc2 bytes per row)
   uint8_t* out2 = nullptr;
   long ldc2 = 0;
+  // EPI_RESID_STATS / EPI_LNFOLD_GELU16: row statistics [d / 16][stats_ld]; the 16-bit copy of x; folded constants
+  float2* stats = nullptr;
+  long stats_ld = 0;
+  uint16_t* out16 = nullptr;
+  const float* c1 = nullptr;
+  const float* c2 = nullptr;
 };
 
 // padded key stride of the cross K/V images (a multiple of 32 keys; the pad stays zero)
@@ -129,6 +138,7 @@ struct PackedCall {
   // in-situ probe: [slot][workgroup][start, end] wall-clock ticks (probe_record) at slot *pslot, or null
   unsigned long long* tprobe = nullptr;
   const int* pslot = nullptr;
+  int nct = 0;  // 16-column tiles per workgroup (0: packed_nct's choice; 1, 2 or 4)
 };
 void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st);
 // the launch geometry launch_gemm_packed chooses: MT 16-row fragments x NCT 16-column tiles per workgroup, NW waves,
@@ -136,7 +146,7 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st);
 struct PackedPlan {
   int MT, NCT, NW, KU, gx, gz;
 };
-PackedPlan packed_plan(int M, int N, int K, int S);
+PackedPlan packed_plan(int M, int N, int K, int S, int nct = 0);
 // the element offsets a packed-GEMM lane reads, shared by gemm_packed_kernel and the host-side extent check
 // (packed_extent): k-step range of one wave, the B fragment of column tile t (clamped to the last tile) and the A
 // fragment of row `row` (clamped to the last row)
@@ -159,7 +169,7 @@ __host__ __device__ inline long packed_a_elem(int row, int M, long lda, int kste
 struct PackedExtent {
   long w_end, a_end, part_end, stray_ksteps;
 };
-PackedExtent packed_extent(int M, int N, int K, int S, long lda);
+PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct = 0);
 // whether a partial-output launch of this shape can carry the RedTail; counters the tail needs
 bool packed_tail_ok(int M, int N, int K, int S);
 constexpr int packed_tail_counters() { return 4096; }
@@ -195,7 +205,10 @@ void launch_unpack_packed(const uint16_t* packed, uint16_t* rowmajor, int N, int
 // decode step (Tn == 1): x = embed, out16 = LN(x) * g + b, in one launch
 void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
                      const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,
-                     hipStream_t st);
+                     hipStream_t st, float2* stats = nullptr, long stats_ld = 0);
+// LayerNorm (g, b) folded into the projection W (+ bias): packed Wp = W diag(g), c1 = Wp 1, c2 = bias + W b
+void launch_fold_ln(DT dt, const uint16_t* Wrm, const float* g, const float* b, const float* bias, int N, int K,
+                    uint16_t* Wp, float* c1, float* c2, hipStream_t st);
 
 // attention
 struct AttnArgs {
@@ -253,6 +266,12 @@ struct DecAttnArgs {
   int qS = 0;
   long qpart_stride = 0, qpart_ld = 0;
   const float* qbias = nullptr;
+  // LayerNorm folded into the projection feeding qpart (wmx_common.h row_ln_from_stats): value =
+  // rstd_row (sum_s qpart - mean_row ln_c1[col]) + ln_c2[col] instead of qbias + sum_s qpart
+  const float* ln_c1 = nullptr;
+  const float* ln_c2 = nullptr;
+  const float2* ln_stats = nullptr;  // [d / 16][ln_ld]
+  long ln_ld = 0;
   int win_of_row_div;  // row -> window = row / rows_per_win
 };
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);

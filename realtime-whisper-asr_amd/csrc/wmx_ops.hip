@@ -289,13 +289,16 @@ void launch_unpack_packed(const uint16_t* packed, uint16_t* rowmajor, int N, int
 
 // ---------------- decode step: token + position embedding and the first layer's LN1 in one launch ----------------
 // one wave per row (4 rows per workgroup); the same arithmetic as embed_kernel followed by layernorm_kernel
+// stats != null (LayerNorm folded into the projections): out = the 16-bit copy of x, stats[g][r] = (mean, M2) of
+// each aligned 16-column group g of x (wmx_common.h row_ln_from_stats), no LN here
 template <DT T>
 __global__ __launch_bounds__(256) void embed_ln_kernel(const uint16_t* __restrict__ tok_emb,
                                                        const uint16_t* __restrict__ pos_emb, const int* __restrict__ hist,
                                                        long hist_ld, const int* __restrict__ pad,
                                                        const int* __restrict__ slot0, const float* __restrict__ g,
                                                        const float* __restrict__ bb, int rows, int d,
-                                                       float* __restrict__ x, uint16_t* __restrict__ out) {
+                                                       float* __restrict__ x, uint16_t* __restrict__ out,
+                                                       float2* __restrict__ stats, long stats_ld) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
   if (r >= rows) return;
@@ -316,7 +319,27 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const uint16_t* __restric
                          to_f32<T>(te[2]) + to_f32<T>(pe[2]), to_f32<T>(te[3]) + to_f32<T>(pe[3]));
       reinterpret_cast<float4*>(x + (long)r * d)[c] = v[i];
       s += v[i].x + v[i].y + v[i].z + v[i].w;
+    } else {
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  }
+  if (stats) {  // per 16-column group = 4 consecutive quads = an aligned group of 4 lanes (d % 64 == 0)
+    uint16_t* o = out + (long)r * d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i * 64 >= n4) break;  // wave-uniform
+      const int c = lane + i * 64;
+      const float4 a = v[i];
+      const float mg = sum4_lanes((a.x + a.y) + (a.z + a.w)) * (1.f / 16.f);
+      const float dx = a.x - mg, dy = a.y - mg, dz = a.z - mg, dw = a.w - mg;
+      const float m2 = sum4_lanes((dx * dx + dy * dy) + (dz * dz + dw * dw));
+      if (c < n4) {
+        const u16x4 h = {from_f32<T>(a.x), from_f32<T>(a.y), from_f32<T>(a.z), from_f32<T>(a.w)};
+        reinterpret_cast<u16x4*>(o)[c] = h;
+        if ((c & 3) == 0) stats[(long)(c >> 2) * stats_ld + r] = make_float2(mg, m2);
+      }
+    }
+    return;
   }
   const float mean = wave_sum(s) / d;
   float q = 0.f;
@@ -348,15 +371,56 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const uint16_t* __restric
 
 void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
                      const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,
-                     hipStream_t st) {
-  WMX_CHECK(d % 32 == 0 && d <= 2048, "embed_ln: d");
+                     hipStream_t st, float2* stats, long stats_ld) {
+  WMX_CHECK(d % 32 == 0 && d <= 2048 && (!stats || d % 64 == 0), "embed_ln: d");
   dim3 grid(cdiv(R, 4));
   if (dt == DT::BF16)
     hipLaunchKernelGGL(embed_ln_kernel<DT::BF16>, grid, dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, pad, slot0,
-                       g, b, R, d, x, out);
+                       g, b, R, d, x, out, stats, stats_ld);
   else
     hipLaunchKernelGGL(embed_ln_kernel<DT::F16>, grid, dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, pad, slot0,
-                       g, b, R, d, x, out);
+                       g, b, R, d, x, out, stats, stats_ld);
+  WMX_HIP(hipGetLastError());
+}
+
+// ---------------- LayerNorm folded into the following projection (decode step; wmx_common.h) ----------------
+// one workgroup per output row n of W [N][K] (row-major copy): Wp (packed) = 16-bit(W[n][k] g[k]),
+// c1[n] = sum_k Wp[n][k] (the rounded values the GEMM multiplies), c2[n] = bias[n] + sum_k b[k] W[n][k]
+template <DT T>
+__global__ __launch_bounds__(256) void fold_ln_kernel(const uint16_t* __restrict__ Wrm, const float* __restrict__ g,
+                                                      const float* __restrict__ b, const float* __restrict__ bias,
+                                                      int K, uint16_t* __restrict__ Wp, float* __restrict__ c1,
+                                                      float* __restrict__ c2) {
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float red[2][4];
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = tid; k < K; k += 256) {
+    const float w = to_f32<T>(Wrm[(long)n * K + k]);
+    const uint16_t wf = from_f32<T>(w * g[k]);
+    Wp[packed_index(n, k, K)] = wf;
+    s1 += to_f32<T>(wf);
+    s2 += b[k] * w;
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    red[0][wave] = s1;
+    red[1][wave] = s2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    c1[n] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    c2[n] = (bias ? bias[n] : 0.f) + ((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+  }
+}
+
+void launch_fold_ln(DT dt, const uint16_t* Wrm, const float* g, const float* b, const float* bias, int N, int K,
+                    uint16_t* Wp, float* c1, float* c2, hipStream_t st) {
+  WMX_CHECK(N % 16 == 0 && K % 32 == 0, "fold_ln: shape");
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(fold_ln_kernel<DT::BF16>, dim3(N), dim3(256), 0, st, Wrm, g, b, bias, K, Wp, c1, c2);
+  else
+    hipLaunchKernelGGL(fold_ln_kernel<DT::F16>, dim3(N), dim3(256), 0, st, Wrm, g, b, bias, K, Wp, c1, c2);
   WMX_HIP(hipGetLastError());
 }
 

@@ -20,6 +20,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/wmx.h"
@@ -126,6 +127,10 @@ struct DecLayer {
   // row-major [N][K] copies of the packed projections (derived after every weight load) for the many-row
   // passes (prompt prefill, word-alignment forward), which run on the tiled MFMA GEMM instead of the packed one
   uint16_t *rqkv, *ro, *rcq, *rco, *rfc1, *rfc2;
+  // the decode step's LayerNorm-folded projections (wmx_common.h row_ln_from_stats; derived after every weight
+  // load): packed W diag(g) of qkv (LN1), cross-q (LN2), fc1 (LN3) and their c1 = W' 1, c2 = bias + W b
+  uint16_t *fqkv, *fcq, *ffc1;
+  float *c1qkv, *c2qkv, *c1cq, *c2cq, *c1fc1, *c2fc1;
 };
 
 struct Model {
@@ -148,6 +153,8 @@ struct Model {
   int *mel_first = nullptr, *mel_count = nullptr, *mel_off = nullptr;
   float* mel_w = nullptr;
   bool initialized = false;
+  bool dirty = false;  // a tensor was set since the derived copies (row-major, MX-fp8, folded) were made
+  bool fold = false;   // decode step on the LayerNorm-folded projections (WMX_FOLD=1; default: reduce_ln form)
   hipStream_t st = nullptr;
 };
 
@@ -229,6 +236,18 @@ static void build_model(Model& m) {
     P.add(&L.bfc1, 4 * dt);
     P.add(&L.wfc2, (size_t)4 * dt * dt);
     P.add(&L.bfc2, dt);
+  }
+  for (auto& L : m.dec) {
+    if (!m.fold) break;  // the folded copies exist only for the opt-in folded step (WMX_FOLD=1)
+    P.add(&L.fqkv, (size_t)3 * dt * dt);
+    P.add(&L.fcq, (size_t)dt * dt);
+    P.add(&L.ffc1, (size_t)4 * dt * dt);
+    P.add(&L.c1qkv, 3 * dt);
+    P.add(&L.c2qkv, 3 * dt);
+    P.add(&L.c1cq, dt);
+    P.add(&L.c2cq, dt);
+    P.add(&L.c1fc1, 4 * dt);
+    P.add(&L.c2fc1, 4 * dt);
   }
   for (auto& L : m.dec) {
     P.add(&L.rqkv, (size_t)3 * dt * dt);
@@ -374,6 +393,30 @@ static void prepare_rowmajor(Model& m) {
 
 // MX-fp8 mode: derive the e4m3 + e8m0 copies of the encoder projections from the 16-bit weights (after every
 // weight load; deterministic, so ranks that receive the broadcast arena may redo it harmlessly)
+// WMX_DEBUG_SYNC=1: after a preparation stage, wait for the device, give an asynchronous fault time to be delivered
+// and report it under the stage's name
+static void debug_device(const char* what) {
+  static const bool on = getenv("WMX_DEBUG_SYNC") != nullptr;
+  if (!on) return;
+  hipError_t e = hipDeviceSynchronize();
+  usleep(300000);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipGetLastError();
+  fprintf(stderr, "[wmx debug] %s: %s\n", what, hipGetErrorString(e));
+  if (e != hipSuccess) throw std::runtime_error(std::string("debug check after ") + what + ": " + hipGetErrorString(e));
+}
+
+static void prepare_fold(Model& m) {
+  if (!m.fold) return;
+  const int dt = m.d.n_text_state;
+  for (auto& L : m.dec) {
+    launch_fold_ln(m.dt, L.rqkv, L.ln1g, L.ln1b, L.bqkv, 3 * dt, dt, L.fqkv, L.c1qkv, L.c2qkv, m.st);
+    launch_fold_ln(m.dt, L.rcq, L.ln2g, L.ln2b, L.bcq, dt, dt, L.fcq, L.c1cq, L.c2cq, m.st);
+    launch_fold_ln(m.dt, L.rfc1, L.ln3g, L.ln3b, L.bfc1, 4 * dt, dt, L.ffc1, L.c1fc1, L.c2fc1, m.st);
+  }
+  WMX_HIP(hipStreamSynchronize(m.st));
+}
+
 static void prepare_mx8(Model& m) {
   if (!m.mx8) return;
   const int da = m.d.n_audio_state;
@@ -434,6 +477,7 @@ struct Ctx {
   float* ws = nullptr;
   long ws_elems = 0;
   float* part = nullptr;  // split-K partials of the packed decode GEMMs [S][rows][N]
+  float2* rstat = nullptr;  // LayerNorm-folded step: per-16-column (mean, M2) of the residual rows [dt / 16][R]
   long part_elems = 0;
   int *hist = nullptr, *hist_tmp = nullptr, *anc = nullptr, *anc_tmp = nullptr, *pad_row = nullptr, *pad_win = nullptr;
   int *slot = nullptr, *n_done = nullptr, *lang_slot = nullptr, *lang_tok = nullptr, *row_map = nullptr, *gather = nullptr;
@@ -482,7 +526,13 @@ struct Ctx {
   int rec_cap = 0, rec_R = 0;
 };
 
-static void sync(Ctx& c) { WMX_HIP(hipStreamSynchronize(c.st)); }
+static void sync_at(Ctx& c, int line) {
+  const hipError_t e = hipStreamSynchronize(c.st);
+  if (e != hipSuccess)
+    throw Error(2, std::string("hipStreamSynchronize(c.st) at wmx_runtime.hip:") + std::to_string(line) + ": " +
+                       hipGetErrorString(e));
+}
+#define sync(c) sync_at(c, __LINE__)
 
 static void alloc_ctx(Ctx& c) {
   const wmx_dims& d = c.m->d;
@@ -533,6 +583,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.vc, (size_t)Lt * T * R * dt);
   P.add(&c.logits, (size_t)c.logits_rows * c.ldl);
   P.add(&c.ws, (size_t)c.ws_elems);
+  P.add(&c.rstat, (size_t)(dt / 16) * R);
   c.part_elems = (long)R * dt * 48;
   P.add(&c.part, (size_t)c.part_elems);
   P.add(&c.hist, (size_t)R * T);
@@ -594,6 +645,7 @@ static void alloc_ctx(Ctx& c) {
   for (int t : c.suppress)
     if (t >= 0 && t < V) mask[t >> 5] |= 1u << (t & 31);
   WMX_HIP(hipMemcpyAsync(c.mask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, c.st));
+  debug_device("ctx alloc");
   for (auto& e : c.ev) WMX_HIP(hipEventCreate(&e));
   {
     int khz = 0;
@@ -978,6 +1030,150 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
   }
 }
 
+// Decode step with every LayerNorm folded into the projection that consumes it (wmx_common.h row_ln_from_stats):
+// the residual producers (embedding, out-projection, cross out-projection, fc2) run unsplit and leave x, its 16-bit
+// copy and per-16-column statistics; the consumers (QKV -> self attention, cross-q -> cross attention, fc1) apply
+// LN through W diag(g), c1, c2.  8 launches per layer instead of 11 (no reduce_ln), plus one final LayerNorm.
+// Leaves LN_final(x) of every row in c.dhb.
+static Epi epi_resid_stats(Ctx& c, const float* bias, int R) {
+  Epi e = epi(EPI_RESID_STATS, bias, c.dx, c.m->d.n_text_state);
+  e.out16 = c.dhb;
+  e.stats = c.rstat;
+  e.stats_ld = R;
+  return e;
+}
+
+static void gemm_p_resid(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, const Epi& e) {
+  PackedCall g;
+  g.A = A;
+  g.lda = lda;
+  g.W = Wp;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.S = 1;
+  g.epi = e;
+  g.nct = 1;  // unsplit: 16 columns per workgroup (N / 16 workgroups, 16 waves splitting K)
+  g.tprobe = c.cur_probe;
+  g.pslot = c.slot;
+  launch_gemm_packed(c.dt, g, c.st);
+}
+
+// WMX_DEBUG_SYNC=1 (fault localisation on eager, uncaptured steps): synchronise after each launch of the step
+// and name the launch that failed
+static void debug_sync(Ctx& c, const char* what, int l) {
+  static const bool on = getenv("WMX_DEBUG_SYNC") != nullptr;
+  if (!on) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  WMX_HIP(hipStreamIsCapturing(c.st, &cs));
+  if (cs != hipStreamCaptureStatusNone) return;
+  const hipError_t e = hipStreamSynchronize(c.st);
+  if (e != hipSuccess) throw std::runtime_error(std::string("debug sync after ") + what + " (layer " + std::to_string(l) + "): " + hipGetErrorString(e));
+}
+
+static void dec_step_fold(Ctx& c, const FwdArgs& f) {
+  Model& m = *c.m;
+  const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
+  const int R = f.rows;
+  const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
+  launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, nullptr, nullptr, dt, c.dx, c.dhb,
+                  c.st, c.rstat, R);
+  debug_sync(c, "embed", -1);
+  const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
+  for (int l = 0; l < Lt; ++l) {
+    DecLayer& L = m.dec[l];
+    const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
+    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
+    // self attention: x16 . (LN1-folded QKV)^T partials -> (LN1 + reduce, cache write, attention)
+    probe(kProbeQKV);
+    int S = gemm_p_part(c, c.dhb, dt, L.fqkv, R, 3 * dt, dt);
+    c.cur_probe = nullptr;
+    debug_sync(c, "qkv", l);
+    DecAttnArgs a{};
+    a.o = c.dao;
+    a.R = R;
+    a.Tn = 1;
+    a.H = H;
+    a.d = dt;
+    a.kc = c.kc + l * cache_layer;
+    a.vc = c.vc + l * cache_layer;
+    a.kv_R = c.R;
+    a.anc = f.anc;
+    a.anc_ld = c.Tctx;
+    a.pad = f.pad_seq;
+    a.slot0 = c.slot;
+    a.qpart = c.part;
+    a.qS = S;
+    a.qpart_stride = (long)R * 3 * dt;
+    a.qpart_ld = 3 * dt;
+    a.ln_c1 = L.c1qkv;
+    a.ln_c2 = L.c2qkv;
+    a.ln_stats = c.rstat;
+    a.ln_ld = R;
+    launch_self_attn(c.dt, a, c.st);
+    debug_sync(c, "self_attn", l);
+    // out-projection, unsplit: x += o Wo^T + bo, x16, statistics
+    probe(kProbeOut);
+    gemm_p_resid(c, c.dao, dt, L.wo, R, dt, dt, epi_resid_stats(c, L.bo, R));
+    debug_sync(c, "out_resid", l);
+    // cross attention: x16 . (LN2-folded cross-q)^T partials -> (LN2 + reduce, attention)
+    probe(kProbeCrossQ);
+    S = gemm_p_part(c, c.dhb, dt, L.fcq, R, dt, dt);
+    c.cur_probe = nullptr;
+    debug_sync(c, "cross_q", l);
+    DecAttnArgs x{};
+    x.o = c.dao;
+    x.R = R;
+    x.Tn = 1;
+    x.H = H;
+    x.d = dt;
+    x.ck = cross_k(c, l);
+    x.cv = cross_v(c, l);
+    x.x_wstride = (long)kXS * dt;
+    x.x_hstride = (long)kXS * 64;
+    x.Tk = 1500;
+    x.rows_per_win = c.K;
+    x.qpart = c.part;
+    x.qS = S;
+    x.qpart_stride = (long)R * dt;
+    x.qpart_ld = dt;
+    x.ln_c1 = L.c1cq;
+    x.ln_c2 = L.c2cq;
+    x.ln_stats = c.rstat;
+    x.ln_ld = R;
+    x.xcnt = c.xa_cnt;
+    x.slot0 = c.slot;
+    if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
+    launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    debug_sync(c, "cross_attn", l);
+    probe(kProbeCrossOut);
+    gemm_p_resid(c, c.dao, dt, L.wco, R, dt, dt, epi_resid_stats(c, L.bco, R));
+    debug_sync(c, "cross_out_resid", l);
+    // MLP: GELU(LN3-folded fc1) -> fc2 unsplit (x += ..., x16, statistics)
+    probe(kProbeFc1);
+    Epi e1 = epi(EPI_LNFOLD_GELU16, nullptr, c.df1, 4 * dt);
+    e1.c1 = L.c1fc1;
+    e1.c2 = L.c2fc1;
+    e1.stats = c.rstat;
+    e1.stats_ld = R;
+    gemm_p(c, c.dhb, dt, L.ffc1, R, 4 * dt, dt, e1);
+    debug_sync(c, "fc1_fold", l);
+    probe(kProbeFc2);
+    gemm_p_resid(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, epi_resid_stats(c, L.bfc2, R));
+    c.cur_probe = nullptr;
+    debug_sync(c, "fc2_resid", l);
+  }
+  launch_layernorm_rows(c.dt, c.dx, nullptr, m.lng, m.lnb, c.dhb, R, dt, c.st);
+  debug_sync(c, "final_ln", -1);
+}
+
+static void dec_step(Ctx& c, const FwdArgs& f) {
+  if (c.m->fold)
+    dec_step_fold(c, f);
+  else
+    dec_step_fast(c, f);
+}
+
 static void dec_forward(Ctx& c, const FwdArgs& f) {
   Model& m = *c.m;
   const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
@@ -1176,8 +1372,10 @@ static void logmel_dev(Ctx& c, const float* pcm_dev, long stride, const long* le
     for (int b = 0; b < B; ++b) sk[b] = seek_host[b];
   WMX_HIP(hipMemcpyAsync(c.lens, lens_host, B * sizeof(long), hipMemcpyHostToDevice, c.st));
   WMX_HIP(hipMemcpyAsync(c.seek, sk.data(), B * 4, hipMemcpyHostToDevice, c.st));
+  debug_device("before logmel");
   launch_logmel(pcm_dev, stride, c.lens, c.seek, B, (int)(maxlen / 160) + 1, m.mel_basis, m.mel_first, m.mel_count,
                 m.mel_off, m.mel_w, m.d.n_mels, c.mel_raw, c.fcap, c.wmax, out_dev, c.st);
+  debug_device("logmel");
   sync(c);  // sk / lens host vectors
 }
 
@@ -1216,9 +1414,11 @@ static void run_step(Ctx& c, int B) {
   f.pad_seq = c.pad_row;
   f.prefill = false;
   f.anc = c.K > 1 ? c.anc : nullptr;
-  dec_step_fast(c, f);
+  dec_step(c, f);
   dec_logits(c, nullptr, f.rows, true);
+  debug_sync(c, "logits", -1);
   select_and_update(c, B, nullptr);
+  debug_sync(c, "select_update", -1);
 }
 
 // decode steps between n_done read-backs; the chunk is one graph launch
@@ -1258,10 +1458,21 @@ static void ensure_step_graphs(Ctx& c, int B) {
   c.graph_key = key;
 }
 
+// tensors set one by one (wmx_model_set_tensor) since the last preparation: re-derive the MX-fp8, row-major and
+// LayerNorm-folded copies before the next use
+static void ensure_prepared(Model& m) {
+  if (!m.dirty || !m.initialized) return;
+  prepare_mx8(m);
+  prepare_rowmajor(m);
+  prepare_fold(m);
+  m.dirty = false;
+}
+
 static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const long* lens, const int32_t* seek, int B,
                                 const int32_t* prompt_ids, const int32_t* prompt_lens) {
   Model& m = *c.m;
   WMX_CHECK(m.initialized, "transcribe: model weights not initialised");
+  ensure_prepared(m);
   WMX_CHECK(B >= 1 && B <= c.maxB, "transcribe: batch exceeds max_batch");
   const int K = c.K, R = K * B, V = m.d.n_vocab, T = c.Tctx;
   const Special& sp = c.sp;
@@ -1269,8 +1480,10 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   logmel_dev(c, pcm_dev, stride, lens, seek, B, c.mel);
   rec(c, 1);
   encode(c, B);
+  debug_device("encode");
   rec(c, 2);
   cross_kv(c, B);
+  debug_device("cross_kv");
   rec(c, 3);
 
   // ---- prompts (left padded to Pmax) ----
@@ -1325,6 +1538,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   std::vector<int> rmap(R);
   for (int r = 0; r < R; ++r) rmap[r] = r / K;
   WMX_HIP(hipMemcpyAsync(c.row_map, rmap.data(), R * 4, hipMemcpyHostToDevice, c.st));
+  debug_device("prompt setup");
   sync(c);
 
   // ---- language detection: one decoder step on <|startoftranscript|> ----
@@ -1347,6 +1561,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     dec_forward(c, f);
     dec_logits(c, nullptr, B);
     launch_lang_detect(c.logits, c.ldl, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st);
+    debug_sync(c, "lang_detect", -1);
   }
   rec(c, 4);
 
@@ -1386,6 +1601,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   }
   if (max_new > 0) {
     select_and_update(c, B, c.row_map);
+    debug_sync(c, "first_select", -1);
     steps = 1;
   }
   rec(c, 5);
@@ -1669,6 +1885,9 @@ wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_mod
       w->m.device = device;
       w->m.dt = dtype == WMX_DTYPE_F16 ? DT::F16 : DT::BF16;
       w->m.mx8 = dtype == WMX_DTYPE_MX8;
+      // opt-in (WMX_FOLD=1): the LayerNorm-folded decode step passes every parity test but measured slower than
+      // the split-K + reduce_ln step (356-390 vs 389-393x real time, interleaved on one box)
+      w->m.fold = getenv("WMX_FOLD") != nullptr;
       WMX_HIP(hipSetDevice(device));
       WMX_HIP(hipStreamCreateWithFlags(&w->m.st, hipStreamNonBlocking));
       build_model(w->m);
@@ -1708,9 +1927,14 @@ wmx_status wmx_model_init_synthetic(wmx_model* w, uint64_t seed) {
       launch_init_tensor(m.dt, seed, s, m.st);
     }
     WMX_HIP(hipStreamSynchronize(m.st));
+    debug_device("init tensors");
     prepare_mx8(m);
     prepare_rowmajor(m);
+    debug_device("prepare_rowmajor");
+    prepare_fold(m);
+    debug_device("prepare_fold");
     m.initialized = true;
+    m.dirty = false;
   });
 }
 
@@ -1732,6 +1956,7 @@ wmx_status wmx_model_set_tensor(wmx_model* w, const char* name, const float* dat
       return;
     }
     const TensorEntry& e = find_entry(m, name, n);
+    m.dirty = true;
     if (e.store_f32) {
       WMX_HIP(hipMemcpy(e.dst, data, n * 4, hipMemcpyHostToDevice));
       return;
@@ -1770,6 +1995,7 @@ wmx_status wmx_model_get_tensor(wmx_model* w, const char* name, float* out, int6
       return;
     }
     const TensorEntry& e = find_entry(m, name, n);
+    m.dirty = true;
     if (e.store_f32) {
       WMX_HIP(hipMemcpy(out, e.dst, n * 4, hipMemcpyDeviceToHost));
       return;
@@ -1809,7 +2035,9 @@ wmx_status wmx_model_arena_loaded(wmx_model* w) {
     WMX_HIP(hipSetDevice(w->m.device));
     prepare_mx8(w->m);
     prepare_rowmajor(w->m);
+    prepare_fold(w->m);
     w->m.initialized = true;
+    w->m.dirty = false;
   });
 }
 
@@ -1933,6 +2161,7 @@ wmx_status wmx_encode_device(wmx_ctx* x, const float* mel_dev, int B) {
     WMX_CHECK(c.m->initialized, "encode: weights not initialised");
     WMX_CHECK(B >= 1 && B <= c.maxB, "encode: batch");
     WMX_HIP(hipSetDevice(c.m->device));
+    ensure_prepared(*c.m);
     if (mel_dev != c.mel)
       WMX_HIP(hipMemcpyAsync(c.mel, mel_dev, (size_t)B * c.m->d.n_mels * 3000 * 4, hipMemcpyDeviceToDevice, c.st));
     encode(c, B);
@@ -1947,6 +2176,7 @@ wmx_status wmx_encode(wmx_ctx* x, const float* mel, int B, float* enc_out) {
     WMX_CHECK(c.m->initialized, "encode: weights not initialised");
     WMX_CHECK(B >= 1 && B <= c.maxB, "encode: batch");
     WMX_HIP(hipSetDevice(c.m->device));
+    ensure_prepared(*c.m);
     WMX_HIP(hipMemcpyAsync(c.mel, mel, (size_t)B * c.m->d.n_mels * 3000 * 4, hipMemcpyHostToDevice, c.st));
     encode(c, B);
     cross_kv(c, B);
@@ -1964,6 +2194,7 @@ wmx_status wmx_decoder_logits(wmx_ctx* x, const int32_t* tokens, const int32_t* 
     Ctx& c = x->c;
     Model& m = *c.m;
     WMX_CHECK(B >= 1 && B <= c.maxB && T >= 1 && T <= c.Tctx, "decoder_logits: shape");
+    ensure_prepared(m);
     WMX_HIP(hipSetDevice(m.device));
     const int K = c.K, Tc = c.Tctx, V = m.d.n_vocab;
     std::vector<int> tok((size_t)B * K * Tc, 0);
@@ -2003,6 +2234,7 @@ wmx_status wmx_ctx_forced_decode(wmx_ctx* x, const int32_t* prefix, const int32_
     Ctx& c = x->c;
     Model& m = *c.m;
     WMX_CHECK(m.initialized, "forced_decode: weights not initialised");
+    ensure_prepared(m);
     WMX_CHECK(B >= 1 && B <= c.maxB && P >= 1 && n_steps >= 0 && P + n_steps <= c.Tctx, "forced_decode: shape");
     WMX_CHECK(prefix && top1 && (n_steps == 0 || (tokens && parents)) && (!logits || every >= 1),
               "forced_decode: null argument");
@@ -2089,7 +2321,7 @@ wmx_status wmx_ctx_forced_decode(wmx_ctx* x, const int32_t* prefix, const int32_
       f.pad_seq = c.pad_row;
       f.prefill = false;
       f.anc = K > 1 ? c.anc : nullptr;
-      dec_step_fast(c, f);
+      dec_step(c, f);
       dec_logits(c, nullptr, R, true);
       collect(i + 1, R, 1);
     }
@@ -2101,12 +2333,13 @@ wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int sp
     WMX_CHECK(out9 && M >= 1 && N >= 1 && K >= 32 && K % 32 == 0, "debug_packed_launch: arguments");
     // the split count the runtime's callers use: gemm_p (S = 1, epilogue) or gemm_p_part (partials, S >= 2)
     int S = 1;
-    if (split) {
+    if (split == 1) {
       S = packed_splits(M, N, K, part_cap);
       if (S == 1) S = 2;
     }
-    const PackedPlan p = packed_plan(M, N, K, S);
-    const PackedExtent e = packed_extent(M, N, K, S, lda);
+    const int nct = split == 2 ? 1 : 0;  // 2: the unsplit residual producers of the folded step (gemm_p_resid)
+    const PackedPlan p = packed_plan(M, N, K, S, nct);
+    const PackedExtent e = packed_extent(M, N, K, S, lda, nct);
     const int64_t v[9] = {S, p.MT, p.NCT, p.NW, p.KU, e.w_end, e.a_end, e.part_end, e.stray_ksteps};
     std::memcpy(out9, v, sizeof(v));
   });

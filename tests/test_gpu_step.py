@@ -297,3 +297,19 @@ def test_control_tokens_suppressed_with_boosted_logits():
         _replay_and_compare(f"suppressed control tokens K={K}", ctx, res, K, opt, sp, 16)
         bare = E.Context(m, max_batch=2, beam_size=K, max_new_tokens=24, word_timestamps=False, language=sp.lang0)
         assert any(set(r.tokens) & set(ctrl) for r in bare.transcribe(audios))
+
+
+def test_folded_layernorm_step_parity():
+    """The opt-in LayerNorm-folded decode step (WMX_FOLD=1: unsplit residual producers with per-16-column row
+    statistics, LN applied through W diag(g), c1, c2 by the consumers; wmx_runtime.hip dec_step_fold) against the
+    oracle: this file's step and search tests rerun in a child process with the switch set (read at model creation)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WMX_FOLD="1")
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+           "-k", "not folded_layernorm and not full_depth", "tests/test_gpu_step.py"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

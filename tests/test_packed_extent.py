@@ -38,7 +38,11 @@ def decode_launches(d, B, K):
            ("cross_q", R, dt, dt, 1, dt, dt * dt, rows_cap),
            ("fc1", R, 4 * dt, dt, 0, dt, 4 * dt * dt, rows_cap),
            ("fc2", R, dt, 4 * dt, 1, 4 * dt, 4 * dt * dt, rows_cap),
-           ("logits", R, V, dt, 0, dt, (V + 15) // 16 * 16 * dt, rows_cap)]
+           ("logits", R, V, dt, 0, dt, (V + 15) // 16 * 16 * dt, rows_cap),
+           # the LayerNorm-folded step (wmx_runtime.hip dec_step_fold): unsplit residual producers, 16 columns per
+           # workgroup (split mode 2), and the folded QKV / cross-q / fc1 on the same shapes as above
+           ("out_resid", R, dt, dt, 2, dt, dt * dt, rows_cap),
+           ("fc2_resid", R, dt, 4 * dt, 2, 4 * dt, 4 * dt * dt, rows_cap)]
     # dec_forward on packed weights: rows x Tn <= 256 (more rows take the row-major tiled GEMM)
     for M in sorted({1, 2, 3, B, min(256, 3 * B), min(256, 7 * B), 255, 256}):
         if M > rows_cap:
@@ -68,7 +72,9 @@ def test_packed_launches_stay_inside_their_buffers(name):
             assert e["stray"] == 0, where
             assert e["w_end"] <= w_elems, where
             assert e["a_end"] <= a_rows * lda, where
-            assert (e["S"] == 1) == (split == 0), where
+            assert (e["S"] == 1) == (split != 1), where
+            if split == 2 and M <= 64:  # more rows: launch_packed_mt's 96- / 64-row configurations (NCT 2)
+                assert e["NCT"] == 1, where
             if split:
                 assert e["part_end"] <= part_cap, where
                 assert e["S"] <= 8, where
