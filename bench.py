@@ -343,26 +343,31 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     p50 = 1000.0 * float(np.median(lat))
 
-    # roofline of the dominant kernel family.  achieved = ALGORITHMIC bytes / launch duration, the duration from
-    # HIP events on the context stream around 20 back-to-back replays of each decode-step launch (geometry and data
-    # of the timed region's last step) -- the same dispatch-to-completion span rocprofv3 reports per kernel (the
-    # rocprofv3 trace of the bench is recomputed by tools/roofline_from_profile.py into profiles/).  The in-situ
-    # device-clock probes of the timed region (first workgroup start .. last workgroup end of layer
-    # `probe_layer`'s launches, every step, both groups concurrent) are reported beside it.
-    agg = {}
-    for c in ctxs:
-        for k, (ms_k, n_k, by_k) in c.probe_launches().items():
-            a = agg.setdefault(k, [0.0, 0, by_k])
-            a[0] += ms_k * n_k
-            a[1] += n_k
-    insitu = {k: (v[0] / v[1] if v[1] else 0.0, v[1], v[2]) for k, v in agg.items()}
+    # roofline of the dominant kernel family.  achieved = ALGORITHMIC bytes / launch duration; the duration is
+    # measured in situ over the timed region with HIP events recorded around each decode-step launch of layer
+    # `probe_layer` inside the captured decode graph (event record nodes; every step of every 8-step replay, both
+    # context groups) -- the dispatch-to-completion span rocprofv3 reports per kernel (the rocprofv3 trace of this
+    # bench is recomputed by tools/roofline_from_profile.py into profiles/).  Beside it: the device-clock workgroup
+    # span of the same launches, and 20 back-to-back replays of each launch alone (HIP events, after the timed region)
+    def gather(events):
+        agg = {}
+        for c in ctxs:
+            for k, (ms_k, n_k, by_k) in c.probe_launches(events=events).items():
+                a = agg.setdefault(k, [0.0, 0, by_k])
+                a[0] += ms_k * n_k
+                a[1] += n_k
+        return {k: (v[0] / v[1] if v[1] else 0.0, v[1], v[2]) for k, v in agg.items()}
+    evs = gather(True)
+    insitu = gather(False)
     replay_id = {"dec_qkv": "dec_qkv", "dec_out": "dec_proj", "dec_cross_q": "dec_proj", "dec_cross_out": "dec_proj",
                  "dec_fc1": "dec_fc1", "dec_fc2": "dec_fc2", "cross_attn": "cross_attn"}
     replay_cache = {}
     for k, rid in replay_id.items():
         if rid not in replay_cache:
             replay_cache[rid] = ctx.bench_kernel(rid, Bg, iters=20)
-    launch = {k: (replay_cache[rid][0], replay_cache[rid][1]) for k, rid in replay_id.items()}
+    replay = {k: (replay_cache[rid][0], replay_cache[rid][1]) for k, rid in replay_id.items()}
+    use_ev = all(evs[k][1] > 0 for k in replay_id)
+    launch = {k: ((evs[k][0], evs[k][2]) if use_ev else replay[k]) for k in replay_id}
     fams = {"gemm_packed_kernel": [k for k in launch if k.startswith("dec_")], "dec_cross_attn_kernel": ["cross_attn"]}
     fam_ms = {f: sum(launch[k][0] for k in ks) for f, ks in fams.items()}  # per layer-step, one group
     dom = max(fam_ms, key=fam_ms.get)
@@ -386,15 +391,17 @@ def main():
             roof["traffic_source"] = f"profiles/{tag}_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
             break
     roof["kernel"] = dom
-    roof["measured"] = ("HIP events on the context stream around 20 back-to-back replays of each launch of one "
-                        "decoder layer's step (wmx_ctx_bench_kernel), after the timed region")
+    roof["measured"] = (f"in situ over the timed region: HIP events captured around layer {probe_layer}'s launches "
+                        f"in the decode graph, {sum(evs[k][1] for k in fams[dom])} launch samples" if use_ev else
+                        "HIP events around 20 back-to-back replays of each launch (wmx_ctx_bench_kernel)")
     roof["launches"] = {k: {"us": round(1000 * launch[k][0], 2), "bytes": launch[k][1],
                             "gbs": round(launch[k][1] / (launch[k][0] * 1e-3) / 1e9, 1)} for k in fams[dom]}
     roof["algorithmic_bytes_per_layer_step"] = by
     roof["layer_step_ms"] = round(ms, 4)
     roof["family_ms_per_layer_step"] = {f: round(v, 4) for f, v in fam_ms.items()}
+    roof["replayed_us"] = {k: round(1000 * replay[k][0], 2) for k in fams[dom]}
     span = sum(insitu[k][0] for k in fams[dom])
-    roof["in_situ"] = {"what": f"device-clock span first workgroup start .. last workgroup end, layer {probe_layer}, "
+    roof["wg_span"] = {"what": f"device-clock span first workgroup start .. last workgroup end, layer {probe_layer}, "
                                f"every timed decode step, both groups", "samples": sum(insitu[k][1] for k in fams[dom]),
                        "us": {k: round(1000 * insitu[k][0], 2) for k in fams[dom]},
                        "achieved_gbs": round(by / (span * 1e-3) / 1e9, 1) if span > 0 else None}
@@ -435,7 +442,8 @@ def main():
     log(f"[rank {rank}] encoder: {encoder}")
     log(f"[rank {rank}] in-situ span us/launch (layer {probe_layer}): " +
         ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in insitu.items() if v[1]))
-    log(f"[rank {rank}] replayed us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in launch.items()))
+    log(f"[rank {rank}] in-situ event us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in evs.items() if v[1]))
+    log(f"[rank {rank}] replayed us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in replay.items()))
     log(f"[rank {rank}] replayed kernel us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in kern_stats.items()))
 
     out = {

@@ -226,10 +226,12 @@ wmx_status wmx_dedup_features(wmx_ctx* c, const float* x, int64_t stride, const 
  * first workgroup start and last workgroup end (device wall clock, hipDeviceAttributeWallClockRate) at every
  * decode step of the timed wmx_transcribe; kernel < 0 disables the probes.  wmx_ctx_probe_stats: the cross
  * attention's average launch duration (ms), steps sampled and ALGORITHMIC bytes of one launch;
- * wmx_ctx_probe_launches: the same for all eight launch ids (avg_ms8 / bytes8 / n8 [8]; id 7 unused). */
+ * wmx_ctx_probe_launches: the same for all eight launch ids (avg_ms8 / bytes8 / n8 [8]; id 7 unused), and
+ * (ev_ms8 / ev_n8, nullable) the launches' durations between HIP events recorded around them inside the captured
+ * decode graph (event record nodes; every step of every full 8-step graph replay). */
 wmx_status wmx_ctx_set_probe(wmx_ctx* c, int kernel, int layer);
 wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
-wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* avg_ms8, double* bytes8, int* n8);
+wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* avg_ms8, double* bytes8, int* n8, float* ev_ms8, int* ev_n8);
 
 #ifdef __cplusplus
 }

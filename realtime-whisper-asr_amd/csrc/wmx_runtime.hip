@@ -515,6 +515,13 @@ struct Ctx {
   int probe_kernel = -1, probe_layer = 0;
   unsigned long long* probe_buf = nullptr;
   unsigned long long* cur_probe = nullptr;
+  // the same launches bracketed by HIP events captured into the kGraphChunk-step graph (event record nodes):
+  // pev[step in chunk][launch][before, after]; cur_id = the probed launch being issued (-1: none); cap_step = the
+  // step of the chunk graph being captured (-1: not capturing the chunk graph)
+  hipEvent_t pev[8][8][2] = {};
+  int cur_id = -1, cap_step = -1;
+  double ev_ms[8] = {0};
+  int ev_n[8] = {0};
   double probe_bytes[8] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   float stage_ms[7] = {0};
@@ -533,6 +540,11 @@ static void sync_at(Ctx& c, int line) {
                        hipGetErrorString(e));
 }
 #define sync(c) sync_at(c, __LINE__)
+
+// event record node around a probed launch while the chunk graph is captured (see Ctx::pev)
+static void ev_mark(Ctx& c, int which) {
+  if (c.cur_id >= 0 && c.cap_step >= 0 && c.cap_step < 8) WMX_HIP(hipEventRecord(c.pev[c.cap_step][c.cur_id][which], c.st));
+}
 
 static void alloc_ctx(Ctx& c) {
   const wmx_dims& d = c.m->d;
@@ -740,7 +752,9 @@ static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int 
   g.epi = e;
   g.tprobe = c.cur_probe;
   g.pslot = c.slot;
+  ev_mark(c, 0);
   launch_gemm_packed(c.dt, g, c.st);
+  ev_mark(c, 1);
 }
 
 // decoder projection on packed weights, split-K raw partials into c.part; returns the split count
@@ -760,7 +774,9 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
     g.S = 2;
     WMX_CHECK(2L * M * N <= c.part_elems, "decode gemm: partial buffer too small");
   }
+  ev_mark(c, 0);
   launch_gemm_packed(c.dt, g, c.st);
+  ev_mark(c, 1);
   return g.S;
 }
 
@@ -967,11 +983,15 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     DecLayer& L = m.dec[l];
     const bool last = l + 1 == Lt;
     const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
-    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
+    auto probe = [&](int id) {
+      c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr;
+      c.cur_id = probed ? id : -1;
+    };
     // self attention: QKV partials -> (reduce, cache write, attention) -> out-proj partials -> +x, LN2
     probe(kProbeQKV);
     int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt);
     c.cur_probe = nullptr;
+    c.cur_id = -1;
     DecAttnArgs a{};
     a.o = c.dao;
     a.R = R;
@@ -997,6 +1017,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     probe(kProbeCrossQ);
     S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
     c.cur_probe = nullptr;
+    c.cur_id = -1;
     DecAttnArgs x{};
     x.o = c.dao;
     x.R = R;
@@ -1017,7 +1038,11 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
     if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
+    c.cur_id = probed ? (int)kProbeCross : -1;
+    ev_mark(c, 0);
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    ev_mark(c, 1);
+    c.cur_id = -1;
     probe(kProbeCrossOut);
     gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b);
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
@@ -1027,6 +1052,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
                  last ? m.lnb : m.dec[l + 1].ln1b);
     c.cur_probe = nullptr;
+    c.cur_id = -1;
   }
 }
 
@@ -1056,7 +1082,9 @@ static void gemm_p_resid(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp
   g.nct = 1;  // unsplit: 16 columns per workgroup (N / 16 workgroups, 16 waves splitting K)
   g.tprobe = c.cur_probe;
   g.pslot = c.slot;
+  ev_mark(c, 0);
   launch_gemm_packed(c.dt, g, c.st);
+  ev_mark(c, 1);
 }
 
 // WMX_DEBUG_SYNC=1 (fault localisation on eager, uncaptured steps): synchronise after each launch of the step
@@ -1083,11 +1111,15 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
     const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
-    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
+    auto probe = [&](int id) {
+      c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr;
+      c.cur_id = probed ? id : -1;
+    };
     // self attention: x16 . (LN1-folded QKV)^T partials -> (LN1 + reduce, cache write, attention)
     probe(kProbeQKV);
     int S = gemm_p_part(c, c.dhb, dt, L.fqkv, R, 3 * dt, dt);
     c.cur_probe = nullptr;
+    c.cur_id = -1;
     debug_sync(c, "qkv", l);
     DecAttnArgs a{};
     a.o = c.dao;
@@ -1120,6 +1152,7 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
     probe(kProbeCrossQ);
     S = gemm_p_part(c, c.dhb, dt, L.fcq, R, dt, dt);
     c.cur_probe = nullptr;
+    c.cur_id = -1;
     debug_sync(c, "cross_q", l);
     DecAttnArgs x{};
     x.o = c.dao;
@@ -1144,7 +1177,11 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
     if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
+    c.cur_id = probed ? (int)kProbeCross : -1;
+    ev_mark(c, 0);
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    ev_mark(c, 1);
+    c.cur_id = -1;
     debug_sync(c, "cross_attn", l);
     probe(kProbeCrossOut);
     gemm_p_resid(c, c.dao, dt, L.wco, R, dt, dt, epi_resid_stats(c, L.bco, R));
@@ -1161,6 +1198,7 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
     probe(kProbeFc2);
     gemm_p_resid(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, epi_resid_stats(c, L.bfc2, R));
     c.cur_probe = nullptr;
+    c.cur_id = -1;
     debug_sync(c, "fc2_resid", l);
   }
   launch_layernorm_rows(c.dt, c.dx, nullptr, m.lng, m.lnb, c.dhb, R, dt, c.st);
@@ -1450,7 +1488,11 @@ static void ensure_step_graphs(Ctx& c, int B) {
   for (int gi = 0; gi < 2; ++gi) {
     hipGraph_t gph = nullptr;
     WMX_HIP(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < (gi ? kGraphChunk : 1); ++i) run_step(c, B);
+    for (int i = 0; i < (gi ? kGraphChunk : 1); ++i) {
+      c.cap_step = (gi == 1 && c.probe_kernel >= 0) ? i : -1;  // event probes only in the chunk graph
+      run_step(c, B);
+    }
+    c.cap_step = -1;
     WMX_HIP(hipStreamEndCapture(c.st, &gph));
     WMX_HIP(hipGraphInstantiate(&c.graph[gi], gph, nullptr, nullptr, 0));
     WMX_HIP(hipGraphDestroy(gph));
@@ -1608,6 +1650,10 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   // ---- decode loop: one hipGraph replay per step ----
   const int need_done = K == 1 ? R : B;
   c.probe_slots[0] = steps > 0 ? Pmax : 0;  // slots of the graph-replayed steps of this call
+  for (int k = 0; k < kProbeLaunches; ++k) {
+    c.ev_ms[k] = 0;
+    c.ev_n[k] = 0;
+  }
   if (c.probe_kernel >= 0)  // per-workgroup records of this call only (read after the timed region)
     WMX_HIP(hipMemsetAsync(c.probe_buf, 0, (size_t)kProbeLaunches * T * kProbeWG * 2 * 8, c.st));
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
@@ -1630,6 +1676,15 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     steps += chunk;
     WMX_HIP(hipMemcpyAsync(c.pinned_i, c.n_done, 4, hipMemcpyDeviceToHost, c.st));
     sync(c);
+    if (c.probe_kernel >= 0 && c.o.use_graph && chunk == kGraphChunk)  // event probes of this chunk replay
+      for (int s8 = 0; s8 < kGraphChunk; ++s8)
+        for (int k = 0; k < kProbeLaunches; ++k) {
+          float ms = 0.f;
+          if (c.pev[s8][k][0] && hipEventElapsedTime(&ms, c.pev[s8][k][0], c.pev[s8][k][1]) == hipSuccess && ms > 0) {
+            c.ev_ms[k] += ms;
+            c.ev_n[k] += 1;
+          }
+        }
 
     if (c.pinned_i[0] >= need_done) break;
   }
@@ -2123,6 +2178,10 @@ void wmx_ctx_destroy(wmx_ctx* x) {
   if (c.pinned_i) (void)hipHostFree(c.pinned_i);
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& a : c.pev)
+    for (auto& b : a)
+      for (auto& e : b)
+        if (e) (void)hipEventDestroy(e);
   if (c.st) (void)hipStreamDestroy(c.st);
   delete x;
 }
@@ -2507,8 +2566,13 @@ wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
   return guard([&] {
     WMX_CHECK(kernel < 1, "probe: 0 enables the decode-step probes, < 0 disables them");
     WMX_CHECK(layer >= 0 && layer < x->c.m->d.n_text_layer, "probe: layer");
-    x->c.probe_kernel = kernel;
-    x->c.probe_layer = layer;
+    Ctx& c = x->c;
+    if (kernel >= 0 && !c.pev[0][0][0])
+      for (auto& a : c.pev)
+        for (auto& b : a)
+          for (auto& e : b) WMX_HIP(hipEventCreate(&e));
+    c.probe_kernel = kernel;
+    c.probe_layer = layer;
   });
 }
 
@@ -2551,7 +2615,7 @@ wmx_status wmx_ctx_probe_stats(wmx_ctx* x, float* avg_ms, int* n, double* bytes)
   });
 }
 
-wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* avg_ms8, double* bytes8, int* n8) {
+wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* avg_ms8, double* bytes8, int* n8, float* ev_ms8, int* ev_n8) {
   return guard([&] {
     Ctx& c = x->c;
     double ms[kProbeLaunches];
@@ -2559,6 +2623,8 @@ wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* avg_ms8, double* bytes8, in
     for (int k = 0; k < kProbeLaunches; ++k) {
       avg_ms8[k] = (float)ms[k];
       bytes8[k] = c.probe_bytes[k];
+      if (ev_ms8) ev_ms8[k] = c.ev_n[k] ? (float)(c.ev_ms[k] / c.ev_n[k]) : 0.f;
+      if (ev_n8) ev_n8[k] = c.ev_n[k];
     }
   });
 }

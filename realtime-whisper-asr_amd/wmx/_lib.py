@@ -104,7 +104,7 @@ def _load():
                                           P(C.c_double), C.c_int, VP]),
         "wmx_dedup_features": (C.c_int, [VP, P(F), I64, P(I64), C.c_int, F, P(F)]),
         "wmx_ctx_probe_stats": (C.c_int, [VP, P(F), P(C.c_int), P(C.c_double)]),
-        "wmx_ctx_probe_launches": (C.c_int, [VP, P(F), P(C.c_double), P(C.c_int)]),
+        "wmx_ctx_probe_launches": (C.c_int, [VP, P(F), P(C.c_double), P(C.c_int), P(F), P(C.c_int)]),
         "wmx_ctx_bench_kernel": (C.c_int, [VP, C.c_int, C.c_int, C.c_int, P(F), P(C.c_double), P(C.c_double)]),
     }
     for name, (res, args) in sig.items():

@@ -318,12 +318,19 @@ class Context:
         last-workgroup end on the device clock."""
         check(lib.wmx_ctx_set_probe(self._h, 0 if on else -1, layer))
 
-    def probe_launches(self) -> dict:
-        """{launch: (average in-situ duration ms, samples, algorithmic bytes of one launch)} of the last transcribe."""
+    def probe_launches(self, events: bool = False) -> dict:
+        """{launch: (average in-situ duration ms, samples, algorithmic bytes of one launch)} of the last transcribe:
+        the device-clock workgroup span, or (events=True) the span between the HIP events captured around the
+        launch in the decode graph."""
         ms = np.zeros(8, np.float32)
         by = np.zeros(8, np.float64)
         n = np.zeros(8, np.int32)
-        check(lib.wmx_ctx_probe_launches(self._h, fptr(ms), by.ctypes.data_as(C.POINTER(C.c_double)), iptr(n)))
+        ems = np.zeros(8, np.float32)
+        en = np.zeros(8, np.int32)
+        check(lib.wmx_ctx_probe_launches(self._h, fptr(ms), by.ctypes.data_as(C.POINTER(C.c_double)), iptr(n),
+                                         fptr(ems), iptr(en)))
+        if events:
+            ms, n = ems, en
         return {k: (float(ms[i]), int(n[i]), float(by[i])) for i, k in enumerate(self.PROBE_LAUNCHES)}
 
     def probe_stats(self):
