@@ -344,21 +344,22 @@ def main():
     p50 = 1000.0 * float(np.median(lat))
 
     # roofline of the dominant kernel family.  achieved = ALGORITHMIC bytes / launch duration; the duration is
-    # measured in situ over the timed region with HIP events recorded around each decode-step launch of layer
-    # `probe_layer` inside the captured decode graph (event record nodes; every step of every 8-step replay, both
-    # context groups) -- the dispatch-to-completion span rocprofv3 reports per kernel (the rocprofv3 trace of this
-    # bench is recomputed by tools/roofline_from_profile.py into profiles/).  Beside it: the device-clock workgroup
-    # span of the same launches, and 20 back-to-back replays of each launch alone (HIP events, after the timed region)
+    # measured in situ over the timed region by device-clock probes on every launch of layer `probe_layer` (and the
+    # previous layer's last one), every decode step, both context groups: a launch's duration = its last workgroup
+    # end minus its predecessor's -- dispatch + execution, the per-kernel span rocprofv3 reports (the rocprofv3 trace
+    # of this bench is recomputed by tools/roofline_from_profile.py into profiles/).  Beside it: the execution-only
+    # workgroup span of the same launches, and 20 back-to-back replays of each launch alone (HIP events on the
+    # context stream, after the timed region)
     def gather(events):
         agg = {}
         for c in ctxs:
-            for k, (ms_k, n_k, by_k) in c.probe_launches(events=events).items():
+            for k, (ms_k, n_k, by_k) in c.probe_launches(e2e=events).items():
                 a = agg.setdefault(k, [0.0, 0, by_k])
                 a[0] += ms_k * n_k
                 a[1] += n_k
         return {k: (v[0] / v[1] if v[1] else 0.0, v[1], v[2]) for k, v in agg.items()}
-    evs = gather(True)
-    insitu = gather(False)
+    evs = gather(True)      # end-to-end: dispatch + execution (rocprofv3's per-kernel span)
+    insitu = gather(False)  # first-workgroup-start .. last-workgroup-end
     replay_id = {"dec_qkv": "dec_qkv", "dec_out": "dec_proj", "dec_cross_q": "dec_proj", "dec_cross_out": "dec_proj",
                  "dec_fc1": "dec_fc1", "dec_fc2": "dec_fc2", "cross_attn": "cross_attn"}
     replay_cache = {}
@@ -391,8 +392,9 @@ def main():
             roof["traffic_source"] = f"profiles/{tag}_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
             break
     roof["kernel"] = dom
-    roof["measured"] = (f"in situ over the timed region: HIP events captured around layer {probe_layer}'s launches "
-                        f"in the decode graph, {sum(evs[k][1] for k in fams[dom])} launch samples" if use_ev else
+    roof["measured"] = (f"in situ over the timed region: device-clock end of each launch of layer {probe_layer} minus "
+                        f"its predecessor's, every decode step, both groups, {sum(evs[k][1] for k in fams[dom])} "
+                        f"launch samples" if use_ev else
                         "HIP events around 20 back-to-back replays of each launch (wmx_ctx_bench_kernel)")
     roof["launches"] = {k: {"us": round(1000 * launch[k][0], 2), "bytes": launch[k][1],
                             "gbs": round(launch[k][1] / (launch[k][0] * 1e-3) / 1e9, 1)} for k in fams[dom]}
@@ -442,7 +444,7 @@ def main():
     log(f"[rank {rank}] encoder: {encoder}")
     log(f"[rank {rank}] in-situ span us/launch (layer {probe_layer}): " +
         ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in insitu.items() if v[1]))
-    log(f"[rank {rank}] in-situ event us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in evs.items() if v[1]))
+    log(f"[rank {rank}] in-situ end-to-end us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in evs.items() if v[1]))
     log(f"[rank {rank}] replayed us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in replay.items()))
     log(f"[rank {rank}] replayed kernel us/launch: " + ", ".join(f"{k}={1000 * v[0]:.2f}" for k, v in kern_stats.items()))
 

@@ -221,17 +221,19 @@ wmx_status wmx_filtfilt_device(wmx_ctx* c, const float* x_dev, int64_t stride, c
 wmx_status wmx_dedup_features(wmx_ctx* c, const float* x, int64_t stride, const int64_t* lens, int B, float sr,
                               float* out);
 
-/* in-situ roofline probes: with kernel = 0, the decode-step launches of decoder layer `layer` -- the six packed
- * projection GEMMs (0 qkv, 1 out, 2 cross-q, 3 cross-out, 4 fc1, 5 fc2) and the cross attention (6) -- record their
- * first workgroup start and last workgroup end (device wall clock, hipDeviceAttributeWallClockRate) at every
- * decode step of the timed wmx_transcribe; kernel < 0 disables the probes.  wmx_ctx_probe_stats: the cross
- * attention's average launch duration (ms), steps sampled and ALGORITHMIC bytes of one launch;
- * wmx_ctx_probe_launches: the same for all eight launch ids (avg_ms8 / bytes8 / n8 [8]; id 7 unused), and
- * (ev_ms8 / ev_n8, nullable) the launches' durations between HIP events recorded around them inside the captured
- * decode graph (event record nodes; every step of every full 8-step graph replay). */
+/* in-situ roofline probes: with kernel = 0, every launch of decoder layer `layer` (>= 1) of every decode step of the
+ * timed wmx_transcribe -- the six packed projection GEMMs (ids 0 qkv, 1 out, 2 cross-q, 3 cross-out, 4 fc1, 5 fc2),
+ * the cross attention (6), the self attention (7), the three reduce + LayerNorm launches (8, 9, 10) and the
+ * previous layer's last launch (11) -- store each workgroup's first and last device wall-clock tick
+ * (hipDeviceAttributeWallClockRate), one plain store per workgroup; kernel < 0 disables them.
+ * wmx_ctx_probe_stats: the cross attention's average span (ms), steps sampled, ALGORITHMIC bytes of one launch.
+ * wmx_ctx_probe_launches, arrays of 12: span_ms / span_n = average first-workgroup-start .. last-workgroup-end;
+ * e2e_ms / e2e_n (nullable) = average last-workgroup-end minus that of the launch before it in the layer's chain
+ * (dispatch + execution: the per-kernel span rocprofv3 reports, plus the inter-kernel gap); bytes = ALGORITHMIC
+ * bytes of one launch (ids 0-6; 0 for the others). */
 wmx_status wmx_ctx_set_probe(wmx_ctx* c, int kernel, int layer);
 wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
-wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* avg_ms8, double* bytes8, int* n8, float* ev_ms8, int* ev_n8);
+wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* span_ms, double* bytes, int* span_n, float* e2e_ms, int* e2e_n);
 
 #ifdef __cplusplus
 }

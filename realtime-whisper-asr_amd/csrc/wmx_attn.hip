@@ -491,6 +491,7 @@ template <DT T>
 __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
   constexpr int J = 8;  // keys per thread per batch (32 key groups x 8 = 256 keys)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned long long probe_t0 = (a.tprobe && tid == 0) ? probe_clock() : 0ull;  // in-situ probe
   const int h = blockIdx.x;
   const int m = blockIdx.y;  // r * Tn + i
   const int r = m / a.Tn, i = m - r * a.Tn;
@@ -628,6 +629,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
     const float o = (fin[0][tid] + fin[1][tid] + fin[2][tid] + fin[3][tid]) / tot;
     a.o[(long)m * a.d + h * 64 + tid] = from_f32<T>(o);
   }
+  if (a.tprobe && tid == 0) probe_record(a.tprobe, *a.slot0, probe_t0);
 }
 
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st) {

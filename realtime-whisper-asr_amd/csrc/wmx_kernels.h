@@ -179,7 +179,8 @@ int packed_splits(int M, int N, int K, long cap_elems);
 
 // x[m] += bias + sum_s part[s][m]; optionally out16[m] = LayerNorm(x[m]) (g == nullptr: no LN)
 void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float* x, const float* g, const float* b,
-                      uint16_t* out16, int rows, int d, hipStream_t st);
+                      uint16_t* out16, int rows, int d, hipStream_t st, unsigned long long* tprobe = nullptr,
+                      const int* pslot = nullptr);
 void gemm_init_attributes();
 
 // log-mel

@@ -433,6 +433,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_ln_kernel(const float* __r
                                                                 const float* __restrict__ bias, float* __restrict__ x,
                                                                 const float* __restrict__ g, const float* __restrict__ b,
                                                                 uint16_t* __restrict__ out, int d) {
+  // (not probed: the float4 form below is the one the decode step runs)
   constexpr int MAXV = 2;  // d <= 2048
   constexpr int NW = kRedThreads / 64;
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -500,8 +501,11 @@ template <DT T>
 __global__ __launch_bounds__(1024) void reduce_ln4_kernel(const float* __restrict__ part, int S, long pstride,
                                                           const float* __restrict__ bias, float* __restrict__ x,
                                                           const float* __restrict__ g, const float* __restrict__ b,
-                                                          uint16_t* __restrict__ out, int d) {
+                                                          uint16_t* __restrict__ out, int d,
+                                                          unsigned long long* __restrict__ tprobe,
+                                                          const int* __restrict__ pslot) {
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const unsigned long long probe_t0 = (tprobe && tid == 0) ? probe_clock() : 0ull;  // in-situ probe
   __shared__ float red[2][16];
   const int c = tid * 4;
   const bool ok = c < d;
@@ -519,7 +523,10 @@ __global__ __launch_bounds__(1024) void reduce_ln4_kernel(const float* __restric
   for (int u = 0; u < kRedMaxS; ++u) p = make_float4(p.x + t[u].x, p.y + t[u].y, p.z + t[u].z, p.w + t[u].w);
   const float4 v = make_float4(xv.x + bv.x + p.x, xv.y + bv.y + p.y, xv.z + bv.z + p.z, xv.w + bv.w + p.w);
   if (ok) *reinterpret_cast<float4*>(x + (long)m * d + c) = v;
-  if (!g) return;
+  if (!g) {
+    if (tprobe && tid == 0) probe_record(tprobe, *pslot, probe_t0);
+    return;
+  }
   float sum = ok ? (v.x + v.y) + (v.z + v.w) : 0.f;
   sum = wave_sum(sum);
   if (lane == 0) red[0][wave] = sum;
@@ -541,10 +548,12 @@ __global__ __launch_bounds__(1024) void reduce_ln4_kernel(const float* __restric
                      from_f32<T>(q.z * rstd * gg.z + bb.z), from_f32<T>(q.w * rstd * gg.w + bb.w)};
     *reinterpret_cast<u16x4*>(out + (long)m * d + c) = h;
   }
+  if (tprobe && tid == 0) probe_record(tprobe, *pslot, probe_t0);
 }
 
 void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float* x, const float* g, const float* b,
-                      uint16_t* out16, int rows, int d, hipStream_t st) {
+                      uint16_t* out16, int rows, int d, hipStream_t st, unsigned long long* tprobe,
+                      const int* pslot) {
   WMX_CHECK(d <= 2 * kRedThreads && S >= 1 && S <= kRedMaxS, "reduce_ln: width / split count");
   const long pstride = (long)rows * d;
   static const bool legacy = getenv("WMX_REDLN_LEGACY") != nullptr;  // A/B switch for tuning runs
@@ -552,10 +561,10 @@ void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float*
     const int nt = ((d / 4 + 63) / 64) * 64;
     if (dt == DT::BF16)
       hipLaunchKernelGGL(reduce_ln4_kernel<DT::BF16>, dim3(rows), dim3(nt), 0, st, part, S, pstride, bias, x, g, b,
-                         out16, d);
+                         out16, d, tprobe, pslot);
     else
       hipLaunchKernelGGL(reduce_ln4_kernel<DT::F16>, dim3(rows), dim3(nt), 0, st, part, S, pstride, bias, x, g, b,
-                         out16, d);
+                         out16, d, tprobe, pslot);
     WMX_HIP(hipGetLastError());
     return;
   }

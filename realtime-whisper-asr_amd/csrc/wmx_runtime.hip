@@ -443,7 +443,13 @@ struct ResultHolder {
 };
 
 // in-situ probe launch ids (one decoder layer of a decode step)
-enum { kProbeQKV = 0, kProbeOut, kProbeCrossQ, kProbeCrossOut, kProbeFc1, kProbeFc2, kProbeCross, kProbeLaunches = 8 };
+// (the six packed projections and the cross attention carry their algorithmic bytes; the others are probed so that
+// every launch of the layer's chain has an end time: a launch's in-situ duration is its end minus its predecessor's
+// end -- dispatch + execution, the span rocprofv3 reports -- kProbePrev = the previous layer's last launch)
+enum {
+  kProbeQKV = 0, kProbeOut, kProbeCrossQ, kProbeCrossOut, kProbeFc1, kProbeFc2, kProbeCross, kProbeSelf,
+  kProbeRedOut, kProbeRedCrossOut, kProbeRedFc2, kProbePrev, kProbeLaunches = 12
+};
 
 struct Ctx {
   Model* m = nullptr;
@@ -515,14 +521,8 @@ struct Ctx {
   int probe_kernel = -1, probe_layer = 0;
   unsigned long long* probe_buf = nullptr;
   unsigned long long* cur_probe = nullptr;
-  // the same launches bracketed by HIP events captured into the kGraphChunk-step graph (event record nodes):
-  // pev[step in chunk][launch][before, after]; cur_id = the probed launch being issued (-1: none); cap_step = the
-  // step of the chunk graph being captured (-1: not capturing the chunk graph)
-  hipEvent_t pev[8][8][2] = {};
-  int cur_id = -1, cap_step = -1;
-  double ev_ms[8] = {0};
-  int ev_n[8] = {0};
-  double probe_bytes[8] = {0}, wall_khz = 0;
+
+  double probe_bytes[kProbeLaunches] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   float stage_ms[7] = {0};
   int last_steps = 0;
@@ -541,10 +541,6 @@ static void sync_at(Ctx& c, int line) {
 }
 #define sync(c) sync_at(c, __LINE__)
 
-// event record node around a probed launch while the chunk graph is captured (see Ctx::pev)
-static void ev_mark(Ctx& c, int which) {
-  if (c.cur_id >= 0 && c.cap_step >= 0 && c.cap_step < 8) WMX_HIP(hipEventRecord(c.pev[c.cap_step][c.cur_id][which], c.st));
-}
 
 static void alloc_ctx(Ctx& c) {
   const wmx_dims& d = c.m->d;
@@ -752,9 +748,7 @@ static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int 
   g.epi = e;
   g.tprobe = c.cur_probe;
   g.pslot = c.slot;
-  ev_mark(c, 0);
   launch_gemm_packed(c.dt, g, c.st);
-  ev_mark(c, 1);
 }
 
 // decoder projection on packed weights, split-K raw partials into c.part; returns the split count
@@ -774,16 +768,14 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
     g.S = 2;
     WMX_CHECK(2L * M * N <= c.part_elems, "decode gemm: partial buffer too small");
   }
-  ev_mark(c, 0);
   launch_gemm_packed(c.dt, g, c.st);
-  ev_mark(c, 1);
   return g.S;
 }
 
 // decoder projection whose split-K partials feed x += bias + sum; out16 = LN(x) (reduce_ln): one packed launch
 // carrying the reduction and the LayerNorm when the shape allows (RedTail), else the GEMM and reduce_ln
 static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K,
-                         const float* bias, const float* g, const float* b) {
+                         const float* bias, const float* g, const float* b, unsigned long long* redprobe = nullptr) {
   // opt-in (WMX_REDLN_FUSED): measured slower than the separate reduce_ln launch, 798 vs 587 ms per call on the
   // default bench -- the in-launch chain (sc1 partial loads, write-through x, a second arrival, the single
   // normalising workgroup's row loads) costs ~10 us more than the kernel boundary it removes
@@ -809,7 +801,8 @@ static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp
     return;
   }
   const int S2 = gemm_p_part(c, A, lda, Wp, M, N, K);
-  launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st);
+  c.cur_probe = nullptr;
+  launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st, redprobe, c.slot);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -983,15 +976,13 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     DecLayer& L = m.dec[l];
     const bool last = l + 1 == Lt;
     const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
-    auto probe = [&](int id) {
-      c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr;
-      c.cur_id = probed ? id : -1;
-    };
+    const bool prev = c.probe_kernel >= 0 && l + 1 == c.probe_layer;  // its last launch precedes the probed qkv
+    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
+    auto pbuf = [&](int id) { return probed ? c.probe_buf + id * probe_stride : nullptr; };
     // self attention: QKV partials -> (reduce, cache write, attention) -> out-proj partials -> +x, LN2
     probe(kProbeQKV);
     int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt);
     c.cur_probe = nullptr;
-    c.cur_id = -1;
     DecAttnArgs a{};
     a.o = c.dao;
     a.R = R;
@@ -1010,14 +1001,14 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     a.qpart_stride = (long)R * 3 * dt;
     a.qpart_ld = 3 * dt;
     a.qbias = L.bqkv;
+    a.tprobe = pbuf(kProbeSelf);
     launch_self_attn(c.dt, a, c.st);
     probe(kProbeOut);
-    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b);
+    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut));
     // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3
     probe(kProbeCrossQ);
     S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
     c.cur_probe = nullptr;
-    c.cur_id = -1;
     DecAttnArgs x{};
     x.o = c.dao;
     x.R = R;
@@ -1038,21 +1029,17 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
     if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
-    c.cur_id = probed ? (int)kProbeCross : -1;
-    ev_mark(c, 0);
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
-    ev_mark(c, 1);
-    c.cur_id = -1;
     probe(kProbeCrossOut);
-    gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b);
+    gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b, pbuf(kProbeRedCrossOut));
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
     probe(kProbeFc1);
     gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
     probe(kProbeFc2);
     gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
-                 last ? m.lnb : m.dec[l + 1].ln1b);
+                 last ? m.lnb : m.dec[l + 1].ln1b,
+                 probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr);
     c.cur_probe = nullptr;
-    c.cur_id = -1;
   }
 }
 
@@ -1082,9 +1069,7 @@ static void gemm_p_resid(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp
   g.nct = 1;  // unsplit: 16 columns per workgroup (N / 16 workgroups, 16 waves splitting K)
   g.tprobe = c.cur_probe;
   g.pslot = c.slot;
-  ev_mark(c, 0);
   launch_gemm_packed(c.dt, g, c.st);
-  ev_mark(c, 1);
 }
 
 // WMX_DEBUG_SYNC=1 (fault localisation on eager, uncaptured steps): synchronise after each launch of the step
@@ -1111,15 +1096,12 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
     const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
-    auto probe = [&](int id) {
-      c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr;
-      c.cur_id = probed ? id : -1;
-    };
+    const bool prev = c.probe_kernel >= 0 && l + 1 == c.probe_layer;  // its last launch precedes the probed qkv
+    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
     // self attention: x16 . (LN1-folded QKV)^T partials -> (LN1 + reduce, cache write, attention)
     probe(kProbeQKV);
     int S = gemm_p_part(c, c.dhb, dt, L.fqkv, R, 3 * dt, dt);
     c.cur_probe = nullptr;
-    c.cur_id = -1;
     debug_sync(c, "qkv", l);
     DecAttnArgs a{};
     a.o = c.dao;
@@ -1142,6 +1124,7 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
     a.ln_c2 = L.c2qkv;
     a.ln_stats = c.rstat;
     a.ln_ld = R;
+    if (probed) a.tprobe = c.probe_buf + kProbeSelf * probe_stride;
     launch_self_attn(c.dt, a, c.st);
     debug_sync(c, "self_attn", l);
     // out-projection, unsplit: x += o Wo^T + bo, x16, statistics
@@ -1152,7 +1135,6 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
     probe(kProbeCrossQ);
     S = gemm_p_part(c, c.dhb, dt, L.fcq, R, dt, dt);
     c.cur_probe = nullptr;
-    c.cur_id = -1;
     debug_sync(c, "cross_q", l);
     DecAttnArgs x{};
     x.o = c.dao;
@@ -1177,11 +1159,7 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
     if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
-    c.cur_id = probed ? (int)kProbeCross : -1;
-    ev_mark(c, 0);
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
-    ev_mark(c, 1);
-    c.cur_id = -1;
     debug_sync(c, "cross_attn", l);
     probe(kProbeCrossOut);
     gemm_p_resid(c, c.dao, dt, L.wco, R, dt, dt, epi_resid_stats(c, L.bco, R));
@@ -1196,9 +1174,9 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
     gemm_p(c, c.dhb, dt, L.ffc1, R, 4 * dt, dt, e1);
     debug_sync(c, "fc1_fold", l);
     probe(kProbeFc2);
+    if (prev) c.cur_probe = c.probe_buf + kProbePrev * probe_stride;
     gemm_p_resid(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, epi_resid_stats(c, L.bfc2, R));
     c.cur_probe = nullptr;
-    c.cur_id = -1;
     debug_sync(c, "fc2_resid", l);
   }
   launch_layernorm_rows(c.dt, c.dx, nullptr, m.lng, m.lnb, c.dhb, R, dt, c.st);
@@ -1488,11 +1466,7 @@ static void ensure_step_graphs(Ctx& c, int B) {
   for (int gi = 0; gi < 2; ++gi) {
     hipGraph_t gph = nullptr;
     WMX_HIP(hipStreamBeginCapture(c.st, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < (gi ? kGraphChunk : 1); ++i) {
-      c.cap_step = (gi == 1 && c.probe_kernel >= 0) ? i : -1;  // event probes only in the chunk graph
-      run_step(c, B);
-    }
-    c.cap_step = -1;
+    for (int i = 0; i < (gi ? kGraphChunk : 1); ++i) run_step(c, B);
     WMX_HIP(hipStreamEndCapture(c.st, &gph));
     WMX_HIP(hipGraphInstantiate(&c.graph[gi], gph, nullptr, nullptr, 0));
     WMX_HIP(hipGraphDestroy(gph));
@@ -1650,17 +1624,14 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   // ---- decode loop: one hipGraph replay per step ----
   const int need_done = K == 1 ? R : B;
   c.probe_slots[0] = steps > 0 ? Pmax : 0;  // slots of the graph-replayed steps of this call
-  for (int k = 0; k < kProbeLaunches; ++k) {
-    c.ev_ms[k] = 0;
-    c.ev_n[k] = 0;
-  }
+
   if (c.probe_kernel >= 0)  // per-workgroup records of this call only (read after the timed region)
     WMX_HIP(hipMemsetAsync(c.probe_buf, 0, (size_t)kProbeLaunches * T * kProbeWG * 2 * 8, c.st));
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
     const double d = m.d.n_text_state, w2 = 2.0, r = R;
     auto proj = [&](double n, double k) { return n * k * w2 + r * k * w2 + r * n * w2; };
     const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), proj(d, d), proj(d, d), proj(4 * d, d),
-                                      proj(d, 4 * d), (double)B * 1500 * 2 * d * w2 + 2.0 * r * d * w2, 0.0};
+                                      proj(d, 4 * d), (double)B * 1500 * 2 * d * w2 + 2.0 * r * d * w2};
     for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
   if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
@@ -1676,15 +1647,6 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     steps += chunk;
     WMX_HIP(hipMemcpyAsync(c.pinned_i, c.n_done, 4, hipMemcpyDeviceToHost, c.st));
     sync(c);
-    if (c.probe_kernel >= 0 && c.o.use_graph && chunk == kGraphChunk)  // event probes of this chunk replay
-      for (int s8 = 0; s8 < kGraphChunk; ++s8)
-        for (int k = 0; k < kProbeLaunches; ++k) {
-          float ms = 0.f;
-          if (c.pev[s8][k][0] && hipEventElapsedTime(&ms, c.pev[s8][k][0], c.pev[s8][k][1]) == hipSuccess && ms > 0) {
-            c.ev_ms[k] += ms;
-            c.ev_n[k] += 1;
-          }
-        }
 
     if (c.pinned_i[0] >= need_done) break;
   }
@@ -2178,10 +2140,6 @@ void wmx_ctx_destroy(wmx_ctx* x) {
   if (c.pinned_i) (void)hipHostFree(c.pinned_i);
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto& a : c.pev)
-    for (auto& b : a)
-      for (auto& e : b)
-        if (e) (void)hipEventDestroy(e);
   if (c.st) (void)hipStreamDestroy(c.st);
   delete x;
 }
@@ -2565,66 +2523,86 @@ wmx_status wmx_dedup_features(wmx_ctx* x, const float* xh, int64_t stride, const
 wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
   return guard([&] {
     WMX_CHECK(kernel < 1, "probe: 0 enables the decode-step probes, < 0 disables them");
-    WMX_CHECK(layer >= 0 && layer < x->c.m->d.n_text_layer, "probe: layer");
+    WMX_CHECK(layer >= 1 && layer < x->c.m->d.n_text_layer, "probe: layer (>= 1: the previous layer is probed too)");
     Ctx& c = x->c;
-    if (kernel >= 0 && !c.pev[0][0][0])
-      for (auto& a : c.pev)
-        for (auto& b : a)
-          for (auto& e : b) WMX_HIP(hipEventCreate(&e));
     c.probe_kernel = kernel;
     c.probe_layer = layer;
   });
 }
 
-// per probed launch id: average over the decode steps of the last transcribe of (latest workgroup end - earliest
-// workgroup start), from the per-workgroup records
-static void probe_collect(Ctx& c, double* ms, int* n) {
+// per probed launch id, averaged over the decode steps of the last transcribe: span = latest workgroup end -
+// earliest workgroup start (execution only); e2e = its latest workgroup end - that of the launch before it in the
+// layer's chain (dispatch + execution: the per-kernel span rocprofv3 reports, plus the inter-kernel gap)
+static void probe_collect(Ctx& c, double* ms, int* n, double* e2e, int* e2e_n) {
   const int T = c.Tctx;
   std::vector<unsigned long long> tk((size_t)kProbeLaunches * T * kProbeWG * 2);
   WMX_HIP(hipStreamSynchronize(c.st));
   WMX_HIP(hipMemcpy(tk.data(), c.probe_buf, tk.size() * 8, hipMemcpyDeviceToHost));
+  // the chain of one layer's launches (dec_step_fast / dec_step_fold)
+  static const int chain_fast[] = {kProbePrev, kProbeQKV, kProbeSelf, kProbeOut, kProbeRedOut, kProbeCrossQ,
+                                   kProbeCross, kProbeCrossOut, kProbeRedCrossOut, kProbeFc1, kProbeFc2, kProbeRedFc2};
+  static const int chain_fold[] = {kProbePrev, kProbeQKV, kProbeSelf, kProbeOut, kProbeCrossQ, kProbeCross,
+                                   kProbeCrossOut, kProbeFc1, kProbeFc2};
+  const int* chain = c.m->fold ? chain_fold : chain_fast;
+  const int nchain = c.m->fold ? 9 : 12;
   for (int k = 0; k < kProbeLaunches; ++k) {
-    ms[k] = 0;
-    n[k] = 0;
-    for (int sl = c.probe_slots[0]; sl < c.probe_slots[1] && sl < T; ++sl) {
-      unsigned long long lo = ~0ull, hi = 0;
+    ms[k] = e2e[k] = 0;
+    n[k] = e2e_n[k] = 0;
+  }
+  for (int sl = c.probe_slots[0]; sl < c.probe_slots[1] && sl < T; ++sl) {
+    unsigned long long lo[kProbeLaunches], hi[kProbeLaunches];
+    for (int k = 0; k < kProbeLaunches; ++k) {
+      lo[k] = ~0ull;
+      hi[k] = 0;
       const unsigned long long* r = tk.data() + ((size_t)k * T + sl) * kProbeWG * 2;
       for (int w = 0; w < kProbeWG; ++w)
         if (r[2 * w + 1] > r[2 * w] && r[2 * w] != 0) {
-          lo = std::min(lo, r[2 * w]);
-          hi = std::max(hi, r[2 * w + 1]);
+          lo[k] = std::min(lo[k], r[2 * w]);
+          hi[k] = std::max(hi[k], r[2 * w + 1]);
         }
-      if (hi > lo) {
-        ms[k] += (double)(hi - lo) / c.wall_khz;
+      if (hi[k] > lo[k]) {
+        ms[k] += (double)(hi[k] - lo[k]) / c.wall_khz;
         n[k] += 1;
       }
     }
+    for (int i = 1; i < nchain; ++i) {
+      const int k = chain[i], p = chain[i - 1];
+      if (hi[k] > 0 && hi[p] > 0 && hi[k] > hi[p]) {
+        e2e[k] += (double)(hi[k] - hi[p]) / c.wall_khz;
+        e2e_n[k] += 1;
+      }
+    }
+  }
+  for (int k = 0; k < kProbeLaunches; ++k) {
     if (n[k]) ms[k] /= n[k];
+    if (e2e_n[k]) e2e[k] /= e2e_n[k];
   }
 }
 
 wmx_status wmx_ctx_probe_stats(wmx_ctx* x, float* avg_ms, int* n, double* bytes) {
   return guard([&] {
     Ctx& c = x->c;
-    double ms[kProbeLaunches];
-    int cnt[kProbeLaunches];
-    probe_collect(c, ms, cnt);
+    double ms[kProbeLaunches], e2e[kProbeLaunches];
+    int cnt[kProbeLaunches], e2e_n[kProbeLaunches];
+    probe_collect(c, ms, cnt, e2e, e2e_n);
     *n = cnt[kProbeCross];
     *avg_ms = (float)ms[kProbeCross];
     *bytes = c.probe_bytes[kProbeCross];
   });
 }
 
-wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* avg_ms8, double* bytes8, int* n8, float* ev_ms8, int* ev_n8) {
+wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* span_ms, double* bytes, int* span_n, float* e2e_ms, int* e2e_n) {
   return guard([&] {
     Ctx& c = x->c;
-    double ms[kProbeLaunches];
-    probe_collect(c, ms, n8);
+    double ms[kProbeLaunches], e2e[kProbeLaunches];
+    int cnt[kProbeLaunches], en[kProbeLaunches];
+    probe_collect(c, ms, cnt, e2e, en);
     for (int k = 0; k < kProbeLaunches; ++k) {
-      avg_ms8[k] = (float)ms[k];
-      bytes8[k] = c.probe_bytes[k];
-      if (ev_ms8) ev_ms8[k] = c.ev_n[k] ? (float)(c.ev_ms[k] / c.ev_n[k]) : 0.f;
-      if (ev_n8) ev_n8[k] = c.ev_n[k];
+      span_ms[k] = (float)ms[k];
+      bytes[k] = c.probe_bytes[k];
+      span_n[k] = cnt[k];
+      if (e2e_ms) e2e_ms[k] = (float)e2e[k];
+      if (e2e_n) e2e_n[k] = en[k];
     }
   });
 }

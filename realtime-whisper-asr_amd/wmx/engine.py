@@ -310,34 +310,29 @@ class Context:
     KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5, "encoder": 6,
                "dec_qkv": 7, "dec_proj": 8, "dec_fc2": 9, "reduce_ln": 10}
 
-    PROBE_LAUNCHES = ("dec_qkv", "dec_out", "dec_cross_q", "dec_cross_out", "dec_fc1", "dec_fc2", "cross_attn")
+    PROBE_LAUNCHES = ("dec_qkv", "dec_out", "dec_cross_q", "dec_cross_out", "dec_fc1", "dec_fc2", "cross_attn",
+                      "self_attn", "reduce_ln_out", "reduce_ln_cross_out", "reduce_ln_fc2", "prev_layer_last")
 
-    def set_probe(self, on: bool, layer: int = 0):
-        """In-situ probes on the decode-step launches of decoder layer `layer` (the six packed projection GEMMs and
-        the cross attention): every step of every following transcribe records their first-workgroup start and
-        last-workgroup end on the device clock."""
+    def set_probe(self, on: bool, layer: int = 1):
+        """In-situ probes on every launch of decoder layer `layer` (>= 1) and the previous layer's last launch: every
+        step of every following transcribe records each workgroup's first and last device-clock tick."""
         check(lib.wmx_ctx_set_probe(self._h, 0 if on else -1, layer))
 
-    def probe_launches(self, events: bool = False) -> dict:
+    def probe_launches(self, e2e: bool = True) -> dict:
         """{launch: (average in-situ duration ms, samples, algorithmic bytes of one launch)} of the last transcribe:
-        the device-clock workgroup span, or (events=True) the span between the HIP events captured around the
-        launch in the decode graph."""
-        ms = np.zeros(8, np.float32)
-        by = np.zeros(8, np.float64)
-        n = np.zeros(8, np.int32)
-        ems = np.zeros(8, np.float32)
-        en = np.zeros(8, np.int32)
+        e2e = end of the launch minus end of its predecessor in the layer's chain (dispatch + execution, what
+        rocprofv3 reports per kernel); else the first-workgroup-start .. last-workgroup-end span."""
+        n_l = len(self.PROBE_LAUNCHES)
+        ms = np.zeros(n_l, np.float32)
+        by = np.zeros(n_l, np.float64)
+        n = np.zeros(n_l, np.int32)
+        ems = np.zeros(n_l, np.float32)
+        en = np.zeros(n_l, np.int32)
         check(lib.wmx_ctx_probe_launches(self._h, fptr(ms), by.ctypes.data_as(C.POINTER(C.c_double)), iptr(n),
                                          fptr(ems), iptr(en)))
-        if events:
+        if e2e:
             ms, n = ems, en
         return {k: (float(ms[i]), int(n[i]), float(by[i])) for i, k in enumerate(self.PROBE_LAUNCHES)}
-
-    def probe_stats(self):
-        """(average in-situ launch duration ms, samples, algorithmic bytes of one launch) of the last transcribe."""
-        ms, n, by = C.c_float(), C.c_int(), C.c_double()
-        check(lib.wmx_ctx_probe_stats(self._h, C.byref(ms), C.byref(n), C.byref(by)))
-        return float(ms.value), int(n.value), float(by.value)
 
     def bench_kernel(self, kernel: str, batch: int, iters: int = 50):
         """Average launch duration (ms) of one hot-path kernel replayed on the context stream (HIP events),
