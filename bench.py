@@ -72,6 +72,8 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="CPU rehearsal of the launch / rendezvous / broadcast / max-over-ranks plumbing (gloo, no GPU)")
     p.add_argument("--no-stream", action="store_true", help="skip the per-stream process_iter latency lines")
+    p.add_argument("--phase-offset-us", type=float, default=0.0,
+                   help="idle offset of context group g's decode loop: g x this many microseconds")
     return p.parse_args()
 
 
@@ -312,8 +314,9 @@ def main():
     # in-situ probes captured into each context's decode-step graph: device-clock start / end of the six packed
     # projection GEMMs and the cross attention of the middle decoder layer, at every step of the timed decode loops
     probe_layer = model.dims.n_text_layer // 2
-    for c in ctxs:
+    for g, c in enumerate(ctxs):
         c.set_probe(True, probe_layer)
+        c.set_phase_offset(g * args.phase_offset_us)
     for _ in range(args.warmup):
         step()
     if dist is not None:

@@ -232,6 +232,10 @@ wmx_status wmx_dedup_features(wmx_ctx* c, const float* x, int64_t stride, const 
  * (dispatch + execution: the per-kernel span rocprofv3 reports, plus the inter-kernel gap); bytes = ALGORITHMIC
  * bytes of one launch (ids 0-6; 0 for the others). */
 wmx_status wmx_ctx_set_probe(wmx_ctx* c, int kernel, int layer);
+/* context groups decoding concurrently on one GPU run the same launch sequence; an idle offset of `us`
+ * microseconds before this context's decode loop shifts its phase against the other group's, so their HBM-heavy
+ * (cross attention) and latency-bound launches overlap each other instead of coinciding.  0 = none. */
+wmx_status wmx_ctx_set_phase_offset(wmx_ctx* c, double us);
 wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
 wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* span_ms, double* bytes, int* span_n, float* e2e_ms, int* e2e_n);
 

@@ -207,6 +207,8 @@ void launch_unpack_packed(const uint16_t* packed, uint16_t* rowmajor, int N, int
 void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
                      const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,
                      hipStream_t st, float2* stats = nullptr, long stats_ld = 0);
+// one wave idles on the stream for `ticks` device wall-clock ticks (a phase offset between context groups)
+void launch_spin(unsigned long long ticks, hipStream_t st);
 // LayerNorm (g, b) folded into the projection W (+ bias): packed Wp = W diag(g), c1 = Wp 1, c2 = bias + W b
 void launch_fold_ln(DT dt, const uint16_t* Wrm, const float* g, const float* b, const float* bias, int N, int K,
                     uint16_t* Wp, float* c1, float* c2, hipStream_t st);

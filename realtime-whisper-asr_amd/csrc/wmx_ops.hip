@@ -587,6 +587,17 @@ __device__ inline float prng_u(uint64_t key, uint64_t i) {
   return __fsub_rn(__fmul_rn(k, 1.1920928955078125e-7f), 1.0f);
 }
 
+// ---------------- stream phase offset: one wave idles for `ticks` device wall-clock ticks ----------------
+__global__ void spin_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
+void launch_spin(unsigned long long ticks, hipStream_t st) {
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, ticks);
+  WMX_HIP(hipGetLastError());
+}
+
 template <DT T>
 __global__ void init_kernel(uint64_t key, InitSpec s) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < s.n; i += (long)gridDim.x * 256) {

@@ -524,6 +524,7 @@ struct Ctx {
 
   double probe_bytes[kProbeLaunches] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
+  double start_delay_us = 0;    // wmx_ctx_set_phase_offset: idle time before the decode loop (group phase offset)
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -1635,6 +1636,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
   if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
+  if (c.start_delay_us > 0 && steps < max_new) launch_spin((unsigned long long)(c.start_delay_us * c.wall_khz / 1000.0), c.st);
   while (steps < max_new) {
     const int chunk = std::min(kGraphChunk, max_new - steps);
     if (!c.o.use_graph) {
@@ -2517,6 +2519,13 @@ wmx_status wmx_dedup_features(wmx_ctx* x, const float* xh, int64_t stride, const
     launch_dedup_features(c.dsp_io, (long)stride, c.dsp_lens, B, sr, c.dsp_io + n, c.st);
     WMX_HIP(hipMemcpyAsync(out, c.dsp_io + n, (size_t)B * 5 * 4, hipMemcpyDeviceToHost, c.st));
     sync(c);
+  });
+}
+
+wmx_status wmx_ctx_set_phase_offset(wmx_ctx* x, double us) {
+  return guard([&] {
+    WMX_CHECK(us >= 0 && us <= 1e5, "phase offset: 0 .. 100000 us");
+    x->c.start_delay_us = us;
   });
 }
 

@@ -54,7 +54,7 @@ EXPORTS = [
     "wmx_model_arena", "wmx_model_arena_loaded", "wmx_opts_default", "wmx_ctx_create", "wmx_ctx_destroy",
     "wmx_ctx_stream", "wmx_logmel", "wmx_logmel_device", "wmx_encode", "wmx_encode_device",
     "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device", "wmx_result_free",
-    "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches",
+    "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_set_phase_offset",
     "wmx_filtfilt", "wmx_filtfilt_device", "wmx_dedup_features", "wmx_ctx_forced_decode",
     "wmx_ctx_record", "wmx_ctx_recorded", "wmx_debug_packed_launch",
 ]
@@ -98,6 +98,7 @@ def _load():
         "wmx_ctx_stage_ms": (C.c_int, [VP, P(F)]),
         "wmx_ctx_last_steps": (C.c_int, [VP]),
         "wmx_ctx_set_probe": (C.c_int, [VP, C.c_int, C.c_int]),
+        "wmx_ctx_set_phase_offset": (C.c_int, [VP, C.c_double]),
         "wmx_filtfilt": (C.c_int, [VP, P(F), I64, P(I64), C.c_int, P(C.c_double), P(C.c_double), P(C.c_double),
                                    C.c_int, P(F)]),
         "wmx_filtfilt_device": (C.c_int, [VP, VP, I64, P(I64), C.c_int, P(C.c_double), P(C.c_double),

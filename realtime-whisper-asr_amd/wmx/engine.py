@@ -318,6 +318,10 @@ class Context:
         step of every following transcribe records each workgroup's first and last device-clock tick."""
         check(lib.wmx_ctx_set_probe(self._h, 0 if on else -1, layer))
 
+    def set_phase_offset(self, us: float):
+        """Idle `us` microseconds before this context's decode loop (wmx_ctx_set_phase_offset)."""
+        check(lib.wmx_ctx_set_phase_offset(self._h, float(us)))
+
     def probe_launches(self, e2e: bool = True) -> dict:
         """{launch: (average in-situ duration ms, samples, algorithmic bytes of one launch)} of the last transcribe:
         e2e = end of the launch minus end of its predecessor in the layer's chain (dispatch + execution, what
