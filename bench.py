@@ -365,6 +365,8 @@ def main():
     insitu = gather(False)  # first-workgroup-start .. last-workgroup-end
     replay_id = {"dec_qkv": "dec_qkv", "dec_out": "dec_proj", "dec_cross_q": "dec_proj", "dec_cross_out": "dec_proj",
                  "dec_fc1": "dec_fc1", "dec_fc2": "dec_fc2", "cross_attn": "cross_attn"}
+    if evs["dec_cross_q"][1] == 0 and evs["cross_attn"][1] > 0:  # cross-q projection fused into the cross attention
+        del replay_id["dec_cross_q"]
     replay_cache = {}
     for k, rid in replay_id.items():
         if rid not in replay_cache:
@@ -405,6 +407,8 @@ def main():
     roof["layer_step_ms"] = round(ms, 4)
     roof["family_ms_per_layer_step"] = {f: round(v, 4) for f, v in fam_ms.items()}
     roof["replayed_us"] = {k: round(1000 * replay[k][0], 2) for k in fams[dom]}
+    # every probed launch of the layer, end to end (the whole layer-step chain of one group, in launch order)
+    roof["layer_e2e_us"] = {k: round(1000 * v[0], 2) for k, v in evs.items() if v[1] and k != "prev_layer_last"}
     span = sum(insitu[k][0] for k in fams[dom])
     roof["wg_span"] = {"what": f"device-clock span first workgroup start .. last workgroup end, layer {probe_layer}, "
                                f"every timed decode step, both groups", "samples": sum(insitu[k][1] for k in fams[dom]),

@@ -662,7 +662,7 @@ typedef __attribute__((address_space(1))) float gf32;
 // chunk records [nwin][H][KS][nq][66]; one arrival counter per (window, head) in DecAttnArgs::xcnt
 inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long)nwin * H * KS * nq * 66; }
 
-template <DT T, int KPW, int NWV>
+template <DT T, int KPW, int NWV, bool XQ = false>
 __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   constexpr int NT = 64 * NWV;
   const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z % KS, qt = blockIdx.z / KS;
@@ -692,22 +692,75 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, 64 * kXS * 2, 0x00020000);
   // fragment-major images (crossk_off / crossv_off): every load below is one contiguous 1 KiB wave piece
   const int loff = lane * 16;
-  auto load_batch = [&](int kb0) {
+  // 32-key block index kb0 / 32 + b (blocks past the image read as zeros)
+  auto load_k = [&](int kb0) {
 #pragma unroll
-    for (int b = 0; b < KPW; ++b) {
-      const int kbi = (kb0 >> 5) + b;  // 32-key block index (blocks past the image read as zeros)
+    for (int b = 0; b < KPW; ++b)
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
           kf[b][u][hh] = __builtin_bit_cast(
-              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, loff, ((kbi * 2 + u) * 2 + hh) * 1024, 0));
+              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, loff, ((((kb0 >> 5) + b) * 2 + u) * 2 + hh) * 1024, 0));
+  };
+  auto load_v = [&](int kb0) {
+#pragma unroll
+    for (int b = 0; b < KPW; ++b)
 #pragma unroll
       for (int db = 0; db < 4; ++db)
-        vf[b][db] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, loff, (kbi * 4 + db) * 1024, 0));
-    }
+        vf[b][db] = __builtin_bit_cast(
+            u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, loff, (((kb0 >> 5) + b) * 4 + db) * 1024, 0));
   };
-  if (kw0 < kw1) load_batch(kw0);
+  auto load_batch = [&](int kb0) {
+    load_k(kb0);
+    load_v(kb0);
+  };
+  // per-wave fp32 tiles: the fused query projection's K-slice partials here, the softmax combine at the end
+  __shared__ float so[NWV][16][65];
+  // ---- fused cross-q projection (a.wq): the wave's share of the K steps of the 16 x 64 tile q = qin . wq_h^T,
+  //      one MFMA fragment per (k-step, 16-column block) from the packed layout (packed_w_elem / packed_a_elem);
+  //      all of the wave's query-projection loads are issued BEFORE the first K / V batch, so its MFMAs wait only
+  //      for them; rows past the tile repeat its last query (never stored) ----
+  constexpr int QKU = 5;
+  const int qksteps = a.d >> 5;
+  const int qkper = (qksteps + NWV - 1) / NWV;
+  const int qk0 = wave * qkper, qk1 = min(qksteps, qk0 + qkper);
+  u16x8 qav[QKU], qbv[QKU][4];
+  constexpr bool fuse_q = XQ;  // (a.wq != null; the launcher picks the instantiation)
+  if (fuse_q && qk0 < qk1) {
+    const uint16_t* ap = a.qin + ((long)w * nq + i0 + min(fr, nqt - 1)) * a.qin_ld + 8 * g;
+    const uint16_t* wp = a.wq + (((long)h * 4 * qksteps) << 9) + lane * 8;
+#pragma unroll
+    for (int u = 0; u < QKU; ++u) {
+      const int k = min(qk0 + u, qk1 - 1);  // clamped: duplicate loads of the last k-step, MFMAs skipped
+      qav[u] = *reinterpret_cast<const u16x8*>(ap + k * 32);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qbv[u][j] = *reinterpret_cast<const u16x8*>(wp + (((long)j * qksteps + k) << 9));
+    }
+  }
+  // K first (the query projection's MFMAs wait only for their own loads), V after them (needed after QK^T, softmax)
+  if (kw0 < kw1) {
+    if (fuse_q)
+      load_k(kw0);
+    else
+      load_batch(kw0);
+  }
+  if (fuse_q) {
+    f32x4 qa[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) qa[j] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < QKU; ++u)
+      if (qk0 + u < qk1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qa[j] = mfma16<T>(qav[u], qbv[u][j], qa[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) so[wave][4 * g + r][16 * j + fr] = qa[j][r];
+    if (kw0 < kw1) load_v(kw0);
+    __syncthreads();
+  }
 
   // ---- the tile's queries into LDS (bf16/f16), one element per thread: q = bias + sum of the split-K partials in
   //      slice order, or the stored q; pre-scaled by log2(e) / sqrt(64) so the scores come out of the MFMA in
@@ -728,7 +781,12 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     if (q < nqt) {
       const long row = (long)w * nq + i0 + q;
       const int col = h * 64 + e;
-      if (a.qS > 0) {
+      if (fuse_q) {  // the waves' K-slice partials in wave order, + bias
+        float p = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < NWV; ++wv) p += so[wv][q][e];
+        v = from_f32<T>((p + (a.qbias ? a.qbias[col] : 0.f)) * kQScale);
+      } else if (a.qS > 0) {
         const float* src = a.qpart + row * a.qpart_ld + col;
         float tv[8];
 #pragma unroll
@@ -824,7 +882,6 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 
   // ---- combine the NWV waves (LDS), then output or a chunk record ----
   __shared__ float sm[NWV][16], sl[NWV][16];
-  __shared__ float so[NWV][16][65];
   if (g == 0) {
     sm[wave][fr] = m_run;
     sl[wave][fr] = l_run;
@@ -947,6 +1004,20 @@ static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
     const char* v = getenv("WMX_XATTN_WAVES");
     return v && atoi(v) == 4 ? 4 : 8;
   }();
+  // the fused query projection holds a wave's whole K share (<= 5 k-steps) in one load batch
+  WMX_CHECK(!a.wq || (a.d / 32 + 7) / 8 <= 5,
+            "cross attn: fused query projection: model width too large for one load batch per wave");
+  WMX_CHECK(!a.wq || (waves == 8 && nq <= 16), "cross attn: the fused query projection runs on the 8-wave decode kernel");
+  if (a.wq) {
+    const int per_wave = ((chunk + 7) / 8 + 31) / 32;
+    switch (std::min(per_wave, 4)) {
+      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+    }
+    return;
+  }
   if (waves == 8 && nq <= 16) {
     const int per_wave = ((chunk + 7) / 8 + 31) / 32;
     switch (std::min(per_wave, 4)) {
@@ -968,6 +1039,8 @@ static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
 
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {
   WMX_CHECK(a.Tk <= 1500 && a.d == a.H * 64, "cross attn: shape");
+  WMX_CHECK(!a.wq || (a.qin && a.Tn == 1 && a.rows_per_win <= 16 && a.d % 32 == 0 && a.qin_ld >= a.d),
+            "cross attn: fused query projection needs a decode step (one 16-query tile per window)");
   if (dt == DT::BF16)
     launch_cross_t<DT::BF16>(a, ws, st);
   else

@@ -275,6 +275,12 @@ struct DecAttnArgs {
   const float* ln_c2 = nullptr;
   const float2* ln_stats = nullptr;  // [d / 16][ln_ld]
   long ln_ld = 0;
+  // cross attention with the query projection fused (decode, wq != null): the workgroup computes its window-rows'
+  // queries of head h itself, q = qin[row] . wq[64 h .. 64 h + 63]^T + qbias, on MFMA with K split over its waves
+  // (wq packed: packed_index; qin 16-bit [rows][qin_ld])
+  const uint16_t* wq = nullptr;
+  const uint16_t* qin = nullptr;
+  long qin_ld = 0;
   int win_of_row_div;  // row -> window = row / rows_per_win
 };
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);

@@ -525,6 +525,7 @@ struct Ctx {
   double probe_bytes[kProbeLaunches] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   double start_delay_us = 0;    // wmx_ctx_set_phase_offset: idle time before the decode loop (group phase offset)
+  bool xq_fused = false;        // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED)
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -1006,10 +1007,13 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     launch_self_attn(c.dt, a, c.st);
     probe(kProbeOut);
     gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut));
-    // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3
-    probe(kProbeCrossQ);
-    S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
-    c.cur_probe = nullptr;
+    // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3; with c.xq_fused the
+    // cross attention projects its own queries from LN2(x) (no cross-q launch)
+    if (!c.xq_fused) {
+      probe(kProbeCrossQ);
+      S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
+      c.cur_probe = nullptr;
+    }
     DecAttnArgs x{};
     x.o = c.dao;
     x.R = R;
@@ -1027,6 +1031,12 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.qpart_stride = (long)R * dt;
     x.qpart_ld = dt;
     x.qbias = L.bcq;
+    if (c.xq_fused) {
+      x.qS = 0;
+      x.wq = L.wcq;
+      x.qin = c.dhb;
+      x.qin_ld = dt;
+    }
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
     if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
@@ -1631,8 +1641,10 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
     const double d = m.d.n_text_state, w2 = 2.0, r = R;
     auto proj = [&](double n, double k) { return n * k * w2 + r * k * w2 + r * n * w2; };
-    const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), proj(d, d), proj(d, d), proj(4 * d, d),
-                                      proj(d, 4 * d), (double)B * 1500 * 2 * d * w2 + 2.0 * r * d * w2};
+    // (fused cross-q: the cross attention also streams the d x d query weights and reads the LN2 rows)
+    const double xq = c.xq_fused ? d * d * w2 + r * d * w2 : 0.0;
+    const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), c.xq_fused ? 0.0 : proj(d, d), proj(d, d),
+                                      proj(4 * d, d), proj(d, 4 * d), (double)B * 1500 * 2 * d * w2 + 2.0 * r * d * w2 + xq};
     for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
   if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
@@ -2117,6 +2129,7 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       c.o.suppress_tokens = nullptr;
       c.o.alignment_heads = nullptr;
       WMX_HIP(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
+      c.xq_fused = getenv("WMX_XQ_FUSED") != nullptr;
       gemm_init_attributes();
       alloc_ctx(c);
     } catch (...) {
@@ -2574,12 +2587,15 @@ static void probe_collect(Ctx& c, double* ms, int* n, double* e2e, int* e2e_n) {
         n[k] += 1;
       }
     }
-    for (int i = 1; i < nchain; ++i) {
-      const int k = chain[i], p = chain[i - 1];
-      if (hi[k] > 0 && hi[p] > 0 && hi[k] > hi[p]) {
+    // a launch's predecessor is the previous launch of the chain that ran (the fused step has no cross-q launch)
+    for (int i = 1, p = chain[0]; i < nchain; ++i) {
+      const int k = chain[i];
+      if (hi[k] == 0) continue;
+      if (hi[p] > 0 && hi[k] > hi[p]) {
         e2e[k] += (double)(hi[k] - hi[p]) / c.wall_khz;
         e2e_n[k] += 1;
       }
+      p = k;
     }
   }
   for (int k = 0; k < kProbeLaunches; ++k) {
@@ -2643,6 +2659,14 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.rows_per_win = c.K;
       by = (double)B * 1500 * 2 * dt * 2 + 2.0 * R * dt * 2;
       fl = 4.0 * R * 1500 * dt;
+      if (c.xq_fused) {  // the decode step's form: the query projection inside (reads LN2 rows + wcq)
+        a.wq = m.dec[0].wcq;
+        a.qin = c.dhb;
+        a.qin_ld = dt;
+        a.qbias = m.dec[0].bcq;
+        by += (double)dt * dt * 2;
+        fl += 2.0 * R * dt * dt;
+      }
       a.xcnt = c.xa_cnt;
       fn = [&c, a] { launch_cross_attn(c.dt, a, c.xa_ws, c.st); };
     } else if (kernel == 1) {
