@@ -525,7 +525,7 @@ struct Ctx {
   double probe_bytes[kProbeLaunches] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   double start_delay_us = 0;    // wmx_ctx_set_phase_offset: idle time before the decode loop (group phase offset)
-  bool xq_fused = false;        // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED)
+  bool xq_fused = true;         // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED=0: off)
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -1642,8 +1642,9 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     const double d = m.d.n_text_state, w2 = 2.0, r = R;
     auto proj = [&](double n, double k) { return n * k * w2 + r * k * w2 + r * n * w2; };
     // (fused cross-q: the cross attention also streams the d x d query weights and reads the LN2 rows)
-    const double xq = c.xq_fused ? d * d * w2 + r * d * w2 : 0.0;
-    const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), c.xq_fused ? 0.0 : proj(d, d), proj(d, d),
+    const bool xqf = c.xq_fused && !m.fold;  // (the folded step keeps its cross-q launch)
+    const double xq = xqf ? d * d * w2 + r * d * w2 : 0.0;
+    const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), xqf ? 0.0 : proj(d, d), proj(d, d),
                                       proj(4 * d, d), proj(d, 4 * d), (double)B * 1500 * 2 * d * w2 + 2.0 * r * d * w2 + xq};
     for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
@@ -2129,7 +2130,9 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       c.o.suppress_tokens = nullptr;
       c.o.alignment_heads = nullptr;
       WMX_HIP(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
-      c.xq_fused = getenv("WMX_XQ_FUSED") != nullptr;
+      // fused cross-q is the default (397-398 vs 383-384x real time, gpurun_out/r02za); WMX_XQ_FUSED=0 restores the
+      // separate split-K launch (A/B runs)
+      c.xq_fused = !(getenv("WMX_XQ_FUSED") && atoi(getenv("WMX_XQ_FUSED")) == 0);
       gemm_init_attributes();
       alloc_ctx(c);
     } catch (...) {
@@ -2659,7 +2662,7 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.rows_per_win = c.K;
       by = (double)B * 1500 * 2 * dt * 2 + 2.0 * R * dt * 2;
       fl = 4.0 * R * 1500 * dt;
-      if (c.xq_fused) {  // the decode step's form: the query projection inside (reads LN2 rows + wcq)
+      if (c.xq_fused && !m.fold) {  // the decode step's form: the query projection inside (reads LN2 rows + wcq)
         a.wq = m.dec[0].wcq;
         a.qin = c.dhb;
         a.qin_ld = dt;

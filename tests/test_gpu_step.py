@@ -313,3 +313,19 @@ def test_folded_layernorm_step_parity():
            "-k", "not folded_layernorm and not full_depth", "tests/test_gpu_step.py"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_separate_cross_q_step_parity():
+    """The decode step with the cross-q projection as its own split-K launch (WMX_XQ_FUSED=0) instead of inside the
+    cross attention (the default, wmx_attn.hip dec_cross_attn_kernel<..., XQ = true>): the teacher-forced step tests
+    of this file in a child process with the switch set (read at context creation)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WMX_XQ_FUSED="0")
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+           "-k", "forced_steps", "tests/test_gpu_step.py"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
