@@ -409,6 +409,7 @@ def main():
     roof["replayed_us"] = {k: round(1000 * replay[k][0], 2) for k in fams[dom]}
     # every probed launch of the layer, end to end (the whole layer-step chain of one group, in launch order)
     roof["layer_e2e_us"] = {k: round(1000 * v[0], 2) for k, v in evs.items() if v[1] and k != "prev_layer_last"}
+    roof["layer_span_us"] = {k: round(1000 * v[0], 2) for k, v in insitu.items() if v[1] and k != "prev_layer_last"}
     span = sum(insitu[k][0] for k in fams[dom])
     roof["wg_span"] = {"what": f"device-clock span first workgroup start .. last workgroup end, layer {probe_layer}, "
                                f"every timed decode step, both groups", "samples": sum(insitu[k][1] for k in fams[dom]),

@@ -2,7 +2,8 @@
 bench.py's in-situ `roofline`).
 
 Every decode step on a queue is  embed_ln, then per decoder layer  [packed qkv, self attention, packed out,
-reduce_ln, packed cross-q, cross attention, packed cross-out, reduce_ln, packed fc1, packed fc2, reduce_ln],
+reduce_ln, (packed cross-q,) cross attention, packed cross-out, reduce_ln, packed fc1, packed fc2, reduce_ln]
+(no cross-q launch when the cross attention projects its own queries, the default: detected from the count),
 then the packed logits GEMM and the selection kernels (wmx_runtime.hip dec_step_fast / run_step).  The packed
 GEMM launches of a step are labelled by their position; durations are averaged per label over every decode step
 of every queue; algorithmic bytes per launch are those bench.py uses (weights + 16-bit activations in and out).
@@ -14,7 +15,8 @@ import collections
 import csv
 import json
 
-PROJ = ("dec_qkv", "dec_out", "dec_cross_q", "dec_cross_out", "dec_fc1", "dec_fc2")
+PROJ6 = ("dec_qkv", "dec_out", "dec_cross_q", "dec_cross_out", "dec_fc1", "dec_fc2")
+PROJ5 = ("dec_qkv", "dec_out", "dec_cross_out", "dec_fc1", "dec_fc2")  # cross-q fused into the cross attention
 
 
 def main():
@@ -33,6 +35,16 @@ def main():
     dur = collections.defaultdict(list)
     steps = 0
     L = args.layers
+    # packed launches per layer: count them in the first complete step of any queue
+    P = 6
+    for q, ks in byq.items():
+        ks.sort()
+        at = [i for i, k in enumerate(ks) if "embed_ln_kernel" in k[2]]
+        if len(at) >= 2:
+            n_p = sum("gemm_packed_kernel" in k[2] for k in ks[at[0]:at[1]])
+            P = 5 if n_p == 5 * L + 1 else 6
+            break
+    PROJ = PROJ5 if P == 5 else PROJ6
     for q, ks in byq.items():
         ks.sort()
         i, n = 0, len(ks)
@@ -46,9 +58,9 @@ def main():
             while i < n and "embed_ln_kernel" not in ks[i][2] and "logmel" not in ks[i][2]:
                 s, e, name = ks[i]
                 if "gemm_packed_kernel" in name:
-                    if p < 6 * L:
-                        dur[PROJ[p % 6]].append(e - s)
-                    elif p == 6 * L:
+                    if p < P * L:
+                        dur[PROJ[p % P]].append(e - s)
+                    elif p == P * L:
                         dur["logits"].append(e - s)
                     p += 1
                 elif "dec_cross_attn_kernel" in name:
@@ -57,7 +69,7 @@ def main():
                     dur["self_attn"].append(e - s)
                 elif "reduce_ln" in name:
                     dur["reduce_ln"].append(e - s)
-                if p > 6 * L:
+                if p > P * L:
                     break
                 i += 1
     d, R, B = args.d, args.rows, args.windows
@@ -66,7 +78,8 @@ def main():
         return nn * k * 2 + R * k * 2 + R * nn * 2
 
     algo = {"dec_qkv": proj(3 * d, d), "dec_out": proj(d, d), "dec_cross_q": proj(d, d), "dec_cross_out": proj(d, d),
-            "dec_fc1": proj(4 * d, d), "dec_fc2": proj(d, 4 * d), "cross_attn": B * 1500 * 2 * d * 2 + 2 * R * d * 2}
+            "dec_fc1": proj(4 * d, d), "dec_fc2": proj(d, 4 * d), "cross_attn": B * 1500 * 2 * d * 2 + 2 * R * d * 2
+            + (d * d * 2 + R * d * 2 if P == 5 else 0)}
     out = {"decode_steps_seen": steps, "launches": {}}
     for k, v in sorted(dur.items()):
         us = sum(v) / len(v) / 1000.0
