@@ -510,6 +510,9 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
     const int part = tid >> 6, e = tid & 63;
     const int col = part * a.d + h * 64 + e;
     float p = 0.f;
+    // the bias rides in the partials' load batch (the LN-fold branch below holds a barrier the compiler will not
+    // hoist loads across)
+    const float bcol = (tid < 192 && a.qbias && !a.ln_c1) ? a.qbias[col] : 0.f;
     if (tid < 192) {
       const float* src = a.qpart + (long)m * a.qpart_ld + col;
       float t[8];
@@ -527,7 +530,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
     }
     if (tid < 192) {
       const float val = a.ln_c1 ? lnrow.y * (p - lnrow.x * a.ln_c1[col]) + a.ln_c2[col]
-                                : p + (a.qbias ? a.qbias[col] : 0.f);
+                                : p + bcol;
       const uint16_t hv = from_f32<T>(val);
       const float f = to_f32<T>(hv);
       if (part == 0) {
@@ -666,7 +669,9 @@ template <DT T, int KPW, int NWV, bool XQ = false>
 __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   constexpr int NT = 64 * NWV;
   const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z % KS, qt = blockIdx.z / KS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: the K / V buffer loads below take their block offsets in the scalar soffset operand, and
+  // a wave index the compiler cannot prove uniform turns every one of them into a readfirstlane waterfall loop
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, g = lane >> 4;
   const int nq = a.rows_per_win * a.Tn;
   // in-situ probe: this workgroup's start / end, device wall-clock ticks
@@ -727,38 +732,49 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const int qk0 = wave * qkper, qk1 = min(qksteps, qk0 + qkper);
   u16x8 qav[QKU], qbv[QKU][4];
   constexpr bool fuse_q = XQ;  // (a.wq != null; the launcher picks the instantiation)
-  if (fuse_q && qk0 < qk1) {
+  // this thread's query column h 64 + (tid & 63) (the same for both of its elements below): its bias now, not
+  // after the projection's barrier
+  const float qb_col = (fuse_q && a.qbias) ? a.qbias[h * 64 + (tid & 63)] : 0.f;
+  if (fuse_q) {
     const uint16_t* ap = a.qin + ((long)w * nq + i0 + min(fr, nqt - 1)) * a.qin_ld + 8 * g;
     const uint16_t* wp = a.wq + (((long)h * 4 * qksteps) << 9) + lane * 8;
 #pragma unroll
     for (int u = 0; u < QKU; ++u) {
-      const int k = min(qk0 + u, qk1 - 1);  // clamped: duplicate loads of the last k-step, MFMAs skipped
+      // clamped into the matrix (also for a wave with no k-steps): finite duplicate data that meets a zeroed A
+      // fragment below, never uninitialised registers (0 x NaN garbage would poison the tile)
+      const int k = min(qk0 + u, qksteps - 1);
       qav[u] = *reinterpret_cast<const u16x8*>(ap + k * 32);
 #pragma unroll
       for (int j = 0; j < 4; ++j) qbv[u][j] = *reinterpret_cast<const u16x8*>(wp + (((long)j * qksteps + k) << 9));
     }
   }
   // K first (the query projection's MFMAs wait only for their own loads), V after them (needed after QK^T, softmax)
-  if (kw0 < kw1) {
-    if (fuse_q)
-      load_k(kw0);
-    else
-      load_batch(kw0);
-  }
+  // (fused path: unconditional -- a wave without keys reads past the image, zeros by the descriptor's range, and
+  // never uses them; a conditional batch would make the compiler's waits for the projection's loads count as if
+  // the K loads had not been issued, i.e. wait for them too)
+  if (fuse_q)
+    load_k(kw0);
+  else if (kw0 < kw1)
+    load_batch(kw0);
+  __builtin_amdgcn_sched_barrier(0);  // keep the K batch in flight under the projection (the scheduler sinks it)
   if (fuse_q) {
     f32x4 qa[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) qa[j] = f32x4{0, 0, 0, 0};
+    // branch-free: a k-step past the wave's share (clamped duplicate load) multiplies a zeroed A fragment, so no
+    // MFMA is conditional and the compiler's waits stay counted per load
 #pragma unroll
-    for (int u = 0; u < QKU; ++u)
-      if (qk0 + u < qk1)
+    for (int u = 0; u < QKU; ++u) {
+      const u16x8 za = {0, 0, 0, 0, 0, 0, 0, 0};
+      const u16x8 av = qk0 + u < qk1 ? qav[u] : za;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) qa[j] = mfma16<T>(qav[u], qbv[u][j], qa[j]);
+      for (int j = 0; j < 4; ++j) qa[j] = mfma16<T>(av, qbv[u][j], qa[j]);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) so[wave][4 * g + r][16 * j + fr] = qa[j][r];
-    if (kw0 < kw1) load_v(kw0);
+    load_v(kw0);
     __syncthreads();
   }
 
@@ -785,7 +801,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         float p = 0.f;
 #pragma unroll
         for (int wv = 0; wv < NWV; ++wv) p += so[wv][q][e];
-        v = from_f32<T>((p + (a.qbias ? a.qbias[col] : 0.f)) * kQScale);
+        v = from_f32<T>((p + qb_col) * kQScale);
       } else if (a.qS > 0) {
         const float* src = a.qpart + row * a.qpart_ld + col;
         float tv[8];

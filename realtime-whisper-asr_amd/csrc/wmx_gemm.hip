@@ -1300,7 +1300,14 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
   }
 }
 
-template <DT T, int MT, int NCT, int NW, bool TAIL>
+// Epilogue class, a template parameter so each launch carries only the code it runs (these launches are a few
+// microseconds long and start on a cold instruction cache: a generic epilogue switch in a split-K launch measured
+// +0.6 us per launch): kPackedPart split-K raw partials (S > 1); kPackedGelu S == 1 bias + GELU -> 16-bit
+// (decode fc1; bias loaded beside the first k-steps); kPackedGeneric every other S == 1 epilogue; kPackedTail
+// partials + the in-launch reduce / LayerNorm tail (RedTail)
+enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2, kPackedTail = 3 };
+
+template <DT T, int MT, int NCT, int NW, int EPK>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
                                                               int S, Epi e, float* __restrict__ part, RedTail rt,
@@ -1308,6 +1315,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
                                                               const int* __restrict__ pslot) {
   constexpr int KU = packed_ku<MT, NCT>();
   constexpr int LDR = 16 * NCT + 1;
+  constexpr bool TAIL = EPK == kPackedTail;
   constexpr int NT = 64 * NW;
   __shared__ float red[NW][MT * 16][LDR];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1321,6 +1329,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   const int ksteps = K >> 5;
   int ks0, ks1;
   packed_wave_ksteps(K, S, NW, sp, wave, ks0, ks1);
+  // kPackedGelu: a thread's column quad is the same in every row it stores (NT is a multiple of 4 NCT), so its
+  // bias is loaded now, beside the first k-step batch, not as a round trip after the reduction barrier
+  float4 pbias = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (EPK == kPackedGelu)
+    pbias = *reinterpret_cast<const float4*>(e.bias + min(t0 * 16 + (tid % (4 * NCT)) * 4, N - 4));
   f32x4 acc[MT][NCT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -1343,6 +1356,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
 #pragma unroll
       for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + k * 32);
     }
+    // the whole batch is in flight before the first MFMA: without this fence the scheduler may interleave a
+    // load behind an MFMA and wait for it with vmcnt(0), two round trips per batch instead of one (measured +1 us
+    // per split-K launch in one instantiation)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < KU; ++u)
       if (kk + u < ks1)
@@ -1360,8 +1377,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   __syncthreads();
   // 4 consecutive columns per thread
   constexpr int C4 = 4 * NCT;  // column quads per row
-  const bool fold_epi = !TAIL && S == 1 && (e.kind == EPI_RESID_STATS || e.kind == EPI_LNFOLD_GELU16);
-  if (fold_epi) packed_fold_epilogue<T, MT, NCT, NW>(red, e, M, N, K, m0, t0);
+  bool fold_epi = false;
+  if constexpr (EPK == kPackedGeneric) {
+    fold_epi = S == 1 && (e.kind == EPI_RESID_STATS || e.kind == EPI_LNFOLD_GELU16);
+    if (fold_epi) packed_fold_epilogue<T, MT, NCT, NW>(red, e, M, N, K, m0, t0);
+  }
   for (int idx = tid; !fold_epi && idx < MT * 16 * C4; idx += NT) {
     const int row = idx / C4, c = (idx - row * C4) * 4;
     const int m = m0 + row, n = t0 * 16 + c;
@@ -1374,19 +1394,25 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
       for (int w = 1; w < NW; ++w) v += red[w][row][c + q];
       v4[q] = v;
     }
-    if (TAIL) {  // write-through (sc1) so the last arriver on another XCD reads them without an L2 release
+    if constexpr (TAIL) {  // write-through (sc1) so the last arriver on another XCD reads them without an L2 release
       tail_st4(tail_rsrc(part), ((long)sp * M + m) * N + n, make_float4(v4[0], v4[1], v4[2], v4[3]));
-    } else if (S > 1) {
+    } else if constexpr (EPK == kPackedGelu) {  // N and ldc multiples of 4 (host-checked)
+      const u16x4 h = {from_f32<T>(gelu_erf(v4[0] + pbias.x)), from_f32<T>(gelu_erf(v4[1] + pbias.y)),
+                       from_f32<T>(gelu_erf(v4[2] + pbias.z)), from_f32<T>(gelu_erf(v4[3] + pbias.w))};
+      *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
+    } else if (EPK == kPackedPart || S > 1) {
       float* dst = part + ((long)sp * M + m) * N + n;
       if (n + 3 < N && (N & 3) == 0) {
         *reinterpret_cast<float4*>(dst) = make_float4(v4[0], v4[1], v4[2], v4[3]);
       } else {
         for (int q = 0; q < 4 && n + q < N; ++q) dst[q] = v4[q];
       }
-    } else if (n + 3 < N && (e.ldc & 3) == 0) {
-      epi_store4<T>(e, m, n, make_float4(v4[0], v4[1], v4[2], v4[3]));
-    } else {
-      for (int q = 0; q < 4 && n + q < N; ++q) epi_store<T>(e, m, n + q, v4[q]);
+    } else if constexpr (EPK == kPackedGeneric) {
+      if (n + 3 < N && (e.ldc & 3) == 0) {
+        epi_store4<T>(e, m, n, make_float4(v4[0], v4[1], v4[2], v4[3]));
+      } else {
+        for (int q = 0; q < 4 && n + q < N; ++q) epi_store<T>(e, m, n + q, v4[q]);
+      }
     }
   }
   if constexpr (TAIL) packed_red_tail<T, MT, NCT, NW>(rt, part, M, N, S, m0, t0);
@@ -1442,14 +1468,21 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
   const int nw = packed_nw<MT, NCT>(g.K, g.S);
   const bool tail = g.tail.cnt != nullptr;
+  const int epk = tail ? kPackedTail
+                 : g.S > 1 ? kPackedPart
+                 : (g.epi.kind == EPI_GELU16 && g.epi.bias && g.N % 4 == 0 && g.epi.ldc % 4 == 0) ? kPackedGelu
+                                                                                                 : kPackedGeneric;
+#define WMX_PACKED_EPK(NWV, EPKV)                                                                                  \
+  hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, EPKV>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W, g.M, \
+                     g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot)
 #define WMX_PACKED_LAUNCH(NWV)                                                                                     \
   do {                                                                                                             \
-    if (tail)                                                                                                      \
-      hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, true>), grid, dim3(64 * NWV), 0, st, g.A, g.lda,     \
-                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot);                      \
-    else                                                                                                           \
-      hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, false>), grid, dim3(64 * NWV), 0, st, g.A, g.lda,    \
-                         g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot);                      \
+    switch (epk) {                                                                                                 \
+      case kPackedTail: WMX_PACKED_EPK(NWV, kPackedTail); break;                                                   \
+      case kPackedPart: WMX_PACKED_EPK(NWV, kPackedPart); break;                                                   \
+      case kPackedGelu: WMX_PACKED_EPK(NWV, kPackedGelu); break;                                                   \
+      default: WMX_PACKED_EPK(NWV, kPackedGeneric); break;                                                         \
+    }                                                                                                              \
   } while (0)
   constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
   constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
@@ -1461,6 +1494,7 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
     if constexpr (fit16) WMX_PACKED_LAUNCH(16);
   }
 #undef WMX_PACKED_LAUNCH
+#undef WMX_PACKED_EPK
 }
 
 template <int MT, int NCT>

@@ -509,10 +509,14 @@ __global__ __launch_bounds__(1024) void reduce_ln4_kernel(const float* __restric
   __shared__ float red[2][16];
   const int c = tid * 4;
   const bool ok = c < d;
-  float4 t[kRedMaxS], xv = make_float4(0.f, 0.f, 0.f, 0.f), bv = xv;
+  float4 t[kRedMaxS], xv = make_float4(0.f, 0.f, 0.f, 0.f), bv = xv, gg = xv, bb = xv;
   if (ok) {
     xv = *reinterpret_cast<const float4*>(x + (long)m * d + c);
     if (bias) bv = *reinterpret_cast<const float4*>(bias + c);
+    if (g) {  // the LayerNorm parameters ride in the same load batch (not a second round trip after the reductions)
+      gg = *reinterpret_cast<const float4*>(g + c);
+      bb = *reinterpret_cast<const float4*>(b + c);
+    }
   }
 #pragma unroll
   for (int u = 0; u < kRedMaxS; ++u)
@@ -543,7 +547,6 @@ __global__ __launch_bounds__(1024) void reduce_ln4_kernel(const float* __restric
   for (int w2 = 0; w2 < nw; ++w2) tq += red[1][w2];
   const float rstd = 1.0f / sqrtf(tq / d + 1e-5f);
   if (ok) {
-    const float4 gg = *reinterpret_cast<const float4*>(g + c), bb = *reinterpret_cast<const float4*>(b + c);
     const u16x4 h = {from_f32<T>(q.x * rstd * gg.x + bb.x), from_f32<T>(q.y * rstd * gg.y + bb.y),
                      from_f32<T>(q.z * rstd * gg.z + bb.z), from_f32<T>(q.w * rstd * gg.w + bb.w)};
     *reinterpret_cast<u16x4*>(out + (long)m * d + c) = h;
