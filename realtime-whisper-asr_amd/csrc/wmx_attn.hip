@@ -495,8 +495,8 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
   const int h = blockIdx.x;
   const int m = blockIdx.y;  // r * Tn + i
   const int r = m / a.Tn, i = m - r * a.Tn;
-  const int slot_q = *a.slot0 + i;
-  const int beg = a.pad ? a.pad[r] : 0;
+  const int slot_q = load_uniform_i32(a.slot0) + i;
+  const int beg = a.pad ? load_uniform_i32(a.pad + r) : 0;
   const int kg = tid >> 3, c = tid & 7;
   const long kvR = a.kv_R;
   __shared__ float qs[64], kcur[64], vcur[64];

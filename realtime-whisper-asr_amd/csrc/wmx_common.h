@@ -94,6 +94,15 @@ __device__ inline float erf_fast(float z) {
 // gelu(x) = x Phi(x), Phi(x) = 1 - Q(|x|) for x >= 0 and Q(|x|) for x < 0, with Q(a) = 0.5 erfc(a / sqrt 2) from the
 // same A&S 7.1.26 expansion as erf_fast, its constants pre-scaled (1 / sqrt 2 folded into t, 0.5 into the
 // polynomial, log2(e) / 2 into the exponent): 15 VALU ops (2 transcendental) instead of ~19
+// Load of a launch-uniform int that no wave of this launch writes (decode slot, row padding) through the scalar
+// data cache: s_load_dword, waited by lgkmcnt, so it does not order behind (or in front of) the vector loads of the
+// kernel's first batch, and the value is scalar without a readfirstlane.  Read-only use: the scalar cache is
+// invalidated at every dispatch, so the previous launch's stores are seen.
+__device__ __forceinline__ int load_uniform_i32(const int* p) {
+  typedef const __attribute__((address_space(4))) int cint4;
+  return *(cint4*)p;
+}
+
 __device__ inline float gelu_erf(float x) {
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(x), 1.0f));
   float p = fmaf(0.5f * 1.061405429f, t, 0.5f * -1.453152027f);
