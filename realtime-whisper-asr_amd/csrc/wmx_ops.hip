@@ -9,6 +9,17 @@
 namespace wmx {
 
 // ---------------- LayerNorm: one wave per row, two-pass (mean, then centred variance), eps 1e-5 ----------------
+// A wave's share of a row is float4 columns lane + 64 i, i < (n4 + 63) / 64 <= 8.  The trip count is uniform and
+// the addresses are clamped into the row, so every load of the row (and of gamma / beta) is issued in one batch
+// before any use: with per-lane `c < n4` guards the compiler closed each guarded load with a vmcnt(0) wait, one
+// round trip per float4 (16 per row).  Lanes past the row (c >= n4, d % 256 != 0) drop out through selects.
+__device__ __forceinline__ void row_load8(const float4* __restrict__ p, int n4, int lane, float4 (&v)[8]) {
+  const int nit = (n4 + 63) >> 6;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < nit) v[i] = p[min(lane + i * 64, n4 - 1)];
+}
+
 template <DT T>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const int* __restrict__ rows_idx,
                                                         const float* __restrict__ g, const float* __restrict__ bb,
@@ -17,26 +28,22 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows) return;
   const int src = rows_idx ? rows_idx[row] : row;
-  const float4* xr = reinterpret_cast<const float4*>(x + (long)src * d);
-  const int n4 = d >> 2;
-  float4 v[8];  // d <= 2048
+  const int n4 = d >> 2, nit = (n4 + 63) >> 6;  // d <= 2048
+  float4 v[8], gg[8], be[8];
+  row_load8(reinterpret_cast<const float4*>(x + (long)src * d), n4, lane, v);
+  row_load8(reinterpret_cast<const float4*>(g), n4, lane, gg);
+  row_load8(reinterpret_cast<const float4*>(bb), n4, lane, be);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = lane + i * 64;
-    if (c < n4) {
-      v[i] = xr[c];
-      s += v[i].x + v[i].y + v[i].z + v[i].w;
-    }
-  }
+  for (int i = 0; i < 8; ++i)
+    if (i < nit) s += lane + i * 64 < n4 ? (v[i].x + v[i].y) + (v[i].z + v[i].w) : 0.f;
   const float mean = wave_sum(s) / d;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = lane + i * 64;
-    if (c < n4) {
+    if (i < nit) {
       const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, e = v[i].w - mean;
-      q += a * a + b * b + cc * cc + e * e;
+      q += lane + i * 64 < n4 ? a * a + b * b + cc * cc + e * e : 0.f;
     }
   }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / d + 1e-5f);
@@ -44,14 +51,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int c = lane + i * 64;
-    if (c < n4) {
-      const float4 gg = reinterpret_cast<const float4*>(g)[c];
-      const float4 be = reinterpret_cast<const float4*>(bb)[c];
+    if (i < nit && c < n4) {
       u16x4 w;
-      w[0] = from_f32<T>((v[i].x - mean) * rstd * gg.x + be.x);
-      w[1] = from_f32<T>((v[i].y - mean) * rstd * gg.y + be.y);
-      w[2] = from_f32<T>((v[i].z - mean) * rstd * gg.z + be.z);
-      w[3] = from_f32<T>((v[i].w - mean) * rstd * gg.w + be.w);
+      w[0] = from_f32<T>((v[i].x - mean) * rstd * gg[i].x + be[i].x);
+      w[1] = from_f32<T>((v[i].y - mean) * rstd * gg[i].y + be[i].y);
+      w[2] = from_f32<T>((v[i].z - mean) * rstd * gg[i].z + be[i].z);
+      w[3] = from_f32<T>((v[i].w - mean) * rstd * gg[i].w + be[i].w);
       reinterpret_cast<u16x4*>(o)[c] = w;
     }
   }
@@ -82,37 +87,31 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const float* __restr
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows) return;
-  const float4* xr = reinterpret_cast<const float4*>(x + (long)row * d);
-  const int n4 = d >> 2;
-  float4 v[8];  // d <= 2048
+  const int n4 = d >> 2, nit = (n4 + 63) >> 6;  // d <= 2048
+  float4 v[8], gg[8], be[8];  // one load batch (row_load8)
+  row_load8(reinterpret_cast<const float4*>(x + (long)row * d), n4, lane, v);
+  row_load8(reinterpret_cast<const float4*>(g), n4, lane, gg);
+  row_load8(reinterpret_cast<const float4*>(bb), n4, lane, be);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = lane + i * 64;
-    if (c < n4) {
-      v[i] = xr[c];
-      s += v[i].x + v[i].y + v[i].z + v[i].w;
-    }
-  }
+  for (int i = 0; i < 8; ++i)
+    if (i < nit) s += lane + i * 64 < n4 ? (v[i].x + v[i].y) + (v[i].z + v[i].w) : 0.f;
   const float mean = wave_sum(s) / d;
   float qq = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = lane + i * 64;
-    if (c < n4) {
+    if (i < nit) {
       const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, e = v[i].w - mean;
-      qq += a * a + b * b + cc * cc + e * e;
+      qq += lane + i * 64 < n4 ? a * a + b * b + cc * cc + e * e : 0.f;
     }
   }
   const float rstd = 1.0f / sqrtf(wave_sum(qq) / d + 1e-5f);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int c = lane + i * 64;
-    if (c < n4) {  // n4 is a multiple of 8 (d % 32 == 0): a block's 8 lanes are all inside or all outside
-      const float4 gg = reinterpret_cast<const float4*>(g)[c];
-      const float4 be = reinterpret_cast<const float4*>(bb)[c];
-      const float y0 = (v[i].x - mean) * rstd * gg.x + be.x, y1 = (v[i].y - mean) * rstd * gg.y + be.y;
-      const float y2 = (v[i].z - mean) * rstd * gg.z + be.z, y3 = (v[i].w - mean) * rstd * gg.w + be.w;
+    if (i < nit && c < n4) {  // n4 is a multiple of 8 (d % 32 == 0): a block's 8 lanes are all inside or all outside
+      const float y0 = (v[i].x - mean) * rstd * gg[i].x + be[i].x, y1 = (v[i].y - mean) * rstd * gg[i].y + be[i].y;
+      const float y2 = (v[i].z - mean) * rstd * gg[i].z + be[i].z, y3 = (v[i].w - mean) * rstd * gg[i].w + be[i].w;
       const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3)))));
       const float is = mx8_inv_scale(ex);
       reinterpret_cast<uint32_t*>(q + (long)row * d)[c] = mx8_pack4(y0 * is, y1 * is, y2 * is, y3 * is);
