@@ -205,6 +205,11 @@ wmx_status wmx_ctx_recorded(wmx_ctx* c, float* logits, int32_t* sel, int* n_step
  * (end offset), A elements touched (end offset), partial elements written (end offset), k-steps loaded outside the
  * wave's slice}, computed by walking the launch through the kernel's own index helpers (wmx_kernels.h). */
 wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int split, int64_t lda, int64_t* out9);
+/* Host-only (no GPU call): the word-alignment DTW of wmx_transcribe on a caller alignment matrix x[N][ld] (first M
+ * columns; the DTW cost is -x, as openai timing calls dtw(-matrix)), returning the backtraced path (ti[k], tj[k]),
+ * k < *len <= N + M, in path order from (0, 0).
+ * Replaces the reference's openai `timing.dtw_cpu` + `backtrace` (via faster-whisper's find_alignment). */
+wmx_status wmx_debug_dtw(const float* x, int N, int M, int ld, int32_t* ti, int32_t* tj, int* len);
 
 /* ---- pre-ASR DSP of the microphone loop, batched over B streams ----
  * band-pass "vocal separation" (reference vocal_separation.py:335-358, SimpleFilterSeparator.separate):

@@ -2380,6 +2380,20 @@ wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int sp
   });
 }
 
+wmx_status wmx_debug_dtw(const float* x, int N, int M, int ld, int32_t* ti, int32_t* tj, int* len) {
+  return guard([&] {
+    WMX_CHECK(x && ti && tj && len && N >= 1 && M >= 1 && ld >= M, "debug_dtw: arguments");
+    std::vector<int> a, b;
+    dtw(x, N, M, ld, a, b);
+    const int n = (int)a.size();
+    for (int k = 0; k < n; ++k) {  // path order, as dtw() leaves it
+      ti[k] = a[k];
+      tj[k] = b[k];
+    }
+    *len = n;
+  });
+}
+
 wmx_status wmx_ctx_record(wmx_ctx* x, int max_steps) {
   return guard([&] {
     Ctx& c = x->c;

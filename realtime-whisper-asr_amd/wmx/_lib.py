@@ -56,7 +56,7 @@ EXPORTS = [
     "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device", "wmx_result_free",
     "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_set_phase_offset",
     "wmx_filtfilt", "wmx_filtfilt_device", "wmx_dedup_features", "wmx_ctx_forced_decode",
-    "wmx_ctx_record", "wmx_ctx_recorded", "wmx_debug_packed_launch",
+    "wmx_ctx_record", "wmx_ctx_recorded", "wmx_debug_packed_launch", "wmx_debug_dtw",
 ]
 
 
@@ -91,6 +91,7 @@ def _load():
                                             C.c_int]),
         "wmx_ctx_record": (C.c_int, [VP, C.c_int]),
         "wmx_debug_packed_launch": (C.c_int, [C.c_int, C.c_int, C.c_int, I64, C.c_int, I64, P(I64)]),
+        "wmx_debug_dtw": (C.c_int, [P(C.c_float), C.c_int, C.c_int, C.c_int, P(C.c_int32), P(C.c_int32), P(C.c_int)]),
         "wmx_ctx_recorded": (C.c_int, [VP, P(F), P(I32), P(C.c_int), P(C.c_int)]),
         "wmx_transcribe": (C.c_int, [VP, P(F), I64, P(I64), P(I32), C.c_int, P(I32), P(I32), P(P(Result))]),
         "wmx_transcribe_device": (C.c_int, [VP, VP, I64, P(I64), P(I32), C.c_int, P(I32), P(I32), P(P(Result))]),
