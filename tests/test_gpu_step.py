@@ -329,3 +329,38 @@ def test_separate_cross_q_step_parity():
            "-k", "forced_steps", "tests/test_gpu_step.py"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# BASELINE config 1 on the HIP path: Whisper tiny at full depth (4 + 4 layers, d 384, 80 mels), greedy
+# ---------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dt", ["f16", "bf16"])
+def test_full_depth_tiny_greedy(dt):
+    """Config 1's model (tiny) through the whole HIP path: encoder rel-L2, language detection, 24 forced decode
+    steps over 3 windows (every row's logits every step) and the free-running greedy search replayed token-exact."""
+    from wmx import engine as E
+    d = O.DIMS["tiny"]
+    sp = O.special_tokens(d.n_vocab)
+    m = E.Model("tiny", 0, DT[dt]).init_synthetic(3)
+    W = O.make_weights(d, 3, dt)
+    lens = [480000, 200000, 64000]
+    audios = [synth.speech_like(700 + i, n) for i, n in enumerate(lens)]
+    mels = np.stack([O.logmel_segment(a, d.n_mels) for a in audios])
+    encs = [O.encoder(W, d, mel) for mel in mels]
+    ctx = E.Context(m, max_batch=3, beam_size=1, max_new_tokens=48, word_timestamps=False)
+    got = ctx.encode(mels)
+    for b in range(3):
+        e = rel_l2(got[b], encs[b])
+        assert e <= REL[dt], (b, e)
+    n = 24
+    tok, par = _forced_stream(np.random.default_rng(9), n, 3, 1)
+    prefix = [[sp.sot, sp.lang0, sp.transcribe]] * 3
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, d, encs, prefix, tok, par, 1)
+    _check_forced("tiny full depth", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
+    ctx.record(49)
+    res = ctx.transcribe(audios)
+    for b in range(3):
+        assert res[b].language == O.detect_language(W, d, encs[b])[0]
+    opt = O.DecodeOptions(beam_size=1, max_new_tokens=48)
+    _replay_and_compare(f"tiny full depth greedy {dt}", ctx, res, 1, opt, sp, 24)
