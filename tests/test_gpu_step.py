@@ -334,14 +334,15 @@ def test_separate_cross_q_step_parity():
 # ---------------------------------------------------------------------------------------------------------------
 # BASELINE config 1 on the HIP path: Whisper tiny at full depth (4 + 4 layers, d 384, 80 mels), greedy
 # ---------------------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("dt", ["f16", "bf16"])
-def test_full_depth_tiny_greedy(dt):
-    """Config 1's model (tiny) through the whole HIP path: encoder rel-L2, language detection, 24 forced decode
-    steps over 3 windows (every row's logits every step) and the free-running greedy search replayed token-exact."""
+@pytest.mark.parametrize("name,dt", [("tiny", "f16"), ("tiny", "bf16"), ("base", "f16")])
+def test_full_depth_small_models_greedy(name, dt):
+    """Config 1's model (tiny) and config 2's (base, fp16) through the whole HIP path at full depth: encoder rel-L2,
+    language detection, 24 forced decode steps over 3 windows (every row's logits every step) and the free-running
+    greedy search replayed token-exact."""
     from wmx import engine as E
-    d = O.DIMS["tiny"]
+    d = O.DIMS[name]
     sp = O.special_tokens(d.n_vocab)
-    m = E.Model("tiny", 0, DT[dt]).init_synthetic(3)
+    m = E.Model(name, 0, DT[dt]).init_synthetic(3)
     W = O.make_weights(d, 3, dt)
     lens = [480000, 200000, 64000]
     audios = [synth.speech_like(700 + i, n) for i, n in enumerate(lens)]
@@ -357,10 +358,10 @@ def test_full_depth_tiny_greedy(dt):
     prefix = [[sp.sot, sp.lang0, sp.transcribe]] * 3
     top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
     ref_top1, ref_margin, ref_lg = O.forced_rows(W, d, encs, prefix, tok, par, 1)
-    _check_forced("tiny full depth", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
+    _check_forced(f"{name} full depth", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
     ctx.record(49)
     res = ctx.transcribe(audios)
     for b in range(3):
         assert res[b].language == O.detect_language(W, d, encs[b])[0]
     opt = O.DecodeOptions(beam_size=1, max_new_tokens=48)
-    _replay_and_compare(f"tiny full depth greedy {dt}", ctx, res, 1, opt, sp, 24)
+    _replay_and_compare(f"{name} full depth greedy {dt}", ctx, res, 1, opt, sp, 24)
