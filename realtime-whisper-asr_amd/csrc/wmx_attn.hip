@@ -706,7 +706,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh)
           kf[b][u][hh] = __builtin_bit_cast(
-              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, loff, ((((kb0 >> 5) + b) * 2 + u) * 2 + hh) * 1024, 0));
+              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, loff, ((((kb0 >> 5) + b) * 2 + u) * 2 + hh) * 1024, WMX_KV_AUX));
   };
   auto load_v = [&](int kb0) {
 #pragma unroll
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
       for (int db = 0; db < 4; ++db)
         vf[b][db] = __builtin_bit_cast(
-            u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, loff, (((kb0 >> 5) + b) * 4 + db) * 1024, 0));
+            u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, loff, (((kb0 >> 5) + b) * 4 + db) * 1024, WMX_KV_AUX));
   };
   auto load_batch = [&](int kb0) {
     load_k(kb0);
@@ -745,7 +745,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
       const int k = min(qk0 + u, qksteps - 1);
       qav[u] = *reinterpret_cast<const u16x8*>(ap + k * 32);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) qbv[u][j] = *reinterpret_cast<const u16x8*>(wp + (((long)j * qksteps + k) << 9));
+      for (int j = 0; j < 4; ++j) qbv[u][j] = stream_load(reinterpret_cast<const u16x8*>(wp + (((long)j * qksteps + k) << 9)));
     }
   }
   // K first (the query projection's MFMAs wait only for their own loads), V after them (needed after QK^T, softmax)

@@ -16,6 +16,21 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
+// Cache policy of the decode step's once-read streams (MI355X_MICROARCH.md "nt-weights"): WMX_WNT=1 loads the
+// packed decoder weights non-temporally, WMX_KV_AUX=2 sets nt on the cross-K/V buffer loads.  Build-time
+// switches for A/B runs (tools/build_variant.sh); the defaults are what was measured fastest.
+#ifndef WMX_WNT
+#define WMX_WNT 0
+#endif
+#ifndef WMX_KV_AUX
+#define WMX_KV_AUX 0
+#endif
+template <class V>
+__device__ inline V stream_load(const V* p) {
+  if constexpr (WMX_WNT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 struct Error : std::runtime_error {
   int code;
   Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}

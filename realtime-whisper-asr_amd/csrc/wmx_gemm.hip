@@ -1352,7 +1352,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     for (int u = 0; u < KU; ++u) {
       const int k = min(kk + u, ks1 - 1);  // clamped: a duplicate load of the wave's last k-step, MFMA skipped
 #pragma unroll
-      for (int j = 0; j < NCT; ++j) b[u][j] = *reinterpret_cast<const u16x8*>(wt[j] + ((long)k << 9));
+      for (int j = 0; j < NCT; ++j) b[u][j] = stream_load(reinterpret_cast<const u16x8*>(wt[j] + ((long)k << 9)));
 #pragma unroll
       for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + k * 32);
     }
