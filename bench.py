@@ -194,6 +194,27 @@ def stream_latency(name, dtype, seconds, cadence_s, max_new_tokens, vac):
             "max_new_tokens": max_new_tokens, "beam": 5}
 
 
+def vad_bench(streams):
+    """Silero VAD v5 on device (wmx_vad_process, synthetic weights): wall time per call, host audio in, probabilities
+    out, for one VAC tick of this GPU's streams (one 512-sample window each) and a 16-window backlog of 64 streams."""
+    from wmx import synth, vad
+    res = []
+    for S_, W_ in ((streams, 1), (64, 16)):
+        eng = vad.SileroVADEngine(max_streams=S_, max_windows=W_)
+        chunk = {s: synth.speech_like(50 + s, 512 * W_).astype(np.float32) for s in range(S_)}
+        for _ in range(5):
+            eng.process(chunk)
+        n = 50
+        t0 = time.perf_counter()
+        for _ in range(n):
+            eng.process(chunk)
+        us = (time.perf_counter() - t0) / n * 1e6
+        eng.close()
+        res.append({"streams": S_, "windows_per_stream": W_, "us_per_call": round(us, 1),
+                    "windows_per_s": round(S_ * W_ / (us * 1e-6), 1)})
+    return {"calls": res, "note": "wall clock per wmx_vad_process (H2D + 2 launches + D2H + sync), synthetic weights"}
+
+
 def dry_run(args):
     """The multi-rank plumbing of main() without a GPU: gloo rendezvous, the arena broadcast, barrier-bracketed
     timed steps, max over ranks, one JSON line from rank 0 (tests/test_bench_launch.py drives it at world 2)."""
@@ -484,6 +505,11 @@ def main():
         "self_attn_us": round(1000 * kern_stats["self_attn"][0], 2),
         "reduce_ln_us": round(1000 * kern_stats["reduce_ln"][0], 2),
     }
+    try:  # reported beside the headline, never the target
+        out["vad"] = vad_bench(B)
+        log(f"[rank {rank}] silero vad: {out['vad']}")
+    except Exception as e:
+        log(f"[vad] failed: {e!r}")
     if rank == 0 and world == 1 and not args.no_stream:
         # per-stream p50 of process_iter -> transcribe, next to the batched call's latency above
         out["stream_latency"] = []

@@ -226,6 +226,30 @@ wmx_status wmx_filtfilt_device(wmx_ctx* c, const float* x_dev, int64_t stride, c
 wmx_status wmx_dedup_features(wmx_ctx* c, const float* x, int64_t stride, const int64_t* lens, int B, float sr,
                               float* out);
 
+/* ---- Silero VAD v5 (16 kHz) on device, batched over streams ----
+ * Replaces the torch.hub Silero model of asr_components.py:96 as called by whisper_streaming's VADIterator
+ * (`model(x, 16000).item()` per 512 samples, `model.reset_states()`).  A wmx_vad holds the f32 weights and, per
+ * slot (one stream each, up to max_streams), the LSTM state (h, c) and the last 64 input samples.
+ * wmx_vad_set_tensor takes the v5 state-dict names without the `_model.` prefix ("stft.forward_basis_buffer",
+ * "encoder.{0..3}.reparam_conv.{weight,bias}", "decoder.rnn.{weight_ih,weight_hh,bias_ih,bias_hh}",
+ * "decoder.decoder.2.{weight,bias}"), row-major as torch stores them; every tensor must be set before processing.
+ * wmx_vad_process: stream i of S (slot slots[i], distinct) brings nwin * 512 new samples at pcm + i * stride
+ * (host memory); probs[i * nwin + j] = speech probability of its window j, windows run in order (the model's
+ * state and context carry across windows and calls). */
+typedef struct wmx_vad wmx_vad;
+wmx_status wmx_vad_create(int device, int max_streams, int max_windows, wmx_vad** out);
+void wmx_vad_free(wmx_vad* v);
+wmx_status wmx_vad_set_tensor(wmx_vad* v, const char* name, const float* data, int64_t n);
+/* zero the state and context of one slot (slot < 0: all slots) */
+wmx_status wmx_vad_reset(wmx_vad* v, int slot);
+wmx_status wmx_vad_process(wmx_vad* v, const float* pcm, int64_t stride, const int32_t* slots, int S, int nwin,
+                           float* probs);
+/* the same on device buffers (pcm_dev, probs_dev on the VAD's device; slots in host memory), no synchronisation;
+ * the stream it runs on is wmx_vad_stream(v) */
+wmx_status wmx_vad_process_device(wmx_vad* v, const float* pcm_dev, int64_t stride, const int32_t* slots, int S,
+                                  int nwin, float* probs_dev);
+void* wmx_vad_stream(wmx_vad* v);
+
 /* in-situ roofline probes: with kernel = 0, every launch of decoder layer `layer` (>= 1) of every decode step of the
  * timed wmx_transcribe -- the six packed projection GEMMs (ids 0 qkv, 1 out, 2 cross-q, 3 cross-out, 4 fc1, 5 fc2),
  * the cross attention (6), the self attention (7), the three reduce + LayerNorm launches (8, 9, 10) and the

@@ -303,6 +303,21 @@ void launch_filtfilt(const float* x, long xstride, const long* lens_dev, int B, 
 void launch_dedup_features(const float* x, long xstride, const long* lens_dev, int B, float sr, float* feats,
                            hipStream_t st);
 
+// Silero VAD v5, 16 kHz (wmx_vad.hip): f32 weight image, offsets in floats.  The LSTM matrices are stored
+// transposed ([128][512]) so a gate-per-thread read is one contiguous row per k.
+constexpr int kVadWindow = 512, kVadContext = 64, kVadInput = 576, kVadPadded = 640, kVadHidden = 128;
+constexpr long kVadOffBasis = 0;
+constexpr long kVadOffC0w = kVadOffBasis + 258L * 256, kVadOffC0b = kVadOffC0w + 128L * 129 * 3;
+constexpr long kVadOffC1w = kVadOffC0b + 128, kVadOffC1b = kVadOffC1w + 64L * 128 * 3;
+constexpr long kVadOffC2w = kVadOffC1b + 64, kVadOffC2b = kVadOffC2w + 64L * 64 * 3;
+constexpr long kVadOffC3w = kVadOffC2b + 64, kVadOffC3b = kVadOffC3w + 128L * 64 * 3;
+constexpr long kVadOffWihT = kVadOffC3b + 128, kVadOffWhhT = kVadOffWihT + 512L * 128;
+constexpr long kVadOffBih = kVadOffWhhT + 512L * 128, kVadOffBhh = kVadOffBih + 512;
+constexpr long kVadOffW2 = kVadOffBhh + 512, kVadOffB2 = kVadOffW2 + 128;
+constexpr long kVadWeights = kVadOffB2 + 1;
+void launch_vad(const float* W, const float* pcm, long stride, float* ctx, float* state, const int* slots_dev, int S,
+                int nwin, float* enc, float* probs, hipStream_t st);
+
 // weights
 struct InitSpec {
   int tid;

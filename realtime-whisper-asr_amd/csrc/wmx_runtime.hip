@@ -2788,3 +2788,169 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
 }
 
 }  // extern "C"
+
+// ---- Silero VAD (wmx_vad.hip) ----
+struct wmx_vad {
+  int device = 0, max_streams = 0, max_windows = 0;
+  hipStream_t st = nullptr;
+  char* base = nullptr;  // one allocation: weights, state, context, pcm staging, encoder outputs, probs, slots
+  float *W = nullptr, *state = nullptr, *ctx = nullptr, *pcm = nullptr, *enc = nullptr, *probs = nullptr;
+  int* slots = nullptr;
+  unsigned loaded = 0;  // bit per tensor of vad_tensors()
+};
+
+namespace {
+struct VadTensor {
+  const char* name;
+  long n, off;
+  int transpose_rows;  // > 0: [rows][n / rows] stored transposed
+};
+const std::vector<VadTensor>& vad_tensors() {
+  static const std::vector<VadTensor> t = {
+      {"stft.forward_basis_buffer", 258L * 256, kVadOffBasis, 0},
+      {"encoder.0.reparam_conv.weight", 128L * 129 * 3, kVadOffC0w, 0},
+      {"encoder.0.reparam_conv.bias", 128, kVadOffC0b, 0},
+      {"encoder.1.reparam_conv.weight", 64L * 128 * 3, kVadOffC1w, 0},
+      {"encoder.1.reparam_conv.bias", 64, kVadOffC1b, 0},
+      {"encoder.2.reparam_conv.weight", 64L * 64 * 3, kVadOffC2w, 0},
+      {"encoder.2.reparam_conv.bias", 64, kVadOffC2b, 0},
+      {"encoder.3.reparam_conv.weight", 128L * 64 * 3, kVadOffC3w, 0},
+      {"encoder.3.reparam_conv.bias", 128, kVadOffC3b, 0},
+      {"decoder.rnn.weight_ih", 512L * 128, kVadOffWihT, 512},
+      {"decoder.rnn.weight_hh", 512L * 128, kVadOffWhhT, 512},
+      {"decoder.rnn.bias_ih", 512, kVadOffBih, 0},
+      {"decoder.rnn.bias_hh", 512, kVadOffBhh, 0},
+      {"decoder.decoder.2.weight", 128, kVadOffW2, 0},
+      {"decoder.decoder.2.bias", 1, kVadOffB2, 0},
+  };
+  return t;
+}
+
+void vad_check_call(wmx_vad* v, int64_t stride, const int32_t* slots, int S, int nwin) {
+  WMX_CHECK(v && slots, "null argument");
+  WMX_CHECK(v->loaded == (1u << vad_tensors().size()) - 1, "vad: weights not fully loaded (wmx_vad_set_tensor)");
+  WMX_CHECK(S >= 1 && S <= v->max_streams, "vad: stream count out of range");
+  WMX_CHECK(nwin >= 1 && nwin <= v->max_windows, "vad: window count out of range");
+  WMX_CHECK(stride >= (int64_t)nwin * kVadWindow, "vad: stride shorter than nwin * 512 samples");
+  std::vector<char> seen(v->max_streams, 0);
+  for (int i = 0; i < S; ++i) {
+    WMX_CHECK(slots[i] >= 0 && slots[i] < v->max_streams, "vad: slot out of range");
+    WMX_CHECK(!seen[slots[i]], "vad: a slot appears twice in one call");
+    seen[slots[i]] = 1;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+wmx_status wmx_vad_create(int device, int max_streams, int max_windows, wmx_vad** out) {
+  return guard([&] {
+    WMX_CHECK(out && max_streams >= 1 && max_windows >= 1 && max_streams <= 65536 && max_windows <= 4096,
+              "vad: bad sizes");
+    auto* v = new wmx_vad();
+    try {
+      v->device = device;
+      v->max_streams = max_streams;
+      v->max_windows = max_windows;
+      WMX_HIP(hipSetDevice(device));
+      WMX_HIP(hipStreamCreateWithFlags(&v->st, hipStreamNonBlocking));
+      const size_t MS = max_streams, MW = max_windows;
+      const size_t nW = (kVadWeights + 63) / 64 * 64, nS = MS * 2 * kVadHidden, nC = MS * kVadContext,
+                   nP = MS * MW * kVadWindow, nE = MS * MW * kVadHidden, nPr = MS * MW;
+      const size_t floats = nW + nS + nC + nP + nE + (nPr + 63) / 64 * 64;
+      WMX_HIP(hipMalloc(&v->base, floats * 4 + MS * 4));
+      WMX_HIP(hipMemset(v->base, 0, floats * 4 + MS * 4));
+      float* f = (float*)v->base;
+      v->W = f;
+      v->state = f + nW;
+      v->ctx = v->state + nS;
+      v->pcm = v->ctx + nC;
+      v->enc = v->pcm + nP;
+      v->probs = v->enc + nE;
+      v->slots = (int*)(f + floats);
+    } catch (...) {
+      if (v->base) (void)hipFree(v->base);
+      if (v->st) (void)hipStreamDestroy(v->st);
+      delete v;
+      throw;
+    }
+    *out = v;
+  });
+}
+
+void wmx_vad_free(wmx_vad* v) {
+  if (!v) return;
+  (void)hipSetDevice(v->device);
+  if (v->base) (void)hipFree(v->base);
+  if (v->st) (void)hipStreamDestroy(v->st);
+  delete v;
+}
+
+void* wmx_vad_stream(wmx_vad* v) { return v ? (void*)v->st : nullptr; }
+
+wmx_status wmx_vad_set_tensor(wmx_vad* v, const char* name, const float* data, int64_t n) {
+  return guard([&] {
+    WMX_CHECK(v && name && data, "null argument");
+    const auto& ts = vad_tensors();
+    for (size_t i = 0; i < ts.size(); ++i) {
+      if (std::string(name) != ts[i].name) continue;
+      WMX_CHECK(n == ts[i].n, std::string("vad: size mismatch for ") + name);
+      std::vector<float> img(data, data + n);
+      if (ts[i].transpose_rows > 0) {  // [rows][cols] -> [cols][rows]
+        const long rows = ts[i].transpose_rows, cols = n / rows;
+        for (long r = 0; r < rows; ++r)
+          for (long c = 0; c < cols; ++c) img[c * rows + r] = data[r * cols + c];
+      }
+      WMX_HIP(hipSetDevice(v->device));
+      WMX_HIP(hipMemcpy(v->W + ts[i].off, img.data(), n * 4, hipMemcpyHostToDevice));
+      v->loaded |= 1u << i;
+      return;
+    }
+    WMX_CHECK(false, std::string("vad: unknown tensor ") + name);
+  });
+}
+
+wmx_status wmx_vad_reset(wmx_vad* v, int slot) {
+  return guard([&] {
+    WMX_CHECK(v && slot < v->max_streams, "vad: slot out of range");
+    WMX_HIP(hipSetDevice(v->device));
+    if (slot < 0) {
+      WMX_HIP(hipMemsetAsync(v->state, 0, (size_t)v->max_streams * 2 * kVadHidden * 4, v->st));
+      WMX_HIP(hipMemsetAsync(v->ctx, 0, (size_t)v->max_streams * kVadContext * 4, v->st));
+    } else {
+      WMX_HIP(hipMemsetAsync(v->state + (size_t)slot * 2 * kVadHidden, 0, 2 * kVadHidden * 4, v->st));
+      WMX_HIP(hipMemsetAsync(v->ctx + (size_t)slot * kVadContext, 0, kVadContext * 4, v->st));
+    }
+    WMX_HIP(hipStreamSynchronize(v->st));
+  });
+}
+
+wmx_status wmx_vad_process_device(wmx_vad* v, const float* pcm_dev, int64_t stride, const int32_t* slots, int S,
+                                  int nwin, float* probs_dev) {
+  return guard([&] {
+    vad_check_call(v, stride, slots, S, nwin);
+    WMX_CHECK(pcm_dev && probs_dev, "null argument");
+    WMX_HIP(hipSetDevice(v->device));
+    // the slot table is rewritten below: an earlier call's launches on this stream must have read it
+    WMX_HIP(hipStreamSynchronize(v->st));
+    WMX_HIP(hipMemcpyAsync(v->slots, slots, (size_t)S * 4, hipMemcpyHostToDevice, v->st));
+    launch_vad(v->W, pcm_dev, (long)stride, v->ctx, v->state, v->slots, S, nwin, v->enc, probs_dev, v->st);
+  });
+}
+
+wmx_status wmx_vad_process(wmx_vad* v, const float* pcm, int64_t stride, const int32_t* slots, int S, int nwin,
+                           float* probs) {
+  return guard([&] {
+    vad_check_call(v, stride, slots, S, nwin);
+    WMX_CHECK(pcm && probs, "null argument");
+    WMX_HIP(hipSetDevice(v->device));
+    const long row = (long)nwin * kVadWindow;
+    WMX_HIP(hipMemcpy2DAsync(v->pcm, row * 4, pcm, (size_t)stride * 4, row * 4, S, hipMemcpyHostToDevice, v->st));
+    WMX_HIP(hipMemcpyAsync(v->slots, slots, (size_t)S * 4, hipMemcpyHostToDevice, v->st));
+    launch_vad(v->W, v->pcm, row, v->ctx, v->state, v->slots, S, nwin, v->enc, v->probs, v->st);
+    WMX_HIP(hipMemcpyAsync(probs, v->probs, (size_t)S * nwin * 4, hipMemcpyDeviceToHost, v->st));
+    WMX_HIP(hipStreamSynchronize(v->st));
+  });
+}
+
+}  // extern "C"

@@ -57,6 +57,8 @@ EXPORTS = [
     "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_set_phase_offset",
     "wmx_filtfilt", "wmx_filtfilt_device", "wmx_dedup_features", "wmx_ctx_forced_decode",
     "wmx_ctx_record", "wmx_ctx_recorded", "wmx_debug_packed_launch", "wmx_debug_dtw",
+    "wmx_vad_create", "wmx_vad_free", "wmx_vad_set_tensor", "wmx_vad_reset", "wmx_vad_process",
+    "wmx_vad_process_device", "wmx_vad_stream",
 ]
 
 
@@ -108,6 +110,13 @@ def _load():
         "wmx_ctx_probe_stats": (C.c_int, [VP, P(F), P(C.c_int), P(C.c_double)]),
         "wmx_ctx_probe_launches": (C.c_int, [VP, P(F), P(C.c_double), P(C.c_int), P(F), P(C.c_int)]),
         "wmx_ctx_bench_kernel": (C.c_int, [VP, C.c_int, C.c_int, C.c_int, P(F), P(C.c_double), P(C.c_double)]),
+        "wmx_vad_create": (C.c_int, [C.c_int, C.c_int, C.c_int, P(VP)]),
+        "wmx_vad_free": (None, [VP]),
+        "wmx_vad_set_tensor": (C.c_int, [VP, C.c_char_p, P(F), I64]),
+        "wmx_vad_reset": (C.c_int, [VP, C.c_int]),
+        "wmx_vad_process": (C.c_int, [VP, P(F), I64, P(I32), C.c_int, C.c_int, P(F)]),
+        "wmx_vad_process_device": (C.c_int, [VP, VP, I64, P(I32), C.c_int, C.c_int, VP]),
+        "wmx_vad_stream": (VP, [VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

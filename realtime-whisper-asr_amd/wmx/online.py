@@ -423,6 +423,9 @@ class DynamicVACOnlineASRProcessor(VACOnlineASRProcessor):
     def __init__(self, online_chunk_size, asr, tokenizer=None, logfile=sys.stderr, buffer_trimming=("segment", 15),
                  initial_silence_ms=500, min_silence_ms=200, max_silence_ms=1000, vad_threshold=0.5, vad_model=None,
                  online=None):
+        if isinstance(vad_model, str):  # "silero" (synthetic weights) or a Silero v5 .safetensors path
+            from .vad import silero_model
+            vad_model = silero_model(vad_model)
         vad = DynamicVADIterator(vad_model or EnergyVAD(), initial_silence_ms, min_silence_ms, max_silence_ms,
                                  vad_threshold)
         super().__init__(online_chunk_size, asr, tokenizer=tokenizer, buffer_trimming=buffer_trimming,
@@ -612,6 +615,9 @@ class EnhancedVACOnlineASRProcessor(VACOnlineASRProcessor):
         online = EnhancedOnlineASRProcessor(asr=asr, tokenizer=tokenizer, logfile=logfile,
                                             buffer_trimming=buffer_trimming, agreement_n=agreement_n,
                                             enable_dynamic_buffer=enable_dynamic_buffer)
+        if isinstance(vad_model, str):  # "silero" (synthetic weights) or a Silero v5 .safetensors path
+            from .vad import silero_model
+            vad_model = silero_model(vad_model)
         vad = DynamicVADIterator(vad_model or EnergyVAD(), initial_silence_ms, min_silence_ms, max_silence_ms,
                                  vad_threshold)
         super().__init__(online_chunk_size, asr, tokenizer=tokenizer, buffer_trimming=buffer_trimming,
