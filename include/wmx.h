@@ -82,6 +82,13 @@ typedef struct {
   int32_t median_filter_width;       /* 7 */
   int32_t use_graph;                 /* capture the decode step in a hipGraph */
   int32_t max_audio_samples;         /* longest pcm per window accepted (default 480000) */
+  /* temperature > 0: faster-whisper's sampling branch (generate_with_fallback: beam_size 1, num_hypotheses = best_of,
+   * sampling_topk 0, sampling_temperature = temperature): best_of independent rows per window, each drawing its next
+   * token from softmax(rule-masked logits / temperature) by Gumbel-max on a counter-based hash of (sample_seed, row,
+   * slot, token); the window keeps the row with the best sum_logprob / length.  beam_size is ignored then. */
+  float temperature;                 /* 0 = deterministic search (default) */
+  int32_t best_of;                   /* rows per window when sampling, 1..8 (faster-whisper default 5) */
+  uint32_t sample_seed;
 } wmx_opts;
 
 /* per-window result of wmx_transcribe */

@@ -800,6 +800,73 @@ def search_replay(logits, sel, K: int, sp: Special, opt: DecodeOptions, eps: flo
     return out
 
 
+def sample_gumbel(seed: int, row: int, slot: int, toks) -> np.ndarray:
+    """The device's sampling noise (csrc/wmx_decode.hip sample_gumbel), bit for bit up to the two f32 logs:
+    splitmix64 of ((row * 1024 + slot) * 65536 + token) + seed * 0x9E3779B97F4A7C15, u = (top 23 bits * 2 + 1) / 2^25,
+    Gumbel = -log(-log(u)) in float32."""
+    g = np.uint64(0x9E3779B97F4A7C15)
+    with np.errstate(over="ignore"):
+        t = np.asarray(toks, np.uint64)
+        base = (np.uint64(row) * np.uint64(1024) + np.uint64(slot)) * np.uint64(65536)
+        z = t + base + np.array([seed], np.uint64) * g
+        z = z + g
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = ((z >> np.uint64(41)).astype(np.uint32) * np.uint32(2) + np.uint32(1)).astype(np.float32) * np.float32(2.0 ** -25)
+    return -np.log(-np.log(u))
+
+
+def sampling_replay(logits, sel, K: int, sp: Special, opt: DecodeOptions, temperature: float, seed: int, slot0: int,
+                    eps: float = 1e-3):
+    """faster-whisper's T > 0 branch (CT2 generate with beam_size 1, num_hypotheses = best_of = K, sampling_topk 0,
+    sampling_temperature = T), replayed on the recorded logits of wmx_ctx_record: every row independently draws
+    argmax(rule-masked logits / T + Gumbel) with the device's noise (sample_gumbel, slot = slot0 + step), accumulates
+    the rule-masked log-softmax of the UNSCALED logits (openai DecodingTask: logprobs before the temperature), and
+    each window keeps the row with the best sum_logprob / length.  A draw that differs from the device's at a step
+    whose top-2 key gap is <= eps is an f32 tie and ends that row's comparison.  Returns per window
+    dict(rows=[dict(steps, ties, mismatch, tokens, total, finished)], best=(row, tokens, total) or None)."""
+    n, R, V = logits.shape
+    inv_t = np.float32(1.0 / temperature)
+    out = []
+    for b in range(R // K):
+        rows = []
+        for j in range(K):
+            r = b * K + j
+            info = dict(steps=0, ties=False, mismatch=None, tokens=[], total=0.0, finished=False)
+            for i in range(n):
+                dev = tuple(sel[i][r])
+                if dev[0] < 0:
+                    break
+                x = apply_rules(logits[i][r], info["tokens"], sp, opt)
+                ok = np.isfinite(x)
+                key = np.full(V, -np.inf, np.float32)
+                key[ok] = x[ok].astype(np.float32) * inv_t + sample_gumbel(seed, r, slot0 + i, np.nonzero(ok)[0])
+                order = np.argsort(-key, kind="stable")
+                tok = int(order[0])
+                gap = min(float(key[order[0]] - key[order[1]]), _ts_rule_gap(logits[i][r], sp, opt))
+                if tok != dev[1]:
+                    if gap <= eps:
+                        info["ties"] = True
+                    else:
+                        info["mismatch"] = (i, tok, dev[1])
+                    break
+                info["steps"] += 1
+                info["total"] += float(log_softmax(x)[tok])
+                if tok == sp.eot:
+                    info["finished"] = True
+                    break
+                info["tokens"].append(tok)
+            rows.append(info)
+        best = None
+        if not any(rw["ties"] or rw["mismatch"] for rw in rows):
+            sc = [rw["total"] / max(len(rw["tokens"]), 1) for rw in rows]
+            jb = int(np.argmax(sc))
+            best = (jb, rows[jb]["tokens"], rows[jb]["total"])
+        out.append(dict(rows=rows, best=best))
+    return out
+
+
 def rank_final(finished, alive, K: int, length_penalty=None):
     """openai BeamSearchDecoder.finalize (fill the finished list from the best alive beams) +
     MaximumLikelihoodRanker; returns (tokens, sum_logprob, ranking margin to the runner-up)."""

@@ -10,6 +10,10 @@ struct RuleOpts {
   int max_init;          // -1 = none
   int without_ts;
   const uint32_t* mask;  // suppress-token bitmask [ceil(V/32)]
+  // sampling (temperature > 0): selection key = logit / T + Gumbel(hash(seed, row, *slot, token)); inv_temp 0 = off
+  float inv_temp = 0.f;
+  uint32_t seed = 0;
+  const int* slot = nullptr;
 };
 
 struct RowPtrs {  // per-row decode state (device arrays of R)

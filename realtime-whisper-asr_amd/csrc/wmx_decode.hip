@@ -256,13 +256,29 @@ __device__ inline void block_topk(TopK& t, int KP, float* ov, int* oi, float* rv
   }
 }
 
+// sampling noise: splitmix64 of the counter ((row * 1024 + slot) * 65536 + token) offset by seed * golden ratio;
+// u = (top 23 bits * 2 + 1) / 2^25 in (0, 1), exact in f32; Gumbel = -log(-log(u)).  Restated bit for bit by
+// oracle/whisper_np.py::sample_gumbel (the replay test).
+__device__ inline float sample_gumbel(uint32_t seed, int row, int slot, int tok) {
+  uint64_t z = ((uint64_t)row * 1024u + (uint64_t)slot) * 65536u + (uint64_t)tok + (uint64_t)seed * 0x9E3779B97F4A7C15ull;
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)((uint32_t)(z >> 41) * 2u + 1u) * 2.98023223876953125e-8f;  // 2^-25
+  return -logf(-logf(u));
+}
+
 // workspace per (row, slice): [0..4] stats (text.m, text.s, ts.m, ts.s, text max), then KP text (v,i), KP ts (v,i)
 __device__ inline int sel_ws_stride(int KP) { return 5 + 4 * KP; }
 
-template <int KP>
+// SAMPLE: the top-KP lists rank tokens by the sampling key logit / T + Gumbel noise (KP = 1: the Gumbel-max sample);
+// the statistics stay on the raw logits (log-probabilities and the timestamp rule, as openai / CT2 compute them)
+template <int KP, bool SAMPLE = false>
 __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict__ logits, int ldl, RuleOpts o,
                                                          RowState rs, const int* row_map, float* __restrict__ ws) {
   const int r = blockIdx.x, sl = blockIdx.y;
+  const int sample_slot = SAMPLE ? *o.slot : 0;
   const int lrow = row_map ? row_map[r] : r;
   const float* x = logits + (long)lrow * ldl;
   const int ns = rs.ns[r], lt = rs.last[r], pt = rs.pen[r], lts = rs.last_ts[r];
@@ -294,13 +310,14 @@ __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict
       const bool ok = t < o.V && !((mw[u] >> (t & 31)) & 1u) && allowed_rules(o, t, ns, last_ts, pen_ts, lts);
       const float v = ok ? (hh ? xv[u].y : xv[u].x) : -INFINITY;
       const int ti = ok ? t : 0x7FFFFFFF;
+      const float key = SAMPLE ? (ok ? v * o.inv_temp + sample_gumbel(o.seed, r, sample_slot, t) : -INFINITY) : v;
       if (t < o.tb) {  // wave-uniform except in the slice that holds timestamp_begin
         text = ms_add_nb(text, v);
         tmax = fmaxf(tmax, v);
-        topk_push_c<KP>(ktx, v, ti);
+        topk_push_c<KP>(ktx, key, ti);
       } else {
         ts = ms_add_nb(ts, v);
-        topk_push_c<KP>(kts, v, ti);
+        topk_push_c<KP>(kts, key, ti);
       }
     }
   }
@@ -352,9 +369,11 @@ __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict
 }
 
 // ---- phase B: one wave per row merges the slices: timestamp-forcing rule, log-softmax normaliser, top-KP ----
-template <int KP>
+template <int KP, bool SAMPLE = false>
 __global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ ws, RuleOpts o,
-                                                      int* __restrict__ out_tok, float* __restrict__ out_lp) {
+                                                      int* __restrict__ out_tok, float* __restrict__ out_lp,
+                                                      const float* __restrict__ logits, int ldl,
+                                                      const int* __restrict__ row_map) {
   static_assert(kSlices <= 64, "one lane per slice");
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
@@ -401,7 +420,12 @@ __global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ 
     const int bi = oi[lane];
     const float bv = ov[lane];
     out_tok[r * KP + lane] = bi == 0x7FFFFFFF ? o.eot : bi;
-    out_lp[r * KP + lane] = bv == -INFINITY ? -INFINITY : bv - lse_all;
+    if (SAMPLE) {  // bv is the sampling key: the log-probability comes from the raw logit of the drawn token
+      const int lrow = row_map ? row_map[r] : r;
+      out_lp[r * KP + lane] = bi == 0x7FFFFFFF ? -INFINITY : logits[(long)lrow * ldl + bi] - lse_all;
+    } else {
+      out_lp[r * KP + lane] = bv == -INFINITY ? -INFINITY : bv - lse_all;
+    }
   }
 }
 
@@ -788,11 +812,18 @@ void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const
   WMX_CHECK(KP <= kMaxKP, "beam too large");
   WMX_CHECK(o.V <= kSlices * kSelPer && ldl % 2 == 0, "logits select: vocabulary / row stride");
   RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
+  if (o.inv_temp > 0.f) {  // sampling: one Gumbel-max draw per row
+    WMX_CHECK(KP == 1 && o.slot, "logits select: sampling draws one token per row");
+    hipLaunchKernelGGL((logits_select_a<1, true>), dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, row_map, ws);
+    hipLaunchKernelGGL((logits_select_b<1, true>), dim3(R), dim3(64), 0, st, ws, o, tok, lp, logits, ldl, row_map);
+    WMX_HIP(hipGetLastError());
+    return;
+  }
   switch (KP) {
 #define WMX_SEL_A(N)                                                                                             \
   case N:                                                                                                        \
     hipLaunchKernelGGL(logits_select_a<N>, dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, row_map, ws); \
-    hipLaunchKernelGGL(logits_select_b<N>, dim3(R), dim3(64), 0, st, ws, o, tok, lp);                           \
+    hipLaunchKernelGGL(logits_select_b<N>, dim3(R), dim3(64), 0, st, ws, o, tok, lp, logits, ldl, row_map);     \
     break;
     WMX_SEL_A(1)
     WMX_SEL_A(2)

@@ -458,6 +458,9 @@ struct Ctx {
   hipStream_t st = nullptr;
   DT dt = DT::BF16;
   int maxB = 1, K = 1, R = 1, Tctx = 448;
+  // K = rows per window: beam_size for deterministic search, best_of when sampling (temperature > 0; rows are then
+  // independent hypotheses: no beam reorder, no ancestry)
+  bool sampling = false, beam = false;
   long max_samples = 480000;
   int fcap = 3001;
   Special sp{51865};
@@ -1417,9 +1420,14 @@ static void select_and_update(Ctx& c, int B, const int* row_map) {
     launch_record_logits(c.logits, c.ldl, m.d.n_vocab, R, row_map, c.slot, c.rec_base, c.rec_cap, c.rec_logits, c.st);
   RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
               c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
-  launch_logits_select(c.logits, c.ldl, ro, c.rp, R, K + (K > 1 ? 1 : 0), c.ctok, c.clp, row_map, c.sel_ws, c.st);
-  if (K == 1) {
-    if (rec) launch_record_select(R, K, c.ctok, c.rp, c.bs, c.slot, c.rec_base, 0, c.rec_cap, c.rec_sel, c.st);
+  if (c.sampling) {
+    ro.inv_temp = 1.0f / c.o.temperature;
+    ro.seed = c.o.sample_seed;
+    ro.slot = c.slot;
+  }
+  launch_logits_select(c.logits, c.ldl, ro, c.rp, R, c.beam ? K + 1 : 1, c.ctok, c.clp, row_map, c.sel_ws, c.st);
+  if (!c.beam) {  // greedy, or best_of independent sampled rows
+    if (rec) launch_record_select(R, 1, c.ctok, c.rp, c.bs, c.slot, c.rec_base, 0, c.rec_cap, c.rec_sel, c.st);
     launch_greedy_update(c.rp, c.ctok, c.clp, R, c.sp.timestamp_begin, c.sp.eot, c.hist, c.Tctx, c.slot, c.n_done,
                          c.st);
   } else {
@@ -1440,7 +1448,7 @@ static void run_step(Ctx& c, int B) {
   f.tok_ld = c.Tctx;
   f.pad_seq = c.pad_row;
   f.prefill = false;
-  f.anc = c.K > 1 ? c.anc : nullptr;
+  f.anc = c.beam ? c.anc : nullptr;
   dec_step(c, f);
   dec_logits(c, nullptr, f.rows, true);
   debug_sync(c, "logits", -1);
@@ -1633,7 +1641,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   }
   rec(c, 5);
   // ---- decode loop: one hipGraph replay per step ----
-  const int need_done = K == 1 ? R : B;
+  const int need_done = c.beam ? B : R;
   c.probe_slots[0] = steps > 0 ? Pmax : 0;  // slots of the graph-replayed steps of this call
 
   if (c.probe_kernel >= 0)  // per-workgroup records of this call only (read after the timed region)
@@ -1684,7 +1692,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   const int nfin = B * c.max_cand;
   std::vector<int> fcount(B), flen(nfin), fh;
   std::vector<float> fscore(nfin);
-  if (K > 1) {
+  if (c.beam) {
     fh.resize((size_t)nfin * T);
     WMX_HIP(hipMemcpyAsync(fcount.data(), c.bs.fin_count, B * 4, hipMemcpyDeviceToHost, c.st));
     WMX_HIP(hipMemcpyAsync(flen.data(), c.bs.fin_len, nfin * 4, hipMemcpyDeviceToHost, c.st));
@@ -1701,6 +1709,24 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     if (K == 1) {
       for (int i = 0; i < ns[b]; ++i) toks.push_back(h[(size_t)b * T + Pmax + i]);
       sum_lp[b] = slp[b];
+    } else if (c.sampling) {
+      // best_of sampled rows: the highest sum_logprob / length (CT2 sorts its num_hypotheses by that score and
+      // faster-whisper takes sequences_ids[0]); ties keep the lower row
+      int best = 0;
+      double best_score = -INFINITY;
+      for (int j = 0; j < K; ++j) {
+        const int r = b * K + j;
+        const double L = std::max(ns[r], 1);
+        const double pen = c.o.length_penalty == 1.0f ? L : std::pow((5.0 + L) / 6.0, (double)c.o.length_penalty);
+        const double sc = slp[r] / pen;
+        if (sc > best_score) {
+          best = j;
+          best_score = sc;
+        }
+      }
+      const int r = b * K + best;
+      for (int i = 0; i < ns[r]; ++i) toks.push_back(h[(size_t)r * T + Pmax + i]);
+      sum_lp[b] = slp[r];
     } else {
       struct Cand {
         std::vector<int> t;
@@ -2089,13 +2115,19 @@ void wmx_opts_default(wmx_opts* o) {
   o->median_filter_width = 7;
   o->use_graph = 1;
   o->max_audio_samples = 480000;
+  o->temperature = 0.0f;
+  o->best_of = 5;
+  o->sample_seed = 0;
 }
 
 wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
   return guard([&] {
     WMX_CHECK(w && o && out, "null argument");
     WMX_CHECK(o->max_batch >= 1 && o->beam_size >= 1 && o->beam_size <= 8, "opts: batch / beam");
-    WMX_CHECK(o->beam_size * o->max_batch <= 1024, "opts: beam * batch <= 1024");
+    WMX_CHECK(o->temperature >= 0.f && std::isfinite(o->temperature), "opts: temperature");
+    WMX_CHECK(o->temperature == 0.f || (o->best_of >= 1 && o->best_of <= 8), "opts: best_of (1..8) when sampling");
+    const int rows_per_win = o->temperature > 0.f ? o->best_of : o->beam_size;
+    WMX_CHECK(rows_per_win * o->max_batch <= 1024, "opts: rows per window * batch <= 1024");
     WMX_CHECK(o->median_filter_width >= 1 && o->median_filter_width <= 15 && o->median_filter_width % 2 == 1,
               "opts: median_filter_width");
     WMX_HIP(hipSetDevice(w->m.device));
@@ -2106,7 +2138,9 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       c.o = *o;
       c.dt = w->m.dt;
       c.maxB = o->max_batch;
-      c.K = o->beam_size;
+      c.sampling = o->temperature > 0.f;
+      c.K = rows_per_win;
+      c.beam = !c.sampling && c.K > 1;
       c.R = c.K * c.maxB;
       c.Tctx = w->m.d.n_text_ctx;
       c.max_samples = o->max_audio_samples > 0 ? o->max_audio_samples : 480000;
@@ -2355,7 +2389,7 @@ wmx_status wmx_ctx_forced_decode(wmx_ctx* x, const int32_t* prefix, const int32_
       f.tok_ld = T;
       f.pad_seq = c.pad_row;
       f.prefill = false;
-      f.anc = K > 1 ? c.anc : nullptr;
+      f.anc = c.beam ? c.anc : nullptr;
       dec_step(c, f);
       dec_logits(c, nullptr, R, true);
       collect(i + 1, R, 1);
@@ -2738,7 +2772,7 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.kc = c.kc;
       a.vc = c.vc;
       a.kv_R = c.R;
-      a.anc = c.K > 1 ? c.anc : nullptr;
+      a.anc = c.beam ? c.anc : nullptr;
       a.anc_ld = c.Tctx;
       a.pad = c.pad_row;
       a.slot0 = c.slot;

@@ -32,6 +32,7 @@ class Opts(C.Structure):
         ("word_timestamps", C.c_int32), ("alignment_heads", C.POINTER(C.c_int32)),
         ("n_alignment_heads", C.c_int32), ("median_filter_width", C.c_int32),
         ("use_graph", C.c_int32), ("max_audio_samples", C.c_int32),
+        ("temperature", C.c_float), ("best_of", C.c_int32), ("sample_seed", C.c_uint32),
     ]
 
 

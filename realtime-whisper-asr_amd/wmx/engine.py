@@ -147,7 +147,8 @@ class Context:
                  language: int | None = None, without_timestamps: bool = False,
                  max_initial_timestamp_index: int | None = 50, suppress_blank: bool = True,
                  suppress_tokens=(), word_timestamps: bool = True, alignment_heads=None,
-                 median_filter_width: int = 7, use_graph: bool = True, max_audio_samples: int = 480000):
+                 median_filter_width: int = 7, use_graph: bool = True, max_audio_samples: int = 480000,
+                 temperature: float = 0.0, best_of: int = 5, sample_seed: int = 0):
         self.model = model
         o = L.Opts()
         lib.wmx_opts_default(C.byref(o))
@@ -172,6 +173,10 @@ class Context:
         o.median_filter_width = median_filter_width
         o.use_graph = int(use_graph)
         o.max_audio_samples = max_audio_samples
+        # temperature > 0: best_of sampled rows per window (faster-whisper's sampling branch), beam_size unused
+        o.temperature = float(temperature)
+        o.best_of = int(best_of)
+        o.sample_seed = int(sample_seed) & 0xFFFFFFFF
         self.opts = o
         self.max_batch = max_batch
         self.max_audio_samples = max_audio_samples

@@ -659,11 +659,13 @@ class StreamBatcher:
             # the ASR's own decoding options, as CustomFasterWhisperASR.transcribe would pass them
             # (asr_components.py:279-288): language (None = detect), task (set_translate_task), beam size
             kw = dict(getattr(self.asr, "transcribe_kargs", None) or {})
-            if float(kw.get("temperature", 0.0) or 0.0) > 0 or kw.get("vad_filter"):
-                raise NotImplementedError("StreamBatcher: temperature > 0 / vad_filter are not implemented")
+            if kw.get("vad_filter"):
+                raise NotImplementedError("StreamBatcher: vad_filter is not implemented")
             results = self.model.transcribe_batch([a for a, _ in reqs], [p for _, p in reqs],
                                                   language=getattr(self.asr, "original_language", None),
-                                                  task=kw.get("task", "transcribe"), beam_size=kw.get("beam_size"))
+                                                  task=kw.get("task", "transcribe"), beam_size=kw.get("beam_size"),
+                                                  temperature=kw.get("temperature", 0.0) or 0.0,
+                                                  best_of=kw.get("best_of", 5))
             for i, res in zip(due, results):
                 on = streams[i].online
                 try:

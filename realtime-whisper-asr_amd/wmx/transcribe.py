@@ -203,7 +203,7 @@ _FW_UNSUPPORTED = {
     "language_detection_segments": 1,
 }
 # accepted and without effect on this path (faster-whisper semantics preserved)
-_FW_NO_EFFECT = ("log_progress", "language_detection_threshold", "prompt_reset_on_temperature")
+_FW_NO_EFFECT = ("log_progress", "language_detection_threshold")
 
 
 def _check_kwargs(kw):
@@ -217,11 +217,10 @@ def _check_kwargs(kw):
 
 
 def _temperatures(temperature):
-    ts = list(temperature) if isinstance(temperature, (list, tuple)) else [temperature]
-    if any(float(t) > 0 for t in ts):
-        # faster-whisper samples best_of candidates at T > 0 (and falls back through the list); only the
-        # deterministic T = 0 search (greedy / beam) runs on this engine
-        raise NotImplementedError(f"temperature={temperature!r}: sampling (T > 0) is not implemented; use 0.0")
+    """faster-whisper: a float is a one-entry schedule; a list / tuple is the fallback schedule."""
+    ts = [float(t) for t in (temperature if isinstance(temperature, (list, tuple)) else [temperature])]
+    if not ts or any(not np.isfinite(t) or t < 0 for t in ts):
+        raise ValueError(f"temperature={temperature!r}: expected finite values >= 0")
     return ts
 
 
@@ -262,17 +261,20 @@ class WhisperModel:
         self.max_new_tokens = max_new_tokens
         self.suppress_tokens = [-1] if suppress_tokens is None else list(suppress_tokens)
         self.use_graph = use_graph
+        self.sample_seed = seed  # sampling (T > 0) is deterministic per model: the same audio draws the same samples
         self._ctx = {}
 
     def context(self, beam_size, language_token, task, word_timestamps, without_timestamps=False, patience=1.0,
                 length_penalty=1.0, suppress_blank=True, suppress_tokens=None, max_initial_timestamp=1.0,
-                max_new_tokens=None):
+                max_new_tokens=None, temperature=0.0, best_of=5):
         sup = tuple(suppressed_tokens(self.tokenizer.sp, self.suppress_tokens if suppress_tokens is None
                                       else suppress_tokens))
         mit = None if max_initial_timestamp is None else int(round(max_initial_timestamp / TIME_PRECISION))
         mnt = max_new_tokens or self.max_new_tokens or 448
+        temperature = float(temperature)
+        best_of = int(best_of) if temperature > 0 else 5
         key = (beam_size, language_token, task, word_timestamps, without_timestamps, float(patience),
-               float(length_penalty), bool(suppress_blank), sup, mit, mnt)
+               float(length_penalty), bool(suppress_blank), sup, mit, mnt, temperature, best_of)
         if key not in self._ctx:
             self._ctx[key] = Context(self.model, max_batch=self.max_batch, beam_size=beam_size, patience=patience,
                                      length_penalty=length_penalty, max_new_tokens=mnt, task=task,
@@ -280,7 +282,8 @@ class WhisperModel:
                                      max_initial_timestamp_index=mit, suppress_blank=suppress_blank,
                                      suppress_tokens=sup, word_timestamps=word_timestamps,
                                      alignment_heads=ALIGNMENT_HEADS.get(self.name), use_graph=self.use_graph,
-                                     max_audio_samples=2 * 480000)
+                                     max_audio_samples=2 * 480000, temperature=temperature, best_of=best_of,
+                                     sample_seed=self.sample_seed)
         return self._ctx[key]
 
     # ---- faster-whisper WhisperModel.transcribe ----
@@ -289,12 +292,13 @@ class WhisperModel:
                    condition_on_previous_text=True, no_speech_threshold=0.6, log_prob_threshold=-1.0,
                    compression_ratio_threshold=2.4, without_timestamps=False, suppress_blank=True,
                    suppress_tokens=(-1,), max_initial_timestamp=1.0, max_new_tokens=None,
-                   prepend_punctuations=PREPEND_PUNCT, append_punctuations=APPEND_PUNCT, **kwargs):
+                   prepend_punctuations=PREPEND_PUNCT, append_punctuations=APPEND_PUNCT,
+                   prompt_reset_on_temperature=0.5, **kwargs):
         """faster-whisper 1.2.1 transcribe + generate_segments over 30 s windows (seek loop).  Language detection
         runs once, on the first window, and every later window decodes with that language; with word timestamps
         a window that does not end on a single timestamp moves seek to its last word's end (round(end * 100))."""
         _check_kwargs(kwargs)
-        _temperatures(temperature)  # T > 0 raises: only deterministic search runs here
+        temps = _temperatures(temperature)
         audio = np.asarray(audio, dtype=np.float32)
         tok = self.tokenizer
         sp = tok.sp
@@ -317,9 +321,9 @@ class WhisperModel:
         while seek < content_frames:
             segment_size = min(N_FRAMES, content_frames - seek)
             prompt = all_tokens[prompt_reset_since:] if condition_on_previous_text else []
-            ctx = self.context(beam_size, lang_tok, task, word_timestamps, **ctx_kw)
-            # the window's features come from the whole buffer (global max normalisation) -> pass the full audio
-            r = ctx.transcribe([audio], prompts=[prompt], seek=[seek])[0]
+            r, used_t = self._decode_with_fallback(audio, seek, prompt, temps, beam_size, best_of, lang_tok, task,
+                                                   word_timestamps, ctx_kw, compression_ratio_threshold,
+                                                   log_prob_threshold, no_speech_threshold)
             if detected is None:
                 detected, det_prob = sp.language_code(r.language), r.language_prob
             if lang_tok is None:
@@ -329,11 +333,37 @@ class WhisperModel:
                 no_speech_threshold, log_prob_threshold, punct)
             segments.extend(segs)
             all_tokens.extend(toks)
-            if not condition_on_previous_text:
+            if not condition_on_previous_text or used_t > prompt_reset_on_temperature:
                 prompt_reset_since = len(all_tokens)
             seek = seek_new if seek_new > seek else seek + max(1, segment_size)
         info = TranscriptionInfo(detected or "en", det_prob, len(audio) / SAMPLE_RATE, len(audio) / SAMPLE_RATE)
         return iter(segments), info
+
+    def _decode_with_fallback(self, audio, seek, prompt, temps, beam_size, best_of, lang_tok, task, word_timestamps,
+                              ctx_kw, compression_ratio_threshold, log_prob_threshold, no_speech_threshold):
+        """faster-whisper generate_with_fallback: decode at each temperature of the schedule until the result passes
+        the compression-ratio and log-prob checks (a likely-silent window passes); if none does, keep the best
+        avg_logprob among those under the compression threshold (else among all), reported at the last
+        temperature.  T = 0: beam search (beam_size); T > 0: best_of sampled rows."""
+        results = []
+        for t in temps:
+            ctx = self.context(beam_size, lang_tok, task, word_timestamps, temperature=t, best_of=best_of, **ctx_kw)
+            # the window's features come from the whole buffer (global max normalisation) -> pass the full audio
+            r = ctx.transcribe([audio], prompts=[prompt], seek=[seek])[0]
+            cr = compression_ratio(self.tokenizer.decode([x for x in r.tokens if x < self.tokenizer.sp.eot]).strip())
+            results.append((r, cr))
+            needs = False
+            if compression_ratio_threshold is not None and cr > compression_ratio_threshold:
+                needs = True
+            if log_prob_threshold is not None and r.avg_logprob < log_prob_threshold:
+                needs = True
+            if (no_speech_threshold is not None and r.no_speech_prob > no_speech_threshold
+                    and log_prob_threshold is not None and r.avg_logprob < log_prob_threshold):
+                needs = False  # silence
+            if not needs:
+                return r, t
+        below = [x for x in results if compression_ratio_threshold is None or x[1] <= compression_ratio_threshold]
+        return max(below or results, key=lambda x: x[0].avg_logprob)[0], temps[-1]
 
     def _window_segments(self, r, seek, segment_size, word_timestamps, language, last_speech, first_id,
                          no_speech_threshold=0.6, log_prob_threshold=-1.0, punct=(PREPEND_PUNCT, APPEND_PUNCT)):
@@ -370,7 +400,8 @@ class WhisperModel:
         return out, toks, seek_new, last_speech
 
     def transcribe_batch(self, audios, prompts=None, language=None, task="transcribe", beam_size=None,
-                         word_timestamps=True, no_speech_threshold=0.6, log_prob_threshold=-1.0):
+                         word_timestamps=True, no_speech_threshold=0.6, log_prob_threshold=-1.0, temperature=0.0,
+                         best_of=5):
         """Many independent streams' buffers in ONE libwmx launch sequence (one window each).  prompts: per-stream
         previous text (str) or token lists.  Buffers longer than one 30 s window (a streaming buffer nothing has
         committed from yet) go through the full seek loop of transcribe() instead.  Returns per stream a list of
@@ -381,12 +412,14 @@ class WhisperModel:
         prompts = list(prompts) if prompts is not None else [None] * len(audios)
         out = [None] * len(audios)
         short = []
+        temps = _temperatures(temperature)
         for i, a in enumerate(audios):
-            if len(a) > N_FRAMES * HOP:
+            if len(a) > N_FRAMES * HOP or len(temps) > 1:  # several windows, or a fallback schedule: per stream
                 p = prompts[i]
                 try:
-                    segs, _ = self.transcribe(a, language=language, task=task, beam_size=beam,
-                                              initial_prompt=p if p else None, word_timestamps=word_timestamps,
+                    segs, _ = self.transcribe(a, language=language, task=task, beam_size=beam, best_of=best_of,
+                                              temperature=temps, initial_prompt=p if p else None,
+                                              word_timestamps=word_timestamps,
                                               no_speech_threshold=no_speech_threshold,
                                               log_prob_threshold=log_prob_threshold)
                     out[i] = list(segs)
@@ -394,7 +427,7 @@ class WhisperModel:
                     out[i] = e
             else:
                 short.append(i)
-        ctx = self.context(beam, lang_tok, task, word_timestamps)
+        ctx = self.context(beam, lang_tok, task, word_timestamps, temperature=temps[0], best_of=best_of)
         for b0 in range(0, len(short), self.max_batch):
             idx = short[b0: b0 + self.max_batch]
             chunk = [np.asarray(audios[i], np.float32) for i in idx]

@@ -365,3 +365,60 @@ def test_full_depth_small_models_greedy(name, dt):
         assert res[b].language == O.detect_language(W, d, encs[b])[0]
     opt = O.DecodeOptions(beam_size=1, max_new_tokens=48)
     _replay_and_compare(f"{name} full depth greedy {dt}", ctx, res, 1, opt, sp, 24)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# temperature > 0 (faster-whisper's sampling branch; the reference's speech-rate adaptation sets T = 0.1,
+# speech_rate_audio_processor.py:217-218): best_of rows per window drawn by Gumbel-max, replayed by the oracle with
+# the same counter-based noise (oracle.sample_gumbel); parity with CT2's own random draws is unpinned by nature
+# ---------------------------------------------------------------------------------------------------------------
+def _sampling_replay_and_compare(tag, ctx, res, K, opt, sp, T, seed, min_steps):
+    lg, sel = ctx.recorded()
+    info = O.sampling_replay(lg, sel, K, sp, opt, T, seed, slot0=2, eps=EPS_TIE)
+    steps, ties, distinct = [], 0, []
+    for b, (r, inf) in enumerate(zip(res, info)):
+        for j, rw in enumerate(inf["rows"]):
+            assert rw["mismatch"] is None, (tag, b, j, rw["mismatch"])
+            steps.append(rw["steps"])
+            ties += rw["ties"]
+        distinct.append(len({tuple(rw["tokens"]) for rw in inf["rows"]}))
+        if inf["best"] is not None:
+            _, toks, total = inf["best"]
+            assert r.tokens == toks, (tag, b, r.tokens, toks)
+            assert abs(r.sum_logprob - total) <= 1e-3 * max(1.0, abs(total)), (tag, b, r.sum_logprob, total)
+    print(f"{tag}: replayed steps per row {steps}; rows ended by a float tie {ties}; distinct samples per window "
+          f"{distinct}")
+    assert min(s for s in steps) >= min(min_steps, 1) and sum(steps) >= min_steps * len(steps) // 2
+    return info, distinct
+
+
+def test_sampling_replay_micro():
+    from wmx import engine as E
+    d = O.DIMS["micro"]
+    sp = O.special_tokens(d.n_vocab)
+    m = E.Model("micro", 0, "bfloat16").init_synthetic(1)
+    T, seed = 1.0, 1234
+    ctx = E.Context(m, max_batch=3, beam_size=7, max_new_tokens=64, word_timestamps=True, language=sp.lang0,
+                    temperature=T, best_of=4, sample_seed=seed)
+    ctx.record(64)
+    res = ctx.transcribe([synth.speech_like(501, 480000), synth.speech_like(502, 160000), synth.speech_like(503, 32000)])
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=1, max_new_tokens=64)
+    _, distinct = _sampling_replay_and_compare("micro T=1.0 best_of 4", ctx, res, 4, opt, sp, T, seed, 16)
+    assert max(distinct) > 1  # the rows of a window are independent draws
+    assert all(r.jump_times is not None for r in res)  # word alignment runs on the chosen row
+
+
+def test_sampling_replay_wide_adaptive_shape(wide20):
+    """The reference's fast-speech setting (beam 7, T 0.1 -> faster-whisper samples best_of = 5) at large-v3 width:
+    4 windows x 5 rows, prompted."""
+    from wmx import engine as E
+    dt, m, W, mels, encs = wide20
+    sp = O.special_tokens(WIDE2.n_vocab)
+    T, seed = 0.1, 99
+    ctx = E.Context(m, max_batch=4, beam_size=7, max_new_tokens=32, word_timestamps=False, language=sp.lang0,
+                    temperature=T, best_of=5, sample_seed=seed)
+    ctx.record(33)
+    audios = [synth.speech_like(100 + i, n) for i, n in enumerate([480000, 150000, 320000, 16000])]
+    res = ctx.transcribe(audios)
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=1, max_new_tokens=32)
+    _sampling_replay_and_compare(f"wide T=0.1 best_of 5 {dt}", ctx, res, 5, opt, sp, T, seed, 16)

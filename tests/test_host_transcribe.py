@@ -113,8 +113,8 @@ def test_initial_prompt_encoding_like_faster_whisper():
 
 
 @pytest.mark.parametrize("kw,exc", [({"vad_filter": True}, NotImplementedError),
-                                    ({"temperature": 0.2}, NotImplementedError),
-                                    ({"temperature": (0.0, 0.2, 0.4)}, NotImplementedError),
+                                    ({"temperature": -0.2}, ValueError),
+                                    ({"temperature": (0.0, float("nan"))}, ValueError),
                                     ({"hotwords": "abc"}, NotImplementedError),
                                     ({"no_such_option": 1}, TypeError)])
 def test_unsupported_options_raise(kw, exc):
@@ -161,8 +161,10 @@ class BatchModel:
     def __init__(self, fail=()):
         self.calls, self.fail = [], set(fail)
 
-    def transcribe_batch(self, audios, prompts, language=None, task="transcribe", beam_size=None):
-        self.calls.append({"n": len(audios), "language": language, "task": task, "beam": beam_size})
+    def transcribe_batch(self, audios, prompts, language=None, task="transcribe", beam_size=None, temperature=0.0,
+                         best_of=5):
+        self.calls.append({"n": len(audios), "language": language, "task": task, "beam": beam_size,
+                           "temperature": temperature, "best_of": best_of})
         return [RuntimeError("boom") if i in self.fail else [] for i in range(len(audios))]
 
 
@@ -180,7 +182,17 @@ def _streams(n):
 def test_stream_batcher_passes_language_and_task():
     bm = BatchModel()
     OL.StreamBatcher(bm, ASRView("zh", "translate")).step(_streams(3))
-    assert bm.calls == [{"n": 3, "language": "zh", "task": "translate", "beam": 5}]
+    assert bm.calls == [{"n": 3, "language": "zh", "task": "translate", "beam": 5, "temperature": 0.0, "best_of": 5}]
+
+
+def test_stream_batcher_passes_the_adaptive_temperature():
+    """speech_rate_audio_processor.py:217-218 raises temperature to 0.1 (beam 7) on fast speech; the batched path
+    samples then instead of failing."""
+    bm = BatchModel()
+    view = ASRView()
+    view.transcribe_kargs.update({"beam_size": 7, "temperature": 0.1})
+    OL.StreamBatcher(bm, view).step(_streams(2))
+    assert bm.calls[0]["temperature"] == 0.1 and bm.calls[0]["beam"] == 7
 
 
 def test_stream_batcher_isolates_a_failing_stream():
@@ -245,3 +257,46 @@ def test_checkpoint_config_names(tmp_path, cfg, name):
     import json
     (tmp_path / "config.json").write_text(json.dumps(cfg))
     assert TR._infer_name(str(tmp_path)) == name
+
+
+def _fallback_model(avg_lp_at):
+    """A fake engine whose window quality depends on the decoding temperature: avg_lp_at(T) -> avg_logprob."""
+    m = make_model(window)
+
+    def context(beam_size, language_token, task, word_timestamps, **kw):
+        t = kw.get("temperature", 0.0)
+        m.log.append({"context": (beam_size, language_token, task, word_timestamps, kw)})
+        return FakeCtx(m.log, (beam_size, language_token, task, t),
+                       lambda s, i: window(s, i, avg_lp=avg_lp_at(t)))
+
+    m.context = context
+    return m
+
+
+def test_temperature_fallback_stops_at_the_first_passing_temperature():
+    """faster-whisper generate_with_fallback: T = 0 beam search, then best_of sampling at each higher T until
+    avg_logprob >= log_prob_threshold (and the compression ratio passes)."""
+    m = _fallback_model(lambda t: -1.5 if t < 0.4 else -0.5)
+    list(m.transcribe(np.zeros(16000 * 5, np.float32), temperature=(0.0, 0.2, 0.4, 0.6), best_of=3, beam_size=4)[0])
+    ctxs = [e["context"] for e in m.log if "context" in e]
+    assert [c[4]["temperature"] for c in ctxs][:4] == [0.0, 0.2, 0.4, 0.0]  # window 1, then window 2 starts at 0
+    assert all(c[4]["best_of"] == 3 for c in ctxs) and all(c[0] == 4 for c in ctxs)
+
+
+def test_temperature_fallback_all_fail_keeps_best_and_resets_prompt():
+    """Every temperature fails: the best avg_logprob is kept, reported at the last temperature (0.6 > 0.5 =
+    prompt_reset_on_temperature), so the next window's prompt is reset."""
+    lp = {0.0: -1.9, 0.2: -1.2, 0.6: -1.6}
+    m = _fallback_model(lambda t: lp[t])
+    segs = list(m.transcribe(np.zeros(16000 * 40, np.float32), temperature=(0.0, 0.2, 0.6))[0])
+    assert segs and segs[0].avg_logprob == -1.2
+    prompts = [e["prompt"] for e in m.log if "prompt" in e]
+    assert prompts[3] == []  # window 2 (after 3 attempts at window 1): prompt reset since window 1's tokens
+
+
+def test_single_temperature_is_one_decode():
+    m = _fallback_model(lambda t: -3.0)  # fails the log-prob check, but there is nothing to fall back to
+    segs = list(m.transcribe(np.zeros(16000 * 5, np.float32), temperature=0.1)[0])
+    ctxs = [e["context"] for e in m.log if "context" in e]
+    n_win = len([e for e in m.log if "seek" in e])
+    assert len(ctxs) == n_win and all(c[4]["temperature"] == 0.1 and c[4]["best_of"] == 5 for c in ctxs)
