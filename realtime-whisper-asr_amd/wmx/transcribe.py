@@ -190,8 +190,6 @@ def add_word_timestamps(subsegments, alignment, seek, last_speech_timestamp, pre
 # faster-whisper 1.2.1 WhisperModel.transcribe keywords this engine does not implement, with the value that means
 # "off"; any other value raises NotImplementedError instead of being silently ignored
 _FW_UNSUPPORTED = {
-    "vad_filter": False,  # Silero VAD pre-filter: the network is remote-only (torch.hub), SURVEY §8f-1
-    "vad_parameters": None,
     "prefix": None,
     "hotwords": None,
     "clip_timestamps": "0",
@@ -248,6 +246,7 @@ class WhisperModel:
         if isinstance(name, str) and os.path.isdir(name):
             model_dir = name
             name = _infer_name(model_dir)
+        self.device_index = int(device_index)
         self.model = Model(name, int(device_index), compute_type)
         self.dims = self.model.dims
         self.tokenizer = load_tokenizer(model_dir, self.dims.n_vocab)
@@ -293,13 +292,20 @@ class WhisperModel:
                    compression_ratio_threshold=2.4, without_timestamps=False, suppress_blank=True,
                    suppress_tokens=(-1,), max_initial_timestamp=1.0, max_new_tokens=None,
                    prepend_punctuations=PREPEND_PUNCT, append_punctuations=APPEND_PUNCT,
-                   prompt_reset_on_temperature=0.5, **kwargs):
+                   prompt_reset_on_temperature=0.5, vad_filter=False, vad_parameters=None, **kwargs):
         """faster-whisper 1.2.1 transcribe + generate_segments over 30 s windows (seek loop).  Language detection
         runs once, on the first window, and every later window decodes with that language; with word timestamps
         a window that does not end on a single timestamp moves seek to its last word's end (round(end * 100))."""
         _check_kwargs(kwargs)
         temps = _temperatures(temperature)
         audio = np.asarray(audio, dtype=np.float32)
+        duration = len(audio) / SAMPLE_RATE
+        speech_chunks = None
+        if vad_filter:  # faster-whisper: transcribe only the speech chunks, map the times back afterwards
+            from .vad import collect_chunks, get_speech_timestamps, speech_probs
+            params = dict(vars(vad_parameters)) if hasattr(vad_parameters, "__dict__") else dict(vad_parameters or {})
+            speech_chunks = get_speech_timestamps(speech_probs(self.vad_engine(), audio), len(audio), **params)
+            audio = collect_chunks(audio, speech_chunks)
         tok = self.tokenizer
         sp = tok.sp
         lang_tok = None if language is None else sp.language_token(language)
@@ -336,8 +342,23 @@ class WhisperModel:
             if not condition_on_previous_text or used_t > prompt_reset_on_temperature:
                 prompt_reset_since = len(all_tokens)
             seek = seek_new if seek_new > seek else seek + max(1, segment_size)
-        info = TranscriptionInfo(detected or "en", det_prob, len(audio) / SAMPLE_RATE, len(audio) / SAMPLE_RATE)
+        if speech_chunks:
+            from .vad import restore_speech_timestamps
+            segments = list(restore_speech_timestamps(segments, speech_chunks))
+        info = TranscriptionInfo(detected or "en", det_prob, duration, len(audio) / SAMPLE_RATE)
         return iter(segments), info
+
+    def vad_engine(self):
+        """The Silero network of vad_filter (device, one slot): weights from the safetensors file named by
+        WMX_SILERO_WEIGHTS when set, else synthetic (no Silero checkpoint ships in this image)."""
+        if getattr(self, "_vad", None) is None:
+            import os
+
+            from .vad import SileroVADEngine, load_state_dict
+            path = os.environ.get("WMX_SILERO_WEIGHTS")
+            self._vad = SileroVADEngine(load_state_dict(path) if path else None, device=self.device_index,
+                                        max_streams=1, max_windows=64)
+        return self._vad
 
     def _decode_with_fallback(self, audio, seek, prompt, temps, beam_size, best_of, lang_tok, task, word_timestamps,
                               ctx_kw, compression_ratio_threshold, log_prob_threshold, no_speech_threshold):

@@ -186,3 +186,152 @@ def silero_model(spec: str = "silero", engine: SileroVADEngine | None = None, sl
         sd = None if spec == "silero" else load_state_dict(spec)
         engine = SileroVADEngine(sd, max_streams=max(1, slot + 1), max_windows=8)
     return SileroVAD(engine, slot)
+
+
+# ---------------------------------------------------------------------------------------------
+# faster-whisper's `vad_filter=True` (the reference's CustomFasterWhisperASR.use_vad, asr_components.py:307-309):
+# vad.py get_speech_timestamps / collect_chunks / SpeechTimestampsMap of faster-whisper 1.2.1, restated (the
+# package is not installed here, so this is parity unpinned), with the speech probabilities from the device network
+# ---------------------------------------------------------------------------------------------
+VAD_DEFAULTS = dict(threshold=0.5, neg_threshold=None, min_speech_duration_ms=0, max_speech_duration_s=float("inf"),
+                    min_silence_duration_ms=2000, speech_pad_ms=400)
+
+
+def speech_probs(engine: SileroVADEngine, audio, slot: int = 0):
+    """Per-512-sample-window probabilities of a whole buffer (zero-padded to whole windows), from a reset state:
+    faster-whisper's SileroVADModel.__call__ (each window prefixed by the previous window's last 64 samples)."""
+    audio = np.asarray(audio, np.float32)
+    n = len(audio)
+    padded = np.pad(audio, (0, WINDOW - n % WINDOW))
+    engine.reset(slot)
+    out = []
+    per = engine.max_windows * WINDOW
+    for i in range(0, len(padded), per):
+        out.append(engine.process({slot: padded[i:i + per]})[slot])
+    return np.concatenate(out) if out else np.zeros(0, np.float32)
+
+
+def get_speech_timestamps(probs, n_samples: int, sampling_rate: int = SAMPLE_RATE, **opts):
+    """faster-whisper vad.get_speech_timestamps on given window probabilities -> [{"start", "end"}] in samples."""
+    o = dict(VAD_DEFAULTS)
+    unknown = set(opts) - set(o)
+    if unknown:
+        raise TypeError(f"unknown VAD options {sorted(unknown)}")
+    o.update(opts)
+    threshold = o["threshold"]
+    neg_threshold = o["neg_threshold"] if o["neg_threshold"] is not None else max(threshold - 0.15, 0.01)
+    ws = WINDOW
+    min_speech_samples = sampling_rate * o["min_speech_duration_ms"] / 1000
+    speech_pad_samples = sampling_rate * o["speech_pad_ms"] / 1000
+    max_speech_samples = sampling_rate * o["max_speech_duration_s"] - ws - 2 * speech_pad_samples
+    min_silence_samples = sampling_rate * o["min_silence_duration_ms"] / 1000
+    min_silence_samples_at_max_speech = sampling_rate * 98 / 1000
+    triggered, speeches, cur = False, [], {}
+    temp_end = prev_end = next_start = 0
+    for i, p in enumerate(probs):
+        if p >= threshold and temp_end:
+            temp_end = 0
+            if next_start < prev_end:
+                next_start = ws * i
+        if p >= threshold and not triggered:
+            triggered = True
+            cur["start"] = ws * i
+            continue
+        if triggered and ws * i - cur["start"] > max_speech_samples:
+            if prev_end:
+                cur["end"] = prev_end
+                speeches.append(cur)
+                cur = {}
+                if next_start < prev_end:  # reached silence (< neg_threshold) and still not speech
+                    triggered = False
+                else:
+                    cur["start"] = next_start
+                prev_end = next_start = temp_end = 0
+            else:
+                cur["end"] = ws * i
+                speeches.append(cur)
+                cur = {}
+                prev_end = next_start = temp_end = 0
+                triggered = False
+                continue
+        if p < neg_threshold and triggered:
+            if not temp_end:
+                temp_end = ws * i
+            if ws * i - temp_end > min_silence_samples_at_max_speech:
+                prev_end = temp_end
+            if ws * i - temp_end < min_silence_samples:
+                continue
+            cur["end"] = temp_end
+            if cur["end"] - cur["start"] > min_speech_samples:
+                speeches.append(cur)
+            cur = {}
+            prev_end = next_start = temp_end = 0
+            triggered = False
+            continue
+    if cur and n_samples - cur["start"] > min_speech_samples:
+        cur["end"] = n_samples
+        speeches.append(cur)
+    for i, sp in enumerate(speeches):
+        if i == 0:
+            sp["start"] = int(max(0, sp["start"] - speech_pad_samples))
+        if i != len(speeches) - 1:
+            gap = speeches[i + 1]["start"] - sp["end"]
+            if gap < 2 * speech_pad_samples:
+                sp["end"] += int(gap // 2)
+                speeches[i + 1]["start"] = int(max(0, speeches[i + 1]["start"] - gap // 2))
+            else:
+                sp["end"] = int(min(n_samples, sp["end"] + speech_pad_samples))
+                speeches[i + 1]["start"] = int(max(0, speeches[i + 1]["start"] - speech_pad_samples))
+        else:
+            sp["end"] = int(min(n_samples, sp["end"] + speech_pad_samples))
+    return speeches
+
+
+def collect_chunks(audio, chunks):
+    """The speech chunks of `audio` concatenated (faster-whisper collect_chunks without a max duration)."""
+    if not chunks:
+        return np.zeros(0, np.float32)
+    return np.concatenate([np.asarray(audio[c["start"]:c["end"]], np.float32) for c in chunks])
+
+
+class SpeechTimestampsMap:
+    """Time in the concatenated speech -> time in the original audio (faster-whisper vad.SpeechTimestampsMap)."""
+
+    def __init__(self, chunks, sampling_rate: int = SAMPLE_RATE, time_precision: int = 2):
+        self.sampling_rate, self.time_precision = sampling_rate, time_precision
+        self.chunk_end_sample, self.total_silence_before = [], []
+        previous_end = silent = 0
+        for c in chunks:
+            silent += c["start"] - previous_end
+            previous_end = c["end"]
+            self.chunk_end_sample.append(c["end"] - silent)
+            self.total_silence_before.append(silent / sampling_rate)
+
+    def get_chunk_index(self, time: float, is_end: bool = False) -> int:
+        import bisect
+        sample = int(time * self.sampling_rate)
+        if is_end and sample in self.chunk_end_sample:
+            return self.chunk_end_sample.index(sample)
+        return min(bisect.bisect(self.chunk_end_sample, sample), len(self.chunk_end_sample) - 1)
+
+    def get_original_time(self, time: float, chunk_index: int | None = None, is_end: bool = False) -> float:
+        if chunk_index is None:
+            chunk_index = self.get_chunk_index(time, is_end)
+        return round(self.total_silence_before[chunk_index] + time, self.time_precision)
+
+
+def restore_speech_timestamps(segments, chunks, sampling_rate: int = SAMPLE_RATE):
+    """faster-whisper restore_speech_timestamps: words mapped through the chunk of their midpoint, segments from
+    their words (or their own start / end)."""
+    ts = SpeechTimestampsMap(chunks, sampling_rate)
+    for seg in segments:
+        if seg.words:
+            for w in seg.words:
+                k = ts.get_chunk_index((w.start + w.end) / 2)
+                w.start = ts.get_original_time(w.start, k)
+                w.end = ts.get_original_time(w.end, k)
+            seg.start, seg.end = seg.words[0].start, seg.words[-1].end
+        else:
+            seg.start = ts.get_original_time(seg.start)
+            seg.end = ts.get_original_time(seg.end, is_end=True)
+        yield seg

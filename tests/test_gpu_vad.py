@@ -187,3 +187,25 @@ def test_checkpoint_path_through_the_vac_processor(tmp_path):
 
     proc = online.DynamicVACOnlineASRProcessor(1.0, NullASR(), vad_model=p)
     assert isinstance(proc.vac.vad.model, vad.SileroVAD)
+
+
+def test_use_vad_through_the_adapter():
+    """CustomFasterWhisperASR.use_vad() (asr_components.py:307-309) turns on faster-whisper's vad_filter: the device
+    Silero network scores the buffer, only speech chunks are transcribed, times map back to the buffer.  With the
+    synthetic weights the network scores everything as speech at the default threshold, so the chunk is the whole
+    buffer; the speech-chunk logic itself is pinned by the host tests (tests/test_host_transcribe.py)."""
+    from wmx import synth, vad
+    from wmx.asr import MI355XWhisperASR
+    asr = MI355XWhisperASR(lan="auto", modelsize="micro", device="cuda", compute_type="float16",
+                           transcribe_kwargs={"beam_size": 1}, max_new_tokens=16)
+    audio = synth.speech_like(61, 16000 * 6)
+    base = asr.transcribe(audio)
+    asr.use_vad()
+    assert asr.transcribe_kargs.get("vad_filter") is True
+    probs = vad.speech_probs(asr.model.vad_engine(), audio)
+    chunks = vad.get_speech_timestamps(probs, len(audio))
+    segs = asr.transcribe(audio)
+    dur = len(audio) / 16000
+    assert all(0.0 <= s.start <= s.end <= dur + 0.02 for s in segs)
+    if chunks == [{"start": 0, "end": len(audio)}]:
+        assert [(s.start, s.end, s.text) for s in segs] == [(s.start, s.end, s.text) for s in base]

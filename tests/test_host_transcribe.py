@@ -112,7 +112,7 @@ def test_initial_prompt_encoding_like_faster_whisper():
     assert [e["prompt"] for e in m.log if "prompt" in e][0] == [5, 6, 7]
 
 
-@pytest.mark.parametrize("kw,exc", [({"vad_filter": True}, NotImplementedError),
+@pytest.mark.parametrize("kw,exc", [({"prefix": "so"}, NotImplementedError),
                                     ({"temperature": -0.2}, ValueError),
                                     ({"temperature": (0.0, float("nan"))}, ValueError),
                                     ({"hotwords": "abc"}, NotImplementedError),
@@ -300,3 +300,51 @@ def test_single_temperature_is_one_decode():
     ctxs = [e["context"] for e in m.log if "context" in e]
     n_win = len([e for e in m.log if "seek" in e])
     assert len(ctxs) == n_win and all(c[4]["temperature"] == 0.1 and c[4]["best_of"] == 5 for c in ctxs)
+
+
+# ---- vad_filter (faster-whisper 1.2.1 vad.py semantics, restated; parity unpinned: the package is absent) ----
+def _vad_track():
+    return np.array([0.0] * 10 + [0.9] * 20 + [0.0] * 100 + [0.9] * 10 + [0.0] * 10, np.float32)
+
+
+def test_speech_timestamps_from_window_probabilities():
+    from wmx import vad
+    got = vad.get_speech_timestamps(_vad_track(), 150 * 512)
+    # start at window 10 (5120), silence from window 30 lasts >= 2 s -> end 15360; the second run is open at the
+    # end of the buffer; 400 ms padding, clipped to the buffer
+    assert got == [{"start": 0, "end": 21760}, {"start": 60160, "end": 76800}]
+    assert vad.get_speech_timestamps(_vad_track(), 150 * 512, min_speech_duration_ms=1000) == []  # both 640 ms runs dropped
+    with pytest.raises(TypeError):
+        vad.get_speech_timestamps(_vad_track(), 150 * 512, window_size_samples=1024)
+
+
+def test_speech_timestamps_map():
+    from wmx import vad
+    chunks = [{"start": 0, "end": 21760}, {"start": 60160, "end": 76800}]
+    m = vad.SpeechTimestampsMap(chunks, 16000)
+    assert m.chunk_end_sample == [21760, 38400] and m.total_silence_before == [0.0, 2.4]
+    assert m.get_original_time(1.0) == 1.0 and m.get_original_time(1.5) == 3.9
+    assert m.get_original_time(21760 / 16000, is_end=True) == 1.36  # a chunk's own end stays in that chunk
+
+
+def test_vad_filter_transcribes_speech_only_and_restores_times():
+    class FakeEngine:
+        max_windows = 64
+
+        def reset(self, slot):
+            self.pos = 0
+
+        def process(self, chunk):
+            (slot, x), = chunk.items()
+            k = len(x) // 512
+            p = _vad_track()[self.pos:self.pos + k]
+            self.pos += k
+            return {slot: p}
+
+    m = make_model(window)
+    m._vad = FakeEngine()
+    m.vad_engine = lambda: m._vad
+    segs, info = m.transcribe(np.zeros(150 * 512, np.float32), vad_filter=True, word_timestamps=False)
+    segs = list(segs)
+    assert info.duration == 4.8 and info.duration_after_vad == 2.4
+    assert (segs[0].start, segs[0].end) == (0.0, 1.0) and (segs[1].start, segs[1].end) == (1.0, 4.4)
