@@ -1,7 +1,7 @@
 // Silero VAD v5, 16 kHz branch, batched over streams (the reference calls the torch.hub model
 // once per 512-sample window, asr_components.py:96 and :58-78).  Two launches per call:
 //
-//  * vad_encode_kernel: one workgroup per (stream, window) -- every window's context-free part at once.  The
+//  * vad_encode_kernel: one 16-wave workgroup per (stream, window) -- every window's context-free part at once.  The
 //    576-sample input (64 context samples + 512 new ones; the context of a stream's first window comes from its
 //    slot, of later windows from the same call's audio) and its right reflection pad land in LDS; the STFT-as-conv
 //    (258 basis rows x 256 taps x 4 frames) runs one wave per basis row with lanes over taps, so every basis load
@@ -54,18 +54,22 @@ __device__ inline void vad_conv(const float* __restrict__ w, const float* __rest
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void vad_encode_kernel(const float* __restrict__ W, const float* __restrict__ pcm,
+constexpr int kVadEncThreads = 1024;  // 16 waves: each layer's channels split 16 ways (the per-window chain is
+                                      // latency-bound: wave sums and dependent weight loads per channel)
+
+__global__ __launch_bounds__(kVadEncThreads) void vad_encode_kernel(const float* __restrict__ W, const float* __restrict__ pcm,
                                                          long stride, const float* __restrict__ ctx,
                                                          const int* __restrict__ slots, int nwin,
                                                          float* __restrict__ enc) {
   const int n = blockIdx.x, s = n / nwin, wi = n - s * nwin;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = kVadEncThreads / 64;
   __shared__ float xs[kVadPadded];
   __shared__ float mag[129 * 4];
   __shared__ float h1[128 * 4], h2[64 * 2], h3[64];
   const float* src = pcm + (long)s * stride;
   const float* cx = ctx + (long)slots[s] * kVadContext;
-  for (int i = tid; i < kVadInput; i += 256) {
+  for (int i = tid; i < kVadInput; i += kVadEncThreads) {
     const long idx = (long)wi * kVadWindow - kVadContext + i;
     xs[i] = idx >= 0 ? src[idx] : cx[idx + kVadContext];
   }
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(256) void vad_encode_kernel(const float* __restrict
 
   // STFT magnitudes: wave per frequency bin c (real row c, imaginary row 129 + c), lanes over the 256 taps
   const float* basis = W + kVadOffBasis;
-  for (int c = wave; c < 129; c += 4) {
+  for (int c = wave; c < 129; c += NW) {
     float re[4] = {0.f, 0.f, 0.f, 0.f}, im[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -95,13 +99,13 @@ __global__ __launch_bounds__(256) void vad_encode_kernel(const float* __restrict
     }
   }
   __syncthreads();
-  vad_conv<129, 128, 4, 1>(W + kVadOffC0w, W + kVadOffC0b, mag, h1, wave, lane, 4);
+  vad_conv<129, 128, 4, 1>(W + kVadOffC0w, W + kVadOffC0b, mag, h1, wave, lane, NW);
   __syncthreads();
-  vad_conv<128, 64, 4, 2>(W + kVadOffC1w, W + kVadOffC1b, h1, h2, wave, lane, 4);
+  vad_conv<128, 64, 4, 2>(W + kVadOffC1w, W + kVadOffC1b, h1, h2, wave, lane, NW);
   __syncthreads();
-  vad_conv<64, 64, 2, 2>(W + kVadOffC2w, W + kVadOffC2b, h2, h3, wave, lane, 4);
+  vad_conv<64, 64, 2, 2>(W + kVadOffC2w, W + kVadOffC2b, h2, h3, wave, lane, NW);
   __syncthreads();
-  vad_conv<64, 128, 1, 1>(W + kVadOffC3w, W + kVadOffC3b, h3, enc + (long)n * kVadHidden, wave, lane, 4);
+  vad_conv<64, 128, 1, 1>(W + kVadOffC3w, W + kVadOffC3b, h3, enc + (long)n * kVadHidden, wave, lane, NW);
 }
 
 __global__ __launch_bounds__(512) void vad_decode_kernel(const float* __restrict__ W, const float* __restrict__ enc,
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(512) void vad_decode_kernel(const float* __restrict
 
 void launch_vad(const float* W, const float* pcm, long stride, float* ctx, float* state, const int* slots_dev, int S,
                 int nwin, float* enc, float* probs, hipStream_t st) {
-  hipLaunchKernelGGL(vad_encode_kernel, dim3(S * nwin), dim3(256), 0, st, W, pcm, stride, ctx, slots_dev, nwin, enc);
+  hipLaunchKernelGGL(vad_encode_kernel, dim3(S * nwin), dim3(kVadEncThreads), 0, st, W, pcm, stride, ctx, slots_dev, nwin, enc);
   hipLaunchKernelGGL(vad_decode_kernel, dim3(S), dim3(512), 0, st, W, enc, nwin, slots_dev, state, ctx, pcm, stride,
                      probs);
   WMX_HIP(hipGetLastError());
