@@ -668,7 +668,22 @@ inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long
 template <DT T, int KPW, int NWV, bool XQ = false>
 __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   constexpr int NT = 64 * NWV;
-  const int h = blockIdx.x, w = blockIdx.y, ks = blockIdx.z % KS, qt = blockIdx.z / KS;
+  int h = blockIdx.x, w = blockIdx.y, zz = blockIdx.z;
+  if (a.xcd_remap) {
+    // workgroups are dispatched round-robin over the 8 XCDs by linear id; this bijection gives each XCD a run of
+    // consecutive (head-major) work items, so the windows and key chunks of one head -- which all stream that head's
+    // query-projection weights -- share one or two XCDs' L2 instead of pulling the slice into up to eight
+    const int N = gridDim.x * gridDim.y * gridDim.z;
+    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int qn = N >> 3, rn = N & 7, xcd = L & 7, j = L >> 3;
+    const int g = xcd < rn ? xcd * (qn + 1) + j : rn * (qn + 1) + (xcd - rn) * qn + j;
+    const int per_h = gridDim.y * gridDim.z;
+    h = g / per_h;
+    const int rem = g - h * per_h;
+    w = rem / gridDim.z;
+    zz = rem - w * gridDim.z;
+  }
+  const int ks = zz % KS, qt = zz / KS;
   // wave index as a scalar: the K / V buffer loads below take their block offsets in the scalar soffset operand, and
   // a wave index the compiler cannot prove uniform turns every one of them into a readfirstlane waterfall loop
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1005,7 +1020,13 @@ size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
 }
 
 template <DT T>
-static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
+static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
+  DecAttnArgs a = a0;
+  static const int remap = [] {  // WMX_XATTN_REMAP=0/1: A/B switch of the head-per-XCD placement
+    const char* v = getenv("WMX_XATTN_REMAP");
+    return v ? atoi(v) : 0;
+  }();
+  a.xcd_remap = remap && a.wq != nullptr;
   const int nq = a.rows_per_win * a.Tn;
   const int nwin = a.R / a.rows_per_win;
   const int chunk = std::min(cross_chunk(a.Tk, nq), a.Tk);

@@ -262,6 +262,7 @@ struct DecAttnArgs {
   int Tk;
   int rows_per_win;    // rows sharing one encoder window (beam)
   int* xcnt = nullptr; // key-chunked launches: one arrival counter per (window, head), zero between launches
+  int xcd_remap = 0;   // cross attention: place the workgroups of one head on one or two XCDs (launch_cross_t)
   unsigned long long* tprobe = nullptr;  // [slot][workgroup][start, end] wall-clock ticks (probe_record), or null
   // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
   // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
