@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 METRIC = "real-time factor + p50 chunk latency, Whisper large-v3 30s@16kHz, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0
 MFMA_BF16_PEAK_TFLOPS = 2500.0
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_16x16x4_f32), spec
 
 
 def log(*a):
@@ -468,7 +469,10 @@ def main():
               "achieved_gbs": round(lm_by / (lm_ms * 1e-3) / 1e9, 1),
               "frac_hbm": round(lm_by / (lm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
               "tflops_f32": round(lm_fl / (lm_ms * 1e-3) / 1e12, 2),
-              "note": "isolated replay, HIP events; DFT-as-GEMM on the f32 MFMA"}
+              "frac_mfma_f32": round(lm_fl / (lm_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
+              "bound": "mfma_f32",
+              "note": "isolated replay, HIP events; the windowed DFT runs as an f32 GEMM on v_mfma_f32_16x16x4_f32 "
+                      "(~1 GFLOP per window), so the launch is bound by the f32 matrix rate, not HBM"}
     # encoder MFMA utilisation (north_star: >= 40 % in the encoder): one whole encoder pass over a context's
     # windows, isolated (HIP events), and the in-situ encoder stage of the timed region (all groups concurrent)
     e_ms, _, e_fl = ctx.bench_kernel("encoder", Bg, iters=3)
