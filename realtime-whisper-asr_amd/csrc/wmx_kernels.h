@@ -184,7 +184,10 @@ void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float*
 void gemm_init_attributes();
 
 // log-mel
+// sparse slaney filterbank limits of the FFT log-mel form (its table is staged in LDS)
+constexpr int kMaxMels = 128, kMelWCap = 640;
 size_t logmel_smem_bytes();
+double logmel_flops_per_frame();  // algorithmic flops of the active log-mel form per STFT frame
 void launch_logmel(const float* pcm, long stride, const long* lens_dev, const int* seek_dev, int B, int max_frames,
                    const float* basis, const int* mfirst, const int* mcount, const int* moff, const float* mw,
                    int n_mels, float* raw, int fcap, int* wmax, float* out, hipStream_t st);

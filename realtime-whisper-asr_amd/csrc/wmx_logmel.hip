@@ -5,7 +5,7 @@
 //   (F = N//160 + 1 frames); per-window max-8 clamp; (x+4)/4; encoder window = frames [seek, seek+3000)
 //   of the first min(3000, F-1-seek) content frames, zero padded (pad_or_trim).
 //
-// Kernel 1 (logmel_raw): one workgroup = 64 consecutive frames of one window, 4 waves x 16 frames.
+// Kernel 1, GEMM form (logmel_raw, opt-in WMX_LOGMEL_GEMM=1; the FFT form below is the default): one workgroup = 64 consecutive frames of one window, 4 waves x 16 frames.
 //   The windowed real DFT is a [frames x 400] x [400 x 416] f32 GEMM on v_mfma_f32_16x16x4_f32 (exact
 //   fp32 FMA chains; bf16 would miss the 1e-4 gate).  Audio for the 64 frames (10480 samples, reflect
 //   applied) is staged once in LDS; the Hann-folded cos/sin basis streams through LDS in 16-sample
@@ -14,6 +14,7 @@
 //   is folded into a per-window atomicMax.
 // Kernel 2 (logmel_finalize): clamp, scale, slice [seek, seek+3000) and zero-pad.  HBM-bound.
 #include "wmx_common.h"
+#include "wmx_kernels.h"
 
 namespace wmx {
 
@@ -127,6 +128,180 @@ __global__ __launch_bounds__(256) void logmel_raw_kernel(const float* __restrict
   if (tid == 0) atomicMax(&wmax[b], enc_max(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Kernel 1, FFT form (default): one workgroup = 32 consecutive frames of one window.  The 400-point real DFT of a
+// frame is a two-pass Cooley-Tukey transform with N = 20 x 20 (n = 20 n1 + n2, k = k1 + 20 k2):
+//   pass 1, thread per (frame, n2):  Y[n2][k1] = sum_n1 xw[20 n1 + n2] W20^(n1 k1), k1 = 0..10 (real input: the
+//           other half is the conjugate), the 20 samples in registers, W20 as compile-time constants;
+//   pass 2, thread per (frame, k1):  t[n2] = Y[n2][k1] W400^(n2 k1) (table in LDS), then
+//           X[k1 + 20 k2] = sum_n2 t[n2] W20^(n2 k2) for the bins <= 200, and |X|^2 straight to the power image.
+// ~54 kFLOP per frame on the vector ALUs instead of the 333 kFLOP of the DFT-as-GEMM (no 666 KB basis stream per
+// workgroup); audio, Y (the 11 stored k1 columns, float2) and the power image all stay in LDS.
+// The filterbank / log10 / per-window max tail is the GEMM form's.
+// ------------------------------------------------------------------------------------------------
+constexpr int kFftFrames = 32;
+constexpr int kFftThreads = kFftFrames * 20;  // 10 waves: one (frame, n2) item per thread in pass 1, (frame, k1) in pass 2
+constexpr int kFftSeg = kHop * (kFftFrames - 1) + kFFT;  // 5360 samples
+
+// cos / sin(2 pi m / 20), m = 0..19 (folded into the unrolled loops as literals)
+__device__ constexpr float kC20[20] = {1.0f, 0.95105651629515357f, 0.80901699437494742f, 0.58778525229247313f,
+                                       0.30901699437494742f, 0.0f, -0.30901699437494742f, -0.58778525229247313f,
+                                       -0.80901699437494742f, -0.95105651629515357f, -1.0f, -0.95105651629515357f,
+                                       -0.80901699437494742f, -0.58778525229247313f, -0.30901699437494742f, 0.0f,
+                                       0.30901699437494742f, 0.58778525229247313f, 0.80901699437494742f,
+                                       0.95105651629515357f};
+__device__ constexpr float kS20[20] = {0.0f, 0.30901699437494742f, 0.58778525229247313f, 0.80901699437494742f,
+                                       0.95105651629515357f, 1.0f, 0.95105651629515357f, 0.80901699437494742f,
+                                       0.58778525229247313f, 0.30901699437494742f, 0.0f, -0.30901699437494742f,
+                                       -0.58778525229247313f, -0.80901699437494742f, -0.95105651629515357f, -1.0f,
+                                       -0.95105651629515357f, -0.80901699437494742f, -0.58778525229247313f,
+                                       -0.30901699437494742f};
+
+// audio + Y (the power image reuses Y's space after pass 2) + the W400 table: 80 KB, two workgroups per CU
+constexpr int kYS = 21;  // Y row stride (float2): odd, so pass 2's per-thread row reads fall in different banks
+size_t logmel_fft_smem_bytes() { return (size_t)kFftSeg * 4 + (size_t)kFftFrames * 11 * kYS * 8 + 2 * kFFT * 4; }
+
+__global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __restrict__ pcm, long stride,
+                                                         const long* __restrict__ lens, MelTable mt, int n_mels,
+                                                         float* __restrict__ raw, int fcap, int* __restrict__ wmax) {
+  const int b = blockIdx.y;
+  const long N = lens[b];
+  const int F = (int)(N / kHop) + 1;
+  const int f0 = blockIdx.x * kFftFrames;
+  if (f0 >= F) return;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* aud = smem;                                            // [kFftSeg], Hann applied per frame in pass 1
+  float2* Y = reinterpret_cast<float2*>(smem + kFftSeg);        // [frame][k1 0..10][n2 0..19, row stride kYS]
+  float* pw = smem + kFftSeg;                                   // [frame][208], over Y once pass 2 has read it
+  float* tc = smem + kFftSeg + kFftFrames * 11 * kYS * 2;       // cos(2 pi j / 400)
+  float* ts = tc + kFFT;                                        // sin(2 pi j / 400)
+  // the sparse filterbank in LDS, loaded beside the audio: the tail's per-mel reads are then LDS, not a chain of
+  // dependent global loads per mel
+  __shared__ int mfirst[kMaxMels], mcount[kMaxMels], moff[kMaxMels];
+  __shared__ float mw[kMelWCap];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < n_mels; i += kFftThreads) {
+    mfirst[i] = mt.first[i];
+    mcount[i] = mt.count[i];
+    moff[i] = mt.offset[i];
+  }
+  for (int i = tid; i < kMelWCap; i += kFftThreads) mw[i] = mt.w[i];  // (the table allocation holds n_mels x 201)
+  const float* x = pcm + (long)b * stride;
+  const long Lp = N + kHop;  // padded length
+  const long period = 2 * (Lp - 1);
+  const long j0 = (long)f0 * kHop - kFFT / 2;
+  for (int i = tid; i < kFftSeg; i += kFftThreads) {
+    const long j = j0 + i;
+    long m = j;
+    if (j < 0 || j >= Lp) {  // reflect (only the frames at the buffer edges take the 64-bit modulo)
+      m = j % period;
+      if (m < 0) m += period;
+      if (m >= Lp) m = period - m;
+    }
+    aud[i] = (m < N) ? x[m] : 0.0f;
+  }
+  for (int j = tid; j < kFFT; j += kFftThreads) {
+    float sv, cv;
+    sincospif(2.0f * (float)j / (float)kFFT, &sv, &cv);
+    tc[j] = cv;
+    ts[j] = sv;
+  }
+  __syncthreads();
+  // pass 1: (frame, n2) -> Y[frame][k1][n2], k1 = 0..10; periodic Hann w[n] = 0.5 - 0.5 cos(2 pi n / 400)
+  for (int it = tid; it < kFftFrames * 20; it += kFftThreads) {
+    const int fr = it / 20, n2 = it - fr * 20;
+    float a[20];
+#pragma unroll
+    for (int n1 = 0; n1 < 20; ++n1) {
+      const int n = 20 * n1 + n2;
+      a[n1] = aud[fr * kHop + n] * (0.5f - 0.5f * tc[n]);
+    }
+#pragma unroll
+    for (int k1 = 0; k1 <= 10; ++k1) {
+      float re = 0.f, im = 0.f;
+#pragma unroll
+      for (int n1 = 0; n1 < 20; ++n1) {
+        re = fmaf(a[n1], kC20[(n1 * k1) % 20], re);
+        im = fmaf(a[n1], -kS20[(n1 * k1) % 20], im);
+      }
+      Y[(fr * 11 + k1) * kYS + n2] = make_float2(re, im);
+    }
+  }
+  __syncthreads();
+  // pass 2: (frame, k1) -> |X[k1 + 20 k2]|^2 for the bins <= 200 (one item per thread: kFftThreads = frames x 20)
+  static_assert(kFftThreads == kFftFrames * 20, "pass 2 keeps its item's powers in registers across the barrier");
+  float pv[11];
+  int pfr = 0, pk1 = 0;
+  {
+    const int it = tid;
+    const int fr = it / 20, k1 = it - fr * 20;
+    pfr = fr;
+    pk1 = k1;
+    const bool conj = k1 > 10;
+    const int kk = conj ? 20 - k1 : k1;
+    float tr[20], ti[20];
+#pragma unroll
+    for (int n2 = 0; n2 < 20; ++n2) {
+      const float2 y = Y[(fr * 11 + kk) * kYS + n2];
+      const float yr = y.x, yi = conj ? -y.y : y.y;
+      const int j = (n2 * k1) % kFFT;  // W400^(n2 k1) = cos - i sin
+      const float c = tc[j], sn = ts[j];
+      tr[n2] = yr * c + yi * sn;
+      ti[n2] = yi * c - yr * sn;
+    }
+#pragma unroll
+    for (int k2 = 0; k2 <= 10; ++k2) {
+      const int k = k1 + 20 * k2;
+      if (k > 200) break;
+      float xr = 0.f, xi = 0.f;
+#pragma unroll
+      for (int n2 = 0; n2 < 20; ++n2) {
+        const float c = kC20[(n2 * k2) % 20], sn = kS20[(n2 * k2) % 20];
+        xr = fmaf(tr[n2], c, fmaf(ti[n2], sn, xr));
+        xi = fmaf(ti[n2], c, fmaf(-tr[n2], sn, xi));
+      }
+      pv[k2] = xr * xr + xi * xi;
+    }
+  }
+  __syncthreads();  // every thread has read Y: its space becomes the power image
+#pragma unroll
+  for (int k2 = 0; k2 <= 10; ++k2)
+    if (pk1 + 20 * k2 <= 200) pw[pfr * (kBinTiles * 16) + pk1 + 20 * k2] = pv[k2];
+  __syncthreads();
+  // sparse filterbank + log10; thread -> (frame = tid & 31, mel stride 8)
+  float bmax = -INFINITY;
+  const int fr = tid & (kFftFrames - 1);
+  const int f = f0 + fr;
+  const bool valid = f < F;
+  constexpr int kPB = kBinTiles * 16;
+  for (int m = tid / kFftFrames; m < n_mels; m += kFftThreads / kFftFrames) {
+    const int s0 = mfirst[m], cnt = mcount[m], off = moff[m];
+    float acc = 0.f;
+    for (int i = 0; i < cnt; ++i) acc += mw[off + i] * pw[fr * kPB + s0 + i];
+    const float v = log10f(fmaxf(acc, 1e-10f));
+    if (valid) {
+      raw[((long)b * n_mels + m) * fcap + f] = v;
+      bmax = fmaxf(bmax, v);
+    }
+  }
+  bmax = wave_max(bmax);
+  __shared__ float red[kFftThreads / 64];
+  if (lane == 0) red[wave] = bmax;
+  __syncthreads();
+  if (tid == 0) {
+    float mx = red[0];
+    for (int w2 = 1; w2 < kFftThreads / 64; ++w2) mx = fmaxf(mx, red[w2]);
+    atomicMax(&wmax[b], enc_max(mx));
+  }
+}
+
+static bool logmel_use_gemm() {  // WMX_LOGMEL_GEMM=1: the DFT-as-GEMM form (A/B and parity reference runs)
+  static const bool v = getenv("WMX_LOGMEL_GEMM") != nullptr;
+  return v;
+}
+
+double logmel_flops_per_frame() { return logmel_use_gemm() ? 400.0 * 416 * 2 : 53600.0; }
+
 // out[b][m][t] = (max(raw, max_b - 8) + 4) / 4 for t < segment_size, else 0
 __global__ __launch_bounds__(256) void logmel_finalize_kernel(const float* __restrict__ raw, const long* __restrict__ lens,
                                                               const int* __restrict__ seek, const int* __restrict__ wmax,
@@ -157,13 +332,22 @@ void launch_logmel(const float* pcm, long stride, const long* lens_dev, const in
   if (!attr) {
     WMX_HIP(hipFuncSetAttribute((const void*)logmel_raw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)logmel_smem_bytes()));
+    WMX_HIP(hipFuncSetAttribute((const void*)logmel_fft_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)logmel_fft_smem_bytes()));
     attr = true;
   }
   WMX_HIP(hipMemsetD32Async((hipDeviceptr_t)wmax, (int)0x80000000, B, st));
   MelTable mt{mfirst, mcount, moff, mw};
-  dim3 g1(cdiv(max_frames, kFramesPerWG), B);
-  hipLaunchKernelGGL(logmel_raw_kernel, g1, dim3(256), logmel_smem_bytes(), st, pcm, stride, lens_dev, basis, mt,
-                     n_mels, raw, fcap, wmax);
+  WMX_CHECK(n_mels <= kMaxMels, "logmel: n_mels");
+  if (logmel_use_gemm()) {
+    dim3 g1(cdiv(max_frames, kFramesPerWG), B);
+    hipLaunchKernelGGL(logmel_raw_kernel, g1, dim3(256), logmel_smem_bytes(), st, pcm, stride, lens_dev, basis, mt,
+                       n_mels, raw, fcap, wmax);
+  } else {
+    dim3 g1(cdiv(max_frames, kFftFrames), B);
+    hipLaunchKernelGGL(logmel_fft_kernel, g1, dim3(kFftThreads), logmel_fft_smem_bytes(), st, pcm, stride, lens_dev, mt,
+                       n_mels, raw, fcap, wmax);
+  }
   long total = (long)B * n_mels * 3000;
   int g2 = (int)std::min<long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(logmel_finalize_kernel, dim3(g2), dim3(256), 0, st, raw, lens_dev, seek_dev, wmax, n_mels, fcap,

@@ -373,6 +373,8 @@ static void build_model(Model& m) {
   WMX_HIP(hipMemcpyAsync(m.mel_first, first.data(), M * 4, hipMemcpyHostToDevice, m.st));
   WMX_HIP(hipMemcpyAsync(m.mel_count, count.data(), M * 4, hipMemcpyHostToDevice, m.st));
   WMX_HIP(hipMemcpyAsync(m.mel_off, off.data(), M * 4, hipMemcpyHostToDevice, m.st));
+  WMX_CHECK(M <= kMaxMels && wts.size() <= (size_t)kMelWCap && (size_t)M * 201 >= (size_t)kMelWCap,
+            "mel filterbank exceeds the log-mel kernel's LDS table");
   WMX_HIP(hipMemcpyAsync(m.mel_w, wts.data(), wts.size() * 4, hipMemcpyHostToDevice, m.st));
   WMX_HIP(hipStreamSynchronize(m.st));
 }
@@ -2749,7 +2751,7 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       WMX_HIP(hipMemcpy(c.lens, lens.data(), B * sizeof(long), hipMemcpyHostToDevice));
       WMX_HIP(hipMemset(c.seek, 0, B * 4));
       by = (double)B * (480000.0 * 4 + m.d.n_mels * 3000.0 * 4);
-      fl = (double)B * 3001 * (400.0 * 416 * 2);
+      fl = (double)B * 3001 * logmel_flops_per_frame();
       fn = [&c, &m, B] {
         launch_logmel(c.pcm, std::min<long>(480000, c.max_samples), c.lens, c.seek, B, 3001, m.mel_basis, m.mel_first,
                       m.mel_count, m.mel_off, m.mel_w, m.d.n_mels, c.mel_raw, c.fcap, c.wmax, c.mel, c.st);
