@@ -20,9 +20,9 @@ import sys
 import time
 
 # HIP hardware queues per process (read at HIP initialisation, so before anything touches the GPU): the decoding
-# context groups, the model stream and torch's streams exceed HIP's default of 4, and two groups sharing one queue
-# fall into a slower mode on some runs (decode 544-562 vs 538 ms per call); 8 queues measured 537.5-538.5 ms on every
-# one of 7 runs (profiles/r02p_hwq_ab/).  An explicit setting from the caller wins.
+# context groups, the model stream and torch's streams exceed HIP's default of 4; runs fall into a slower decode mode
+# (544-563 vs 538 ms per call) less often with 8 queues (2 of 14 runs vs 3 of 7, profiles/r02p_hwq_ab/ and
+# r02q_kernarg_ab/).  An explicit setting from the caller wins.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np
