@@ -476,7 +476,12 @@ class WhisperModel:
 def _infer_name(model_dir):
     import json
     import os
-    cfg = json.load(open(os.path.join(model_dir, "config.json")))
+    if os.path.exists(os.path.join(model_dir, "model.bin")):  # CTranslate2 directory (the reference's models_fast/)
+        from .ct2 import ct2_dims, read_model_bin
+        dims = ct2_dims(read_model_bin(os.path.join(model_dir, "model.bin"))[2])
+        cfg = {"d_model": dims["n_audio_state"], "decoder_layers": dims["n_text_layer"], "num_mel_bins": dims["n_mels"]}
+    else:
+        cfg = json.load(open(os.path.join(model_dir, "config.json")))
     nm = {80: "large-v2", 128: "large-v3"}
     d = cfg.get("d_model")
     for k, v in {"tiny": 384, "base": 512, "small": 768, "medium": 1024}.items():
@@ -488,13 +493,18 @@ def _infer_name(model_dir):
 
 
 def _load_checkpoint(model, model_dir):
-    """HF Whisper safetensors (any of f32 / f16 / bf16 storage) -> wmx_model_set_tensor (rounds to the model
-    dtype, packs the decoder projections).  bf16 has no numpy dtype, so tensors are read through torch."""
+    """A CTranslate2 model.bin (wmx.ct2: f32 / f16 / bf16 / int8 storage) or HF Whisper safetensors (any of f32 / f16 /
+    bf16 storage) -> wmx_model_set_tensor (rounds to the model dtype, packs the decoder projections).  bf16 has no
+    numpy dtype, so safetensors are read through torch."""
     import glob
     import os
+    if os.path.exists(os.path.join(model_dir, "model.bin")):  # CTranslate2 (faster-whisper) directory
+        from .ct2 import load_ct2_dir
+        model.load_state_dict(load_ct2_dir(model_dir)[1])
+        return
     files = sorted(glob.glob(os.path.join(model_dir, "*.safetensors")))
     if not files:
-        raise FileNotFoundError(f"no *.safetensors in {model_dir} (CT2 model.bin conversion is not supported yet)")
+        raise FileNotFoundError(f"no model.bin (CTranslate2) or *.safetensors (HF) in {model_dir}")
     from safetensors.torch import load_file
     sd = {}
     for f in files:

@@ -1,0 +1,71 @@
+"""CTranslate2 model.bin ingestion (wmx.ct2; the reference loads CT2 directories, 一键.py:1115).
+CTranslate2 is not installed here, so parity with its own files is unpinned: the format (binary version 6, the Whisper
+spec's fused variable names, int8 per-row scales) is restated and checked by round trips through the writer; the GPU
+test (tests/test_gpu_checkpoint.py) loads such a directory into a model and transcribes."""
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import whisper_np as O
+from wmx import ct2
+
+
+def _hf(d, seed=1):
+    rng = np.random.default_rng(seed)
+    sd = {name: rng.standard_normal(shape).astype(np.float32) * 0.05 for name, shape, _, _ in O.tensor_specs(d)}
+    sd["encoder.embed_positions.weight"] = rng.standard_normal((1500, d.n_audio_state)).astype(np.float32)
+    return sd
+
+
+def _dims(d):
+    return dict(n_audio_layer=d.n_audio_layer, n_text_layer=d.n_text_layer)
+
+
+@pytest.mark.parametrize("q,tol", [("float32", 0.0), ("float16", 1e-3), ("bfloat16", 8e-3), ("int8", 1.2e-2)])
+def test_roundtrip_through_model_bin(tmp_path, q, tol):
+    d = O.DIMS["micro"]
+    sd = _hf(d)
+    v, al = ct2.hf_to_ct2(sd, _dims(d), q)
+    p = str(tmp_path / "model.bin")
+    ct2.write_model_bin(p, v, al)
+    spec, rev, back, aliases = ct2.read_model_bin(p)
+    assert spec == "WhisperSpec" and aliases == {"decoder/projection/weight": "decoder/embeddings/weight"}
+    dims, hf = ct2.ct2_to_hf(back)
+    assert dims["n_audio_state"] == d.n_audio_state and dims["n_text_layer"] == d.n_text_layer
+    assert dims["n_mels"] == d.n_mels and dims["n_vocab"] == d.n_vocab and dims["n_audio_head"] * 64 == d.n_audio_state
+    for k, ref in sd.items():
+        if k.endswith("k_proj.bias"):
+            continue
+        got = hf[k]
+        assert got.shape == ref.shape, k
+        err = float(np.max(np.abs(got - ref)) / max(1e-6, float(np.max(np.abs(ref)))))
+        lin = k.endswith(".weight") and ("proj" in k or "fc" in k or "embed_tokens" in k)
+        assert err <= (tol if lin else 0.0), (k, err)
+    assert not any(k.endswith("k_proj.bias") for k in hf)  # Whisper keys have no bias (zeros in the fused CT2 bias)
+
+
+def test_format_layout(tmp_path):
+    """Byte layout of the header and of one variable record, as CTranslate2 writes it."""
+    p = str(tmp_path / "model.bin")
+    ct2.write_model_bin(p, {"a/b": np.arange(6, dtype=np.float32).reshape(2, 3), "n": np.array(7, np.int16)})
+    raw = open(p, "rb").read()
+    assert struct.unpack("<I", raw[:4])[0] == 6
+    n = struct.unpack("<H", raw[4:6])[0]
+    assert raw[6:6 + n] == b"WhisperSpec\0"
+    off = 6 + n + 4
+    assert struct.unpack("<I", raw[off:off + 4])[0] == 2
+    off += 4
+    assert struct.unpack("<H", raw[off:off + 2])[0] == 4 and raw[off + 2:off + 6] == b"a/b\0"
+    off += 6
+    assert raw[off] == 2 and struct.unpack("<2I", raw[off + 1:off + 9]) == (2, 3) and raw[off + 9] == 0
+    assert struct.unpack("<I", raw[off + 10:off + 14])[0] == 24
+    _, _, v, _ = ct2.read_model_bin(p)
+    assert v["n"].shape == () and int(v["n"]) == 7 and v["a/b"][1, 2] == 5.0
+
+
+def test_rejects_unknown_versions(tmp_path):
+    p = tmp_path / "model.bin"
+    p.write_bytes(struct.pack("<I", 99))
+    with pytest.raises(ValueError):
+        ct2.read_model_bin(str(p))
