@@ -69,3 +69,21 @@ def test_rejects_unknown_versions(tmp_path):
     p.write_bytes(struct.pack("<I", 99))
     with pytest.raises(ValueError):
         ct2.read_model_bin(str(p))
+
+
+@pytest.mark.parametrize("d,mels,dec,name", [(384, 80, 4, "tiny"), (512, 80, 6, "base"), (1280, 128, 32, "large-v3"),
+                                             (1280, 128, 4, "large-v3-turbo"), (1280, 80, 32, "large-v2")])
+def test_model_size_inferred_from_a_ct2_dir(tmp_path, d, mels, dec, name):
+    """WhisperModel(model_size_or_path=<CT2 dir>) picks the architecture from the tensor shapes (CT2's config.json
+    has no d_model)."""
+    from wmx.transcribe import _infer_name
+    v = {"encoder/conv1/weight": np.zeros((d, mels, 3), np.float16),
+         "encoder/position_encodings/encodings": np.zeros((1500, 1), np.float16),
+         "decoder/position_encodings/encodings": np.zeros((448, 1), np.float16),
+         "decoder/embeddings/weight": np.zeros((10, d), np.float16),
+         "encoder/layer_0/ffn/layer_norm/gamma": np.zeros(1, np.float32)}
+    for i in range(dec):
+        v[f"decoder/layer_{i}/ffn/layer_norm/gamma"] = np.zeros(1, np.float32)
+    ct2.write_model_bin(str(tmp_path / "model.bin"), v)
+    (tmp_path / "config.json").write_text('{"alignment_heads": [[2, 2]], "suppress_ids": [1, 2]}')
+    assert _infer_name(str(tmp_path)) == name
