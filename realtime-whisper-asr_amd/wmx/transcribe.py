@@ -255,6 +255,9 @@ class WhisperModel:
         else:
             self.model.init_synthetic(seed)
         self.name = name
+        # a checkpoint's own alignment heads win over the per-size table (CT2 keeps them in config.json, HF in
+        # generation_config.json; fine-tuned / distilled models differ from openai's table)
+        self.alignment_heads = _checkpoint_alignment_heads(model_dir) or ALIGNMENT_HEADS.get(name)
         self.max_batch = max_batch
         self.default_beam = beam_size
         self.max_new_tokens = max_new_tokens
@@ -280,7 +283,7 @@ class WhisperModel:
                                      language=language_token, without_timestamps=without_timestamps,
                                      max_initial_timestamp_index=mit, suppress_blank=suppress_blank,
                                      suppress_tokens=sup, word_timestamps=word_timestamps,
-                                     alignment_heads=ALIGNMENT_HEADS.get(self.name), use_graph=self.use_graph,
+                                     alignment_heads=self.alignment_heads, use_graph=self.use_graph,
                                      max_audio_samples=2 * 480000, temperature=temperature, best_of=best_of,
                                      sample_seed=self.sample_seed)
         return self._ctx[key]
@@ -471,6 +474,21 @@ class WhisperModel:
                                                       0.0, 0, no_speech_threshold, log_prob_threshold)
                 out[i] = segs
         return out
+
+
+def _checkpoint_alignment_heads(model_dir):
+    """[[layer, head], ...] from a model directory's config.json (CTranslate2) or generation_config.json (HF)."""
+    import json
+    import os
+    if not model_dir:
+        return None
+    for f in ("config.json", "generation_config.json"):
+        p = os.path.join(model_dir, f)
+        if os.path.exists(p):
+            heads = json.load(open(p)).get("alignment_heads")
+            if heads:
+                return [tuple(int(x) for x in h) for h in heads]
+    return None
 
 
 def _infer_name(model_dir):

@@ -87,3 +87,13 @@ def test_model_size_inferred_from_a_ct2_dir(tmp_path, d, mels, dec, name):
     ct2.write_model_bin(str(tmp_path / "model.bin"), v)
     (tmp_path / "config.json").write_text('{"alignment_heads": [[2, 2]], "suppress_ids": [1, 2]}')
     assert _infer_name(str(tmp_path)) == name
+
+
+def test_checkpoint_alignment_heads(tmp_path):
+    from wmx.transcribe import _checkpoint_alignment_heads
+    assert _checkpoint_alignment_heads(None) is None and _checkpoint_alignment_heads(str(tmp_path)) is None
+    (tmp_path / "config.json").write_text('{"alignment_heads": [[2, 3], [3, 0]], "lang_ids": [1]}')
+    assert _checkpoint_alignment_heads(str(tmp_path)) == [(2, 3), (3, 0)]
+    (tmp_path / "config.json").write_text('{"d_model": 384}')
+    (tmp_path / "generation_config.json").write_text('{"alignment_heads": [[1, 1]]}')
+    assert _checkpoint_alignment_heads(str(tmp_path)) == [(1, 1)]
