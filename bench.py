@@ -84,13 +84,6 @@ def parse():
     return p.parse_args()
 
 
-class _ArenaView:
-    """Zero-copy torch view of the library's weight arena (for the RCCL broadcast)."""
-
-    def __init__(self, ptr, nbytes):
-        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}
-
-
 def _cpu_sample(W, d, args, steps_done, n_text):
     """One bounded sample of the oracle on this host: one 30 s window, log-mel + encoder + language detection +
     prompt prefill + 4 beam decode steps (per-step time extrapolated to the GPU run's step count) + the word
@@ -135,9 +128,12 @@ def cpu_baseline(model, args, steps_done, n_text):
     from threadpoolctl import threadpool_limits
 
     d = O.DIMS[args.model] if args.model in O.DIMS else None
-    # the host share this process may use: the box's OMP_NUM_THREADS (its CPU share; the affinity mask lists the
-    # whole machine there), else the affinity mask
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    # BASELINE.md §4 states the host core count from the affinity mask; on the GPU box that mask lists the whole
+    # machine while this process's CPU share is OMP_NUM_THREADS (16), so the all-cores leg runs at the smaller of the
+    # two and both are reported
+    affinity = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
+    cores = min(affinity, omp) if omp else affinity
     t0 = time.perf_counter()
     W = {}
     for name, shape, _, _ in O.tensor_specs(d):
@@ -155,6 +151,7 @@ def cpu_baseline(model, args, steps_done, n_text):
     totalc = out[cores][0]
     return {"value": round(30.0 / total4, 4), "unit": "x_realtime", "cores": 4, "kind": "proxy",
             "all_cores": {"value": round(30.0 / totalc, 4), "cores": cores},
+            "host": {"sched_getaffinity": affinity, "OMP_NUM_THREADS": omp},
             "sample": f"1 x 30 s window of {args.model} through the numpy fp32 oracle (faster-whisper/CT2 absent: "
                       f"proxy): log-mel + encoder + language detect + prefill + 4 beam-{args.beam} decode steps "
                       f"(per-step time extrapolated to the GPU run's {steps_done} steps) + word alignment over "
@@ -318,14 +315,7 @@ def main():
     model = engine.Model(args.model, local, dt)
     t = time.time()
     if world > 1:
-        if rank == 0:
-            model.init_synthetic(args.seed)
-        ptr, nbytes = model.arena()
-        view = torch.as_tensor(_ArenaView(ptr, nbytes), device=f"cuda:{local}")
-        torch.cuda.synchronize()
-        D.broadcast_arena(view, src=0)  # RCCL over xGMI: the only collective of the job
-        torch.cuda.synchronize()
-        model.mark_loaded()
+        D.share_weights(model, rank, torch.device("cuda", local), seed=args.seed)  # RCCL over xGMI
     else:
         model.init_synthetic(args.seed)
     log(f"[rank {rank}] weights ready in {time.time() - t:.2f}s ({model.n_params() / 1e9:.2f} B params)")

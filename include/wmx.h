@@ -206,6 +206,19 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float*
 wmx_status wmx_ctx_record(wmx_ctx* c, int max_steps);
 wmx_status wmx_ctx_recorded(wmx_ctx* c, float* logits, int32_t* sel, int* n_steps, int* rows);
 
+/* the sampling seed of the following wmx_transcribe calls (temperature > 0; initially wmx_opts.sample_seed).  The
+ * Gumbel noise is a pure function of (seed, row, slot, token), so a caller that wants fresh draws per window and per
+ * temperature of a fallback schedule (as faster-whisper / CT2 draw new randomness per generate call) passes a
+ * different seed per call; the same seed replays the same draws. */
+wmx_status wmx_ctx_set_sample_seed(wmx_ctx* c, uint32_t seed);
+
+/* word-alignment matrix of window b of the last wmx_transcribe (tests only): the matrix the DTW ran on -- for the
+ * rows <|notimestamps|> + text tokens (n = n_text_tokens + 1) and the first nf = seek_frames / 2 encoder frames, the
+ * mean over the alignment heads of softmax(cross-attention scores over nf frames), normalised per frame over the
+ * token axis and median-filtered along frames (openai timing.find_alignment `matrix`, via faster-whisper).
+ * out [n][nf] (nullable: sizes only). */
+wmx_status wmx_ctx_alignment_matrix(wmx_ctx* c, int b, float* out, int* n, int* nf);
+
 /* host-only check of the decode GEMM's addressing (no GPU needed; tests only): for a packed-weight launch of
  * M rows x N columns x K (lda = A's row stride), split = 0 as the epilogue launches (S = 1) or 1 as the split-K
  * partial launches with a part_cap-element partial buffer, out9 = {S, MT, NCT, NW, KU, weight elements touched

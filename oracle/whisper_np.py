@@ -939,9 +939,10 @@ def alignment_heads_default(d: Dims):
 
 
 def find_alignment(W, d: Dims, enc: np.ndarray, language: int, task: str, text_tokens, num_frames: int,
-                   align_heads=None, medfilt_width: int = 7):
+                   align_heads=None, medfilt_width: int = 7, return_matrix: bool = False):
     """Returns (text_indices, time_indices, text_token_probs, jump_times) for the token sequence
-    sot_sequence + [<|notimestamps|>] + text + [eot] (openai timing.find_alignment)."""
+    sot_sequence + [<|notimestamps|>] + text + [eot] (openai timing.find_alignment); with return_matrix, also the
+    matrix the DTW runs on ([len(text) + 1][num_frames // 2], before the sign flip)."""
     sp = special_tokens(d.n_vocab)
     heads = align_heads if align_heads is not None else alignment_heads_default(d)
     sot = sot_sequence(sp, language, task)
@@ -961,4 +962,6 @@ def find_alignment(W, d: Dims, enc: np.ndarray, language: int, task: str, text_t
     ti, tj = dtw(-matrix.astype(np.float32))
     jumps = np.pad(np.diff(ti), (1, 0), constant_values=1).astype(bool)
     jump_times = tj[jumps] / 50.0
+    if return_matrix:
+        return ti, tj, text_token_probs, jump_times, matrix
     return ti, tj, text_token_probs, jump_times

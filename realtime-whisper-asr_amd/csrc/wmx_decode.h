@@ -10,9 +10,11 @@ struct RuleOpts {
   int max_init;          // -1 = none
   int without_ts;
   const uint32_t* mask;  // suppress-token bitmask [ceil(V/32)]
-  // sampling (temperature > 0): selection key = logit / T + Gumbel(hash(seed, row, *slot, token)); inv_temp 0 = off
+  // sampling (temperature > 0): selection key = logit / T + Gumbel(hash(*seed, row, *slot, token)); inv_temp 0 = off.
+  // The seed is read from device memory so that the captured decode graph draws with the seed of each call
+  // (wmx_ctx_set_sample_seed), not the one baked in at capture.
   float inv_temp = 0.f;
-  uint32_t seed = 0;
+  const uint32_t* seed = nullptr;
   const int* slot = nullptr;
 };
 

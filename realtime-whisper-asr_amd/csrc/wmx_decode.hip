@@ -279,6 +279,7 @@ __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict
                                                          RowState rs, const int* row_map, float* __restrict__ ws) {
   const int r = blockIdx.x, sl = blockIdx.y;
   const int sample_slot = SAMPLE ? *o.slot : 0;
+  const uint32_t sample_seed = SAMPLE ? *o.seed : 0u;
   const int lrow = row_map ? row_map[r] : r;
   const float* x = logits + (long)lrow * ldl;
   const int ns = rs.ns[r], lt = rs.last[r], pt = rs.pen[r], lts = rs.last_ts[r];
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(kSelA) void logits_select_a(const float* __restrict
       const bool ok = t < o.V && !((mw[u] >> (t & 31)) & 1u) && allowed_rules(o, t, ns, last_ts, pen_ts, lts);
       const float v = ok ? (hh ? xv[u].y : xv[u].x) : -INFINITY;
       const int ti = ok ? t : 0x7FFFFFFF;
-      const float key = SAMPLE ? (ok ? v * o.inv_temp + sample_gumbel(o.seed, r, sample_slot, t) : -INFINITY) : v;
+      const float key = SAMPLE ? (ok ? v * o.inv_temp + sample_gumbel(sample_seed, r, sample_slot, t) : -INFINITY) : v;
       if (t < o.tb) {  // wave-uniform except in the slice that holds timestamp_begin
         text = ms_add_nb(text, v);
         tmax = fmaxf(tmax, v);
@@ -813,7 +814,7 @@ void launch_logits_select(const float* logits, int ldl, const RuleOpts& o, const
   WMX_CHECK(o.V <= kSlices * kSelPer && ldl % 2 == 0, "logits select: vocabulary / row stride");
   RowState rs{rp.ns, rp.last, rp.pen, rp.last_ts, rp.done, rp.sum_lp};
   if (o.inv_temp > 0.f) {  // sampling: one Gumbel-max draw per row
-    WMX_CHECK(KP == 1 && o.slot, "logits select: sampling draws one token per row");
+    WMX_CHECK(KP == 1 && o.slot && o.seed, "logits select: sampling draws one token per row");
     hipLaunchKernelGGL((logits_select_a<1, true>), dim3(R, kSlices), dim3(kSelA), 0, st, logits, ldl, o, rs, row_map, ws);
     hipLaunchKernelGGL((logits_select_b<1, true>), dim3(R), dim3(64), 0, st, ws, o, tok, lp, logits, ldl, row_map);
     WMX_HIP(hipGetLastError());

@@ -1241,7 +1241,11 @@ __device__ __forceinline__ void packed_red_tail(const RedTail& rt, const float* 
 // is straight-line code.  The unsplit residual producers (MT + NCT <= 3, fc2: 10 k-steps per wave) take 5 per batch.
 template <int MT, int NCT>
 constexpr int packed_ku() {
+#ifdef WMX_PACKED_GUARDED  // diagnostic build of round 2's faulting form: per-step guarded loads
+  return (MT + NCT) <= 3 ? 4 : (MT + NCT) <= 8 ? 2 : 1;
+#else
   return (MT + NCT) <= 3 ? 5 : (MT + NCT) <= 8 ? 2 : 1;
+#endif
 }
 
 // S == 1 epilogues of the LayerNorm-folded decode step (wmx_common.h row_ln_from_stats): the residual producer
@@ -1350,7 +1354,25 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     u16x8 b[KU][NCT], av[KU][MT];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
+#ifdef WMX_PACKED_GUARDED
+      if (kk + u >= ks1) continue;
+      int k = kk + u;
+      {  // diagnostic bounds check: report (and do not issue) any load outside the packed weights / the A rows
+        bool bad = k < 0 || k >= ksteps;
+#pragma unroll
+        for (int j = 0; j < NCT; ++j)
+          bad |= (wt[j] + ((long)k << 9) - Wp) + 8 > (long)ntiles * ksteps * 512 || (wt[j] + ((long)k << 9)) < Wp;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) bad |= (ar[i] + k * 32 - A) + 8 > (long)(M - 1) * lda + K || (ar[i] + k * 32) < A;
+        if (bad) {
+          printf("WMX_PACKED_GUARDED OOB: blk (%d,%d,%d) wave %d lane %d kk %d u %d ks0 %d ks1 %d M %d N %d K %d S %d\n",
+                 blockIdx.x, blockIdx.y, blockIdx.z, wave, lane, kk, u, ks0, ks1, M, N, K, S);
+          k = ks0;
+        }
+      }
+#else
       const int k = min(kk + u, ks1 - 1);  // clamped: a duplicate load of the wave's last k-step, MFMA skipped
+#endif
 #pragma unroll
       for (int j = 0; j < NCT; ++j) b[u][j] = stream_load(reinterpret_cast<const u16x8*>(wt[j] + ((long)k << 9)));
 #pragma unroll

@@ -538,6 +538,11 @@ struct Ctx {
   int* rec_sel = nullptr;
   int* rec_base = nullptr;
   int rec_cap = 0, rec_R = 0;
+  // word-alignment matrices of the last transcribe (wmx_ctx_alignment_matrix, tests): [B][Tn][1500] as the DTW read
+  // them, and per window the text-token count and the content frames
+  std::vector<float> last_align;
+  std::vector<int> last_ntext, last_nframes;
+  int last_align_Tn = 0;
 };
 
 static void sync_at(Ctx& c, int line) {
@@ -1424,7 +1429,7 @@ static void select_and_update(Ctx& c, int B, const int* row_map) {
               c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
   if (c.sampling) {
     ro.inv_temp = 1.0f / c.o.temperature;
-    ro.seed = c.o.sample_seed;
+    ro.seed = reinterpret_cast<const uint32_t*>(c.slot + 2);  // written per call (transcribe prologue)
     ro.slot = c.slot;
   }
   launch_logits_select(c.logits, c.ldl, ro, c.rp, R, c.beam ? K + 1 : 1, c.ctok, c.clp, row_map, c.sel_ws, c.st);
@@ -1624,6 +1629,11 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     dec_logits(c, c.gather, 2 * B);
     launch_token_prob(c.logits + (size_t)B * c.ldl, c.ldl, V, sp.no_speech, B, c.nospeech, c.st);
     sync(c);
+  }
+  // this call's sampling seed (slot word 2, read by the captured selection launches)
+  if (c.sampling) {
+    c.pinned_i[3] = (int)c.o.sample_seed;
+    WMX_HIP(hipMemcpyAsync(c.slot + 2, c.pinned_i + 3, 4, hipMemcpyHostToDevice, c.st));
   }
   // first selection from the prefill logits (rows of a window share their window's logits row)
   const int max_new = std::max(0, std::min(c.o.max_new_tokens, T - Pmax));
@@ -1866,6 +1876,10 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
         }
       });
     for (auto& x : th) x.join();
+    c.last_align.swap(mat);  // kept for wmx_ctx_alignment_matrix (a swap: no copy on the hot path)
+    c.last_ntext = ntext;
+    c.last_nframes = nframes;
+    c.last_align_Tn = Tn;
   }
   rec(c, 7);
   WMX_HIP(hipEventSynchronize(c.ev[7]));
@@ -2458,6 +2472,26 @@ wmx_status wmx_ctx_recorded(wmx_ctx* x, float* logits, int32_t* sel, int* n_step
     if (logits)
       WMX_HIP(hipMemcpy(logits, c.rec_logits, (size_t)n * c.rec_R * c.m->d.n_vocab * 4, hipMemcpyDeviceToHost));
     if (sel) WMX_HIP(hipMemcpy(sel, c.rec_sel, (size_t)n * c.rec_R * 2 * 4, hipMemcpyDeviceToHost));
+  });
+}
+
+wmx_status wmx_ctx_set_sample_seed(wmx_ctx* x, uint32_t seed) {
+  return guard([&] { x->c.o.sample_seed = seed; });
+}
+
+wmx_status wmx_ctx_alignment_matrix(wmx_ctx* x, int b, float* out, int* n, int* nf) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(n && nf, "alignment_matrix: null argument");
+    WMX_CHECK(!c.last_align.empty() && b >= 0 && b < (int)c.last_ntext.size(),
+              "alignment_matrix: no word alignment for this window in the last transcribe");
+    const int rows = c.last_ntext[b] + 1, cols = c.last_nframes[b] / 2;
+    *n = rows;
+    *nf = cols;
+    if (!out) return;
+    for (int i = 0; i < rows; ++i)
+      std::memcpy(out + (size_t)i * cols, c.last_align.data() + ((size_t)b * c.last_align_Tn + 3 + i) * 1500,
+                  (size_t)std::max(cols, 0) * 4);
   });
 }
 

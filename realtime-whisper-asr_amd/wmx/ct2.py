@@ -266,7 +266,23 @@ def hf_to_ct2(sd, dims, quantize: str = "float32"):
     return v, {"decoder/projection/weight": "decoder/embeddings/weight"}
 
 
+def resolve_aliases(v: dict, aliases: dict) -> dict:
+    """The variable dict with every alias bound to its target's array.  CTranslate2's converter replaces ANY variable
+    that is element-wise equal to an earlier one (in name order) with an alias, not only the tied output projection:
+    a fine-tuned or distilled model can store e.g. identical LayerNorm or bias vectors once.  Chains resolve."""
+    out = dict(v)
+    for a in aliases:
+        t, seen = aliases[a], {a}
+        while t not in out and t in aliases and t not in seen:
+            seen.add(t)
+            t = aliases[t]
+        if t not in out:
+            raise KeyError(f"CT2 alias {a!r} -> {aliases[a]!r}: target not in the model")
+        out.setdefault(a, out[t])
+    return out
+
+
 def load_ct2_dir(model_dir: str):
-    """(dims, HF state dict) of a CT2 Whisper model directory (model.bin)."""
-    _, _, v, _ = read_model_bin(os.path.join(model_dir, "model.bin"))
-    return ct2_to_hf(v)
+    """(dims, HF state dict) of a CT2 Whisper model directory (model.bin), aliases resolved."""
+    _, _, v, aliases = read_model_bin(os.path.join(model_dir, "model.bin"))
+    return ct2_to_hf(resolve_aliases(v, aliases))

@@ -48,6 +48,35 @@ def broadcast_arena(tensor, src: int = 0):
     return tensor
 
 
+class _ArenaView:
+    """Zero-copy CUDA-array-interface view of a device allocation (libwmx's weight arena)."""
+
+    def __init__(self, ptr, nbytes):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+
+def arena_tensor(model, device):
+    """A torch uint8 tensor aliasing the model's weight arena on `device` (no copy)."""
+    import torch
+    ptr, nbytes = model.arena()
+    return torch.as_tensor(_ArenaView(ptr, nbytes), device=device)
+
+
+def share_weights(model, rank: int, device, seed: int | None = None, src: int = 0):
+    """Make every rank's weights identical: rank `src` initialises (PRNG `seed`, or keeps what is loaded), then ONE RCCL
+    broadcast of the whole arena (parameters plus the derived MX-fp8 / row-major copies) over xGMI, then every rank
+    marks its arena loaded.  The only data-path collective of the job."""
+    import torch
+    if rank == src and seed is not None:
+        model.init_synthetic(seed)
+    view = arena_tensor(model, device)
+    torch.cuda.synchronize(device)
+    broadcast_arena(view, src=src)
+    torch.cuda.synchronize(device)
+    model.mark_loaded()
+    return view
+
+
 def max_over_ranks(value: float, device="cpu") -> float:
     import torch
     import torch.distributed as dist

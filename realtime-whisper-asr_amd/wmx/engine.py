@@ -247,6 +247,11 @@ class Context:
                                         fptr(lg) if lg is not None else None, max(1, logits_every)))
         return top1, lg
 
+    def set_sample_seed(self, seed: int):
+        """Seed of the Gumbel draws of the following transcribe calls (wmx_ctx_set_sample_seed)."""
+        self.opts.sample_seed = int(seed) & 0xFFFFFFFF
+        check(lib.wmx_ctx_set_sample_seed(self._h, self.opts.sample_seed))
+
     def record(self, max_steps: int):
         """Parity recorder of the decode search (wmx_ctx_record); 0 turns it off."""
         check(lib.wmx_ctx_record(self._h, int(max_steps)))
@@ -259,6 +264,15 @@ class Context:
         sel = np.empty((n.value, R.value, 2), np.int32)
         check(lib.wmx_ctx_recorded(self._h, fptr(lg), iptr(sel), C.byref(n), C.byref(R)))
         return lg, sel
+
+    def alignment_matrix(self, b: int) -> np.ndarray:
+        """The word-alignment matrix window b's DTW ran on in the last transcribe (wmx_ctx_alignment_matrix):
+        [n_text_tokens + 1][seek_frames // 2]."""
+        n, nf = C.c_int(), C.c_int()
+        check(lib.wmx_ctx_alignment_matrix(self._h, int(b), None, C.byref(n), C.byref(nf)))
+        out = np.empty((n.value, nf.value), np.float32)
+        check(lib.wmx_ctx_alignment_matrix(self._h, int(b), fptr(out), C.byref(n), C.byref(nf)))
+        return out
 
     def _collect(self, res_ptr) -> list:
         r = res_ptr.contents

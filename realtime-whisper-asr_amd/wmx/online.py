@@ -633,6 +633,26 @@ class EnhancedVACOnlineASRProcessor(VACOnlineASRProcessor):
 # ------------------------------------------------------------------------------------------------
 # multi-stream batching (data parallel over independent streams, one GPU)
 # ------------------------------------------------------------------------------------------------
+# decoding options the batched multi-stream path carries; anything else in a stream's options raises
+_BATCH_KWARGS = ("task", "beam_size", "temperature", "best_of")
+
+
+def batch_transcribe_kwargs(asr):
+    """The decoding options one batched call uses, merged as CustomFasterWhisperASR.transcribe merges them
+    (asr_components.py:270-275): the ASR's transcribe_kargs, overridden by adaptive_params.get_transcribe_kwargs()
+    (speech_rate_audio_processor.py:234-237: beam size / temperature per call) when the ASR has adaptive params.
+    Options the batched path does not implement raise instead of being dropped."""
+    kw = dict(getattr(asr, "transcribe_kargs", None) or {})
+    ap = getattr(asr, "adaptive_params", None)
+    if ap:
+        kw.update(ap.get_transcribe_kwargs())
+    extra = sorted(k for k in kw if k not in _BATCH_KWARGS)
+    if extra:
+        raise NotImplementedError(f"StreamBatcher: transcribe options {extra} are not implemented on the batched "
+                                  f"multi-stream path (supported: {list(_BATCH_KWARGS)})")
+    return kw
+
+
 class StreamBatcher:
     """Runs the due process_iter() of many VAC streams as one batched transcribe on one MI355X.
 
@@ -656,11 +676,7 @@ class StreamBatcher:
                 outs[i] = (None, None, "")
         if due:
             reqs = [streams[i].online.prepare_iter() for i in due]
-            # the ASR's own decoding options, as CustomFasterWhisperASR.transcribe would pass them
-            # (asr_components.py:279-288): language (None = detect), task (set_translate_task), beam size
-            kw = dict(getattr(self.asr, "transcribe_kargs", None) or {})
-            if kw.get("vad_filter"):
-                raise NotImplementedError("StreamBatcher: vad_filter is not implemented")
+            kw = batch_transcribe_kwargs(self.asr)
             results = self.model.transcribe_batch([a for a, _ in reqs], [p for _, p in reqs],
                                                   language=getattr(self.asr, "original_language", None),
                                                   task=kw.get("task", "transcribe"), beam_size=kw.get("beam_size"),

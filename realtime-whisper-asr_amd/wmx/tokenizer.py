@@ -79,13 +79,17 @@ class _Base:
         return self.split_tokens_on_spaces(tokens)
 
     def split_tokens_on_unicode(self, tokens):
+        """openai / faster-whisper split_tokens_on_unicode, with the bounds guard transformers adds: a run that ends
+        inside a cut multi-byte character (the replacement character lies past the full decode) closes a word
+        instead of raising IndexError."""
         decoded_full = self.decode_with_timestamps(tokens)
         rc = "�"
         words, word_tokens, current, offset = [], [], [], 0
         for t in tokens:
             current.append(t)
             dec = self.decode_with_timestamps(current)
-            if rc not in dec or decoded_full[offset + dec.index(rc)] == rc:
+            if (rc not in dec or offset + dec.index(rc) >= len(decoded_full)
+                    or decoded_full[offset + dec.index(rc)] == rc):
                 words.append(dec)
                 word_tokens.append(current)
                 current = []

@@ -222,6 +222,14 @@ def _temperatures(temperature):
     return ts
 
 
+def call_seed(seed: int, call: int, temp_index: int) -> int:
+    """The sampling seed of one decode call: splitmix64 of (model seed, call counter, temperature index), low 32 bits."""
+    z = (seed * 0x9E3779B97F4A7C15 + (call << 8) + temp_index + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return (z ^ (z >> 31)) & 0xFFFFFFFF
+
+
 def get_end(segments):
     """faster-whisper get_end: the last word's end, else the last segment's end."""
     return next((w["end"] for s in reversed(segments) for w in reversed(s.get("words") or [])),
@@ -263,7 +271,12 @@ class WhisperModel:
         self.max_new_tokens = max_new_tokens
         self.suppress_tokens = [-1] if suppress_tokens is None else list(suppress_tokens)
         self.use_graph = use_graph
-        self.sample_seed = seed  # sampling (T > 0) is deterministic per model: the same audio draws the same samples
+        # sampling (T > 0): every decode call draws with its own seed, mixed from the model seed, a per-model call
+        # counter and the temperature's index in the fallback schedule (faster-whisper / CT2 draw fresh randomness per
+        # generate call, so a T = 0.4 retry after a failed T = 0.2 attempt is not correlated with it); the same model
+        # seed and call sequence replays the same draws
+        self.sample_seed = seed
+        self._sample_calls = 0
         self._ctx = {}
 
     def context(self, beam_size, language_token, task, word_timestamps, without_timestamps=False, patience=1.0,
@@ -370,8 +383,11 @@ class WhisperModel:
         avg_logprob among those under the compression threshold (else among all), reported at the last
         temperature.  T = 0: beam search (beam_size); T > 0: best_of sampled rows."""
         results = []
-        for t in temps:
+        for ti, t in enumerate(temps):
             ctx = self.context(beam_size, lang_tok, task, word_timestamps, temperature=t, best_of=best_of, **ctx_kw)
+            if t > 0:
+                ctx.set_sample_seed(call_seed(self.sample_seed, self._sample_calls, ti))
+                self._sample_calls += 1
             # the window's features come from the whole buffer (global max normalisation) -> pass the full audio
             r = ctx.transcribe([audio], prompts=[prompt], seek=[seek])[0]
             cr = compression_ratio(self.tokenizer.decode([x for x in r.tokens if x < self.tokenizer.sp.eot]).strip())
@@ -442,7 +458,7 @@ class WhisperModel:
                 p = prompts[i]
                 try:
                     segs, _ = self.transcribe(a, language=language, task=task, beam_size=beam, best_of=best_of,
-                                              temperature=temps, initial_prompt=p if p else None,
+                                              temperature=temps, initial_prompt=p,
                                               word_timestamps=word_timestamps,
                                               no_speech_threshold=no_speech_threshold,
                                               log_prob_threshold=log_prob_threshold)
@@ -453,6 +469,9 @@ class WhisperModel:
                 short.append(i)
         ctx = self.context(beam, lang_tok, task, word_timestamps, temperature=temps[0], best_of=best_of)
         for b0 in range(0, len(short), self.max_batch):
+            if temps[0] > 0:  # fresh draws per call (call_seed)
+                ctx.set_sample_seed(call_seed(self.sample_seed, self._sample_calls, 0))
+                self._sample_calls += 1
             idx = short[b0: b0 + self.max_batch]
             chunk = [np.asarray(audios[i], np.float32) for i in idx]
             pr = []

@@ -97,3 +97,26 @@ def test_checkpoint_alignment_heads(tmp_path):
     (tmp_path / "config.json").write_text('{"d_model": 384}')
     (tmp_path / "generation_config.json").write_text('{"alignment_heads": [[1, 1]]}')
     assert _checkpoint_alignment_heads(str(tmp_path)) == [(1, 1)]
+
+
+def test_aliased_layer_variables_resolve(tmp_path):
+    """CTranslate2's converter stores a variable equal to an earlier one as an alias: a LayerNorm beta and
+    a bias deduplicated that way, plus an alias chain, load as their targets' values."""
+    d = O.DIMS["micro"]
+    sd = _hf(d)
+    sd["decoder.layers.1.final_layer_norm.bias"] = sd["decoder.layers.0.final_layer_norm.bias"].copy()
+    sd["encoder.layers.1.fc2.bias"] = sd["encoder.layers.0.fc2.bias"].copy()
+    v, al = ct2.hf_to_ct2(sd, _dims(d), "float32")
+    al = dict(al)
+    al["decoder/layer_1/ffn/layer_norm/beta"] = "decoder/layer_0/ffn/layer_norm/beta"
+    al["encoder/layer_1/ffn/linear_1/bias"] = "encoder/layer_0/ffn/linear_1/bias"
+    del v["decoder/layer_1/ffn/layer_norm/beta"], v["encoder/layer_1/ffn/linear_1/bias"]
+    p = tmp_path / "model.bin"
+    ct2.write_model_bin(str(p), v, al)
+    dims, hf = ct2.load_ct2_dir(str(tmp_path))
+    np.testing.assert_array_equal(hf["decoder.layers.1.final_layer_norm.bias"], sd["decoder.layers.0.final_layer_norm.bias"])
+    np.testing.assert_array_equal(hf["encoder.layers.1.fc2.bias"], sd["encoder.layers.0.fc2.bias"])
+    chained = ct2.resolve_aliases({"x": np.ones(2)}, {"a": "b", "b": "x"})
+    np.testing.assert_array_equal(chained["a"], np.ones(2))
+    with pytest.raises(KeyError):
+        ct2.resolve_aliases({}, {"a": "missing"})

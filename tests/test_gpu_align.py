@@ -1,0 +1,92 @@
+"""GPU parity of the word-level timestamps at the shape the bench runs them.
+
+The reference forces word_timestamps=True (/root/reference/asr_components.py:285) and ts_words reads s.words
+(asr_components.py:291-297), so every committed word goes through faster-whisper's find_alignment: a teacher-forced
+decoder pass over sot + <|notimestamps|> + text + eot, the alignment heads' cross-attention -> softmax over the content
+frames -> per-frame normalisation over the tokens -> median filter (7) -> mean over heads -> DTW -> jump times.
+
+Here the device half (the alignment forward, align_softmax / colnorm / median_acc in wmx_runtime.hip) is compared with
+the oracle's matrix (oracle.find_alignment, openai timing.py semantics pinned to HF's _median_filter /
+_dynamic_time_warping by tests/test_oracle_golden.py) at large-v3 width: d = 1280, 20 heads, the 10 large-v3 alignment
+heads (decoder layers 7..25, so the model carries 26 decoder layers), beam 5 as in the bench, >= 100 text tokens per
+window.  Tolerances:
+  * the matrix: relative L2 <= 3e-2 (the bf16 bound of tests/test_gpu_parity.py);
+  * jump_times: EXACTLY the library DTW (wmx_debug_dtw) of the device matrix, and within one frame (20 ms) of the
+    oracle's for >= 95 % of the tokens (the DTW path on a 16-bit-noisy cost can move where two paths nearly tie);
+  * text-token probabilities within 2e-2 absolute.
+"""
+import numpy as np
+import pytest
+
+from oracle import whisper_np as O
+from wmx import synth
+
+pytestmark = pytest.mark.gpu
+
+# large-v3 width: 1 encoder layer (the alignment runs on the encoder output, which the oracle recomputes from the same
+# mel), 26 decoder layers so that every large-v3 alignment head exists
+ALN = O.Dims(128, 51866, 1280, 20, 1, 1280, 20, 26)
+REL_BF16 = 3e-2
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _jumps(ti, tj):
+    ti, tj = np.asarray(ti), np.asarray(tj)
+    jumps = np.pad(np.diff(ti), (1, 0), constant_values=1).astype(bool)
+    return tj[jumps] / 50.0
+
+
+def _lib_dtw(matrix):
+    """wmx_debug_dtw: the library's host DTW (the one wmx_transcribe runs) on -matrix."""
+    import ctypes as C
+    from wmx._lib import check, lib
+    N, M = matrix.shape
+    x = np.ascontiguousarray(matrix, np.float32)
+    ti = np.zeros(N + M, np.int32)
+    tj = np.zeros(N + M, np.int32)
+    n = C.c_int()
+    check(lib.wmx_debug_dtw(x.ctypes.data_as(C.POINTER(C.c_float)), N, M, M,
+                            ti.ctypes.data_as(C.POINTER(C.c_int32)), tj.ctypes.data_as(C.POINTER(C.c_int32)),
+                            C.byref(n)))
+    return ti[: n.value], tj[: n.value]
+
+
+def test_word_alignment_matrix_large_v3_heads_beam5():
+    from wmx import engine as E
+    d = ALN
+    ed = E.ModelDims(d.n_mels, d.n_vocab, d.n_audio_state, d.n_audio_head, d.n_audio_layer, d.n_text_state,
+                     d.n_text_head, d.n_text_layer)
+    m = E.Model(ed, 0, "bfloat16").init_synthetic(11)
+    # the oracle reads the device's weights back (bit-exact with O.make_weights: test_gpu_parity.test_weights_bit_exact)
+    W = {name: m.get_tensor(name, shape) for name, shape, _, _ in O.tensor_specs(d)}
+    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
+    heads = E.ALIGNMENT_HEADS["large-v3"]
+    sp = O.special_tokens(d.n_vocab)
+    ctx = E.Context(m, max_batch=2, beam_size=5, max_new_tokens=120, word_timestamps=True, alignment_heads=heads,
+                    language=sp.lang0)
+    audios = [synth.speech_like(801, 480000), synth.speech_like(802, 400000)]
+    res = ctx.transcribe(audios)
+    for b, (a, r) in enumerate(zip(audios, res)):
+        text = [t for t in r.tokens if t < sp.eot]
+        assert len(text) >= 100, len(text)
+        dev = ctx.alignment_matrix(b)
+        assert dev.shape == (len(text) + 1, r.seek_frames // 2), (dev.shape, len(text), r.seek_frames)
+        # the jump times are exactly the library DTW of this matrix
+        ti, tj = _lib_dtw(dev)
+        np.testing.assert_array_equal(r.jump_times, _jumps(ti, tj).astype(np.float32))
+        # the oracle's matrix for the same tokens
+        enc = O.encoder(W, d, O.logmel_segment(a, d.n_mels))
+        oti, otj, probs, jt, ref = O.find_alignment(W, d, enc, sp.lang0, "transcribe", text, r.seek_frames,
+                                                     align_heads=heads, return_matrix=True)
+        e = rel_l2(dev, ref)
+        err = np.abs(r.jump_times - jt)
+        within = float(np.mean(err <= 0.02 + 1e-6))
+        print(f"window {b}: {len(text)} text tokens x {dev.shape[1]} frames, matrix rel_l2 {e:.2e}, "
+              f"max abs {float(np.max(np.abs(dev - ref))):.3f}; jump times within 1 frame {within:.3f}, "
+              f"max err {float(err.max()):.2f} s; token probs max err {float(np.max(np.abs(r.text_token_probs - probs))):.2e}")
+        assert e <= REL_BF16, e
+        assert within >= 0.95, (within, r.jump_times, jt)
+        np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)

@@ -1,0 +1,111 @@
+"""Correctness of the configuration bench.py times: context groups decoding CONCURRENTLY on one shared model.
+
+bench.py splits its 8 windows over 2 decoding contexts (each its own HIP stream and captured decode graph, both on
+one read-only wmx_model) and runs them from two host threads at once (bench.py step(); ctypes drops the GIL inside
+libwmx).  Here the same shape runs at large-v3 width (d 1280, 20 heads, vocab 51866, 2 decoder layers): 2 contexts x
+4 windows x beam 5, language auto-detect, word timestamps on, the hipGraph decode and the in-situ probes on, started
+from two threads together, several times:
+  * every result (tokens, sum_logprob, no_speech_prob, language, jump_times, token probabilities) must equal, bit for
+    bit, the result of the same context run alone (the kernels are deterministic: fixed-order reductions);
+  * with the search recorder on (both contexts, concurrently), oracle.search_replay must choose exactly the device's
+    selection at every step of both groups, and oracle.rank_final its final sequence.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import whisper_np as O
+from wmx import synth
+
+pytestmark = pytest.mark.gpu
+
+WIDE2 = O.Dims(128, 51866, 1280, 20, 1, 1280, 20, 2)
+EPS_TIE = 1e-3
+
+
+def _edims(d):
+    from wmx import engine as E
+    return E.ModelDims(d.n_mels, d.n_vocab, d.n_audio_state, d.n_audio_head, d.n_audio_layer, d.n_text_state,
+                       d.n_text_head, d.n_text_layer)
+
+
+def _run_concurrently(ctxs, batches):
+    out, err = [None] * len(ctxs), []
+    go = threading.Barrier(len(ctxs))
+
+    def work(i):
+        try:
+            go.wait()
+            out[i] = ctxs[i].transcribe(batches[i])
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(ctxs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if err:
+        raise err[0]
+    return out
+
+
+def _same(a, b, tag):
+    assert a.tokens == b.tokens, (tag, a.tokens, b.tokens)
+    assert a.sum_logprob == b.sum_logprob and a.no_speech_prob == b.no_speech_prob, tag
+    assert a.language == b.language and a.language_prob == b.language_prob, tag
+    np.testing.assert_array_equal(a.jump_times, b.jump_times, err_msg=tag)
+    np.testing.assert_array_equal(a.text_token_probs, b.text_token_probs, err_msg=tag)
+
+
+def test_two_groups_concurrent_equal_sequential_and_replay():
+    from wmx import engine as E
+    m = E.Model(_edims(WIDE2), 0, "bfloat16").init_synthetic(5)
+    sp = O.special_tokens(WIDE2.n_vocab)
+    K, n_new = 5, 40
+    ctxs = [E.Context(m, max_batch=4, beam_size=K, max_new_tokens=n_new, language=None, word_timestamps=True,
+                      use_graph=True) for _ in range(2)]
+    for c in ctxs:
+        c.set_probe(True, 1)  # as bench.py: probes captured into the step graphs
+    audios = [synth.speech_like(900 + i, 480000) for i in range(8)]
+    batches = [audios[:4], audios[4:]]
+    alone = [ctxs[g].transcribe(batches[g]) for g in range(2)]
+    for r in alone[0] + alone[1]:
+        assert len(r.tokens) == n_new and r.jump_times is not None
+    for rep in range(3):
+        both = _run_concurrently(ctxs, batches)
+        for g in range(2):
+            for b in range(4):
+                _same(both[g][b], alone[g][b], f"rep {rep} group {g} window {b}")
+    # search replay of both groups' recorded steps, the groups again running concurrently
+    for c in ctxs:
+        c.record(n_new)
+    both = _run_concurrently(ctxs, batches)
+    opt_langs = []
+    for g in range(2):
+        res = both[g]
+        for b in range(4):
+            _same(res[b], alone[g][b], f"recorded group {g} window {b}")
+        lg, sel = ctxs[g].recorded()
+        assert lg.shape[:2] == (n_new, 4 * K)
+        langs = {r.language for r in res}
+        opt_langs.append(sorted(langs))
+        # the replay needs one language per window: windows share the options unless their detected language
+        # differs, in which case each window is replayed with its own
+        for b in range(4):
+            opt = O.DecodeOptions(language=res[b].language, beam_size=K, max_new_tokens=n_new)
+            rows = slice(b * K, (b + 1) * K)
+            info = O.search_replay(lg[:, rows], sel[:, rows] - np.array([b * K, 0], np.int32) * (sel[:, rows] >= 0),
+                                   K, sp, opt, eps=EPS_TIE)[0]
+            assert info["mismatch"] is None, (g, b, info["mismatch"])
+            if not info["ties"]:
+                assert info["steps"] >= 16, (g, b, info["steps"])
+                toks, sc, margin = O.rank_final(info["finished"], info["alive"], K)
+                if margin > EPS_TIE:
+                    assert res[b].tokens == toks, (g, b)
+                    assert abs(res[b].sum_logprob - sc) <= 1e-3 * max(1.0, abs(sc)), (g, b, res[b].sum_logprob, sc)
+            print(f"group {g} window {b}: replayed {info['steps']} steps, tie {info['ties']}")
+    print("detected languages per group", opt_langs)
+    for c in ctxs:
+        c.record(0)

@@ -6,7 +6,8 @@ Oracle: oracle/whisper_np.py encoder(..., mx8=True) on the same bf16-rounded wei
 projection quantized with the same OCP MX rule, fp32 accumulation).  Tolerance: relative L2 <= 3e-2 (the bf16
 path's bound: q/k/v and the attention stay bf16, and an activation whose f32 value differs in the last bits
 from the oracle's may round to the neighbouring e4m3 code).  The fp8 model's distance to the bf16 model is
-printed for reference.  Translate task: greedy tokens equal the oracle's until the first low-margin step."""
+printed for reference.  Translate task: every greedy step whose oracle margin exceeds 0.15 equals the oracle's
+argmax on the device's own path (>= 4 per window)."""
 import numpy as np
 import pytest
 
@@ -53,22 +54,17 @@ def test_mx8_translate_greedy_matches_oracle():
     W = O.make_weights(d, 9, "bf16")
     audios = [synth.speech_like(91, 480000), synth.speech_like(92, 96000)]
     res = ctx.transcribe(audios)
-    n_cmp = 0
+    from test_gpu_parity import greedy_forced_compare
+    per = []
     for a, r in zip(audios, res):
         enc = O.encoder(W, d, O.logmel_segment(a, d.n_mels), mx8=True)
         lang, _ = O.detect_language(W, d, enc)
         assert r.language == lang
-        ref = O.decode(W, d, enc, O.DecodeOptions(language=lang, beam_size=1, max_new_tokens=24, task="translate"))
-        k = 0
-        for _, margin in ref.trace:
-            if margin < 0.15:
-                break
-            k += 1
-        k = min(k, len(ref.tokens), len(r.tokens))
-        assert r.tokens[:k] == ref.tokens[:k], (r.tokens, ref.tokens, k)
-        n_cmp += k
-    print("mx8 translate greedy tokens compared", n_cmp)
-    assert n_cmp > 0
+        opt = O.DecodeOptions(language=lang, beam_size=1, max_new_tokens=24, task="translate")
+        n, _ = greedy_forced_compare(W, d, enc, opt, r.tokens, 0.15)
+        per.append(n)
+    print("mx8 translate greedy steps compared per window", per)
+    assert min(per) >= 4, per
 
 
 def test_mx8_full_depth_large_v3_translate():

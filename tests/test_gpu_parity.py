@@ -173,39 +173,47 @@ def test_decoder_logits_batched_windows(micro_ctx, dt):
             assert e <= REL[dt], (T, b, e)
 
 
+def greedy_forced_compare(W, d, enc, opt, tokens, tau):
+    """The oracle's greedy decode teacher-forced on the device's own tokens (O.decode(forced=...)): at every step whose
+    oracle top-2 margin (rule-masked logits) exceeds tau the device's token must be the oracle's argmax.  Unlike a
+    prefix comparison this does not stop at the first near-tie: the device's path is followed throughout.
+    Returns (steps compared, oracle result)."""
+    # the device's path ends with EOT (scored) unless it ran out of steps
+    ended = len(tokens) < opt.max_new_tokens
+    ref = O.decode(W, d, enc, opt, forced=list(tokens) + ([O.special_tokens(d.n_vocab).eot] if ended else []))
+    n = 0
+    for i, t in enumerate(tokens):
+        tok, margin = ref.trace[i]
+        if margin > tau:
+            assert t == tok, (i, t, tok, margin)
+            n += 1
+    return n, ref
+
+
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("n_audio", [3, 2])
 def test_greedy_transcribe_matches_oracle(micro_ctx, dt, n_audio):
-    """n_audio < max_batch checks that a partial batch addresses the KV cache rows like a full one."""
+    """n_audio < max_batch checks that a partial batch addresses the KV cache rows like a full one.  Every step of the
+    device's free-running greedy path whose oracle margin exceeds tau is compared (>= 4 per window required)."""
     d = O.DIMS["micro"]
     W = O.make_weights(d, 1, dt)
-    sp = O.special_tokens(d.n_vocab)
     ctx = micro_ctx[dt]
     audios = [synth.speech_like(41, 116800), synth.speech_like(42, 480000), synth.speech_like(43, 40000)][:n_audio]
     res = ctx.transcribe(audios)
-    n_cmp = 0
+    tau = 0.15 if dt == "bf16" else 0.03
+    per = []
     for a, r in zip(audios, res):
         mel = O.logmel_segment(a, d.n_mels)
         enc = O.encoder(W, d, mel)
         lang, lp = O.detect_language(W, d, enc)
         assert r.language == lang
         opt = O.DecodeOptions(language=lang, beam_size=1, max_new_tokens=32)
-        ref = O.decode(W, d, enc, opt)
-        # compare until the first low-margin step of the oracle
-        tau = 0.15 if dt == "bf16" else 0.03
-        k = 0
-        for (tok, margin) in ref.trace:
-            if margin < tau:
-                break
-            k += 1
-        k = min(k, len(ref.tokens), len(r.tokens))
-        assert r.tokens[:k] == ref.tokens[:k], (r.tokens, ref.tokens, k)
-        n_cmp += k
+        n, ref = greedy_forced_compare(W, d, enc, opt, r.tokens, tau)
+        per.append(n)
         assert abs(r.no_speech_prob - ref.no_speech_prob) < 5e-2
-        if r.tokens == ref.tokens:
-            assert abs(r.sum_logprob - ref.sum_logprob) < 0.05 * max(1, len(r.tokens))
-    print(dt, "greedy tokens compared", n_cmp)
-    assert n_cmp > 0
+        assert abs(r.sum_logprob - ref.sum_logprob) < 0.05 * max(1, len(r.tokens))
+    print(dt, "greedy steps compared per window", per)
+    assert min(per) >= 4, per
 
 
 def test_beam_transcribe_runs_and_is_deterministic(micro):
@@ -222,35 +230,31 @@ def test_beam_transcribe_runs_and_is_deterministic(micro):
         assert all(0 <= t < 51865 and t != sp.eot for t in r.tokens)
 
 
-def test_beam_matches_oracle_micro(micro):
+def test_word_alignment_matrix_micro(micro):
+    """The alignment matrix and jump times on the micro model in f16 (default heads = the second decoder half), by the
+    criteria of tests/test_gpu_align.py: matrix rel-L2 <= 5e-3 (f16), jump_times exactly the library DTW of the device
+    matrix, within one frame of the oracle's for >= 95 % of the tokens."""
     E = _engine()
     d = O.DIMS["micro"]
     W = O.make_weights(d, 1, "f16")
-    ctx = E.Context(micro["f16"], max_batch=1, beam_size=3, max_new_tokens=10, word_timestamps=False,
-                    language=50259)
-    a = synth.speech_like(61, 200000)
-    r = ctx.transcribe([a])[0]
-    enc = O.encoder(W, d, O.logmel_segment(a, d.n_mels))
-    ref = O.decode(W, d, enc, O.DecodeOptions(language=50259, beam_size=3, max_new_tokens=10))
-    print("beam gpu", r.tokens, "oracle", ref.tokens)
-    assert r.tokens[:3] == ref.tokens[:3]
-
-
-def test_word_alignment_close_to_oracle(micro):
-    E = _engine()
-    d = O.DIMS["micro"]
-    W = O.make_weights(d, 1, "f16")
-    ctx = E.Context(micro["f16"], max_batch=1, beam_size=1, max_new_tokens=16, word_timestamps=True, language=50259)
+    ctx = E.Context(micro["f16"], max_batch=1, beam_size=1, max_new_tokens=48, word_timestamps=True, language=50259)
     a = synth.speech_like(71, 240000)
     r = ctx.transcribe([a])[0]
     text = [t for t in r.tokens if t < 50257]
+    assert len(text) >= 16, r.tokens
     enc = O.encoder(W, d, O.logmel_segment(a, d.n_mels))
-    ti, tj, probs, jt = O.find_alignment(W, d, enc, 50259, "transcribe", text, r.seek_frames)
+    ti, tj, probs, jt, ref = O.find_alignment(W, d, enc, 50259, "transcribe", text, r.seek_frames, return_matrix=True)
+    dev = ctx.alignment_matrix(0)
+    assert dev.shape == ref.shape, (dev.shape, ref.shape)
+    e = rel_l2(dev, ref)
+    from test_gpu_align import _jumps, _lib_dtw
+    np.testing.assert_array_equal(r.jump_times, _jumps(*_lib_dtw(dev)).astype(np.float32))
     assert len(r.jump_times) == len(jt) == len(text) + 1
-    # DTW on a 16-bit-noisy cost matrix: the path may move by a frame or two
-    assert np.median(np.abs(r.jump_times - jt)) <= 0.1, (r.jump_times, jt)
-    if len(text):
-        np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)
+    within = float(np.mean(np.abs(r.jump_times - jt) <= 0.02 + 1e-6))
+    print(f"micro f16 alignment: {len(text)} tokens, matrix rel_l2 {e:.2e}, jump times within 1 frame {within:.3f}")
+    assert e <= REL["f16"], e
+    assert within >= 0.95, (r.jump_times, jt)
+    np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)
 
 
 def test_fused_reduce_ln_tail_parity():

@@ -236,20 +236,29 @@ def test_recorder_off_keeps_results():
 # ---------------------------------------------------------------------------------------------------------------
 # full depth: the real large-v3 (32 + 32 layers), one window
 # ---------------------------------------------------------------------------------------------------------------
-def test_full_depth_large_v3_one_window():
+@pytest.fixture(scope="module")
+def large_v3():
+    """The real large-v3 (32 + 32 layers, bf16, PRNG weights) and the oracle's copy of its weights: read back from the
+    device (bit-exact with O.make_weights: test_weights_bit_exact; the numpy PRNG over 1.55 B parameters would take a
+    minute), as bench.py's cpu_baseline does."""
+    from wmx import engine as E
+    d = O.DIMS["large-v3"]
+    m = E.Model("large-v3", 0, "bfloat16").init_synthetic(1)
+    W = {name: m.get_tensor(name, shape) for name, shape, _, _ in O.tensor_specs(d)}
+    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
+    ref_small = O.make_weights(O.Dims(128, 51866, 1280, 20, 1, 1280, 20, 1), 1, "bf16")
+    np.testing.assert_array_equal(W["encoder.layers.0.fc1.weight"], ref_small["encoder.layers.0.fc1.weight"])
+    return m, W
+
+
+def test_full_depth_large_v3_one_window(large_v3):
     """Encoder rel-L2 over all 32 layers and 8 forced decode steps through all 32 decoder layers (bf16), plus the
     first free-running greedy steps replayed exactly."""
     from wmx import engine as E
     d = O.DIMS["large-v3"]
     sp = O.special_tokens(d.n_vocab)
     dt = "bf16"
-    m = E.Model("large-v3", 0, DT[dt]).init_synthetic(1)
-    # the oracle reads the device's weights back (bit-exact with O.make_weights: test_weights_bit_exact; the numpy
-    # PRNG over 1.55 B parameters would take a minute), as bench.py's cpu_baseline does
-    W = {name: m.get_tensor(name, shape) for name, shape, _, _ in O.tensor_specs(d)}
-    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
-    ref_small = O.make_weights(O.Dims(128, 51866, 1280, 20, 1, 1280, 20, 1), 1, dt)
-    np.testing.assert_array_equal(W["encoder.layers.0.fc1.weight"], ref_small["encoder.layers.0.fc1.weight"])
+    m, W = large_v3
     audio = synth.speech_like(501, 480000)
     mel = O.logmel_segment(audio, d.n_mels)
     enc = O.encoder(W, d, mel)
@@ -268,6 +277,104 @@ def test_full_depth_large_v3_one_window():
     res = ctx.transcribe([audio])
     opt = O.DecodeOptions(language=sp.lang0, beam_size=1, max_new_tokens=8)
     _replay_and_compare("large-v3 full depth greedy", ctx, res, 1, opt, sp, 1)
+
+
+def test_full_depth_large_v3_beam5_two_windows(large_v3):
+    """Beam 5 (the reference default, asr_components.py:282; BASELINE config 3) through all 32 + 32 layers: 2 windows x
+    5 rows, 16 teacher-forced steps with the beams re-parented every step (every row's logits vs the oracle), then a
+    free-running 16-step beam-5 transcribe replayed token-exact by oracle.search_replay / rank_final."""
+    from wmx import engine as E
+    d = O.DIMS["large-v3"]
+    sp = O.special_tokens(d.n_vocab)
+    m, W = large_v3
+    audios = [synth.speech_like(511, 480000), synth.speech_like(512, 260000)]
+    mels = np.stack([O.logmel_segment(a, d.n_mels) for a in audios])
+    encs = [O.encoder(W, d, mel) for mel in mels]
+    ctx = E.Context(m, max_batch=2, beam_size=5, max_new_tokens=16, word_timestamps=False, language=sp.lang0)
+    ctx.encode(mels, want_output=False)
+    n = 16
+    tok, par = _forced_stream(np.random.default_rng(14), n, 10, 5)
+    prefix = [[sp.sot, sp.lang0, sp.transcribe]] * 2
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, d, encs, prefix, tok, par, 5)
+    _check_forced("large-v3 full depth beam5", "bf16", top1, lg, 1, ref_top1, ref_margin, ref_lg, 0)
+    ctx.record(16)
+    res = ctx.transcribe(audios)
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=5, max_new_tokens=16)
+    _replay_and_compare("large-v3 full depth beam5", ctx, res, 5, opt, sp, 8)
+
+
+def _boost_eot(m, d, factor):
+    """Scale the EOT embedding row (tied to the output projection) so that EOT competes in the top-k and beams finish:
+    finished-hypothesis handling, patience and the length-penalised ranking only act once hypotheses end."""
+    sp = O.special_tokens(d.n_vocab)
+    emb = m.get_tensor("decoder.embed_tokens.weight", (d.n_vocab, d.n_text_state))
+    emb[sp.eot] *= factor
+    m.set_tensor("decoder.embed_tokens.weight", emb)
+    m.mark_loaded()
+
+
+@pytest.mark.parametrize("patience,length_penalty", [(2.0, 0.5), (1.5, None), (1.0, 1.2)])
+def test_beam_options_replay_micro(patience, length_penalty):
+    """Non-default faster-whisper beam options (TranscriptionOptions.patience / length_penalty, carried in wmx_opts)
+    on the device, with EOT made likely so that hypotheses finish: every step's selection and the final ranking
+    replayed by oracle.search_replay / rank_final with the same options."""
+    from wmx import engine as E
+    d = O.DIMS["micro"]
+    sp = O.special_tokens(d.n_vocab)
+    m = E.Model("micro", 0, "bfloat16").init_synthetic(1)
+    _boost_eot(m, d, 6.0)
+    K = 5
+    ctx = E.Context(m, max_batch=3, beam_size=K, patience=patience,
+                    length_penalty=1.0 if length_penalty is None else length_penalty, max_new_tokens=64,
+                    word_timestamps=False, language=sp.lang0)
+    ctx.record(64)
+    res = ctx.transcribe([synth.speech_like(1201 + i, n) for i, n in enumerate((480000, 200000, 90000))])
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=K, patience=patience, length_penalty=length_penalty,
+                          max_new_tokens=64)
+    lg, sel = ctx.recorded()
+    info = O.search_replay(lg, sel, K, sp, opt, eps=EPS_TIE)
+    fin = [len(i["finished"]) for i in info]
+    for b, (r, inf) in enumerate(zip(res, info)):
+        assert inf["mismatch"] is None, (b, inf["mismatch"])
+        if inf["ties"]:
+            continue
+        toks, sc, margin = O.rank_final(inf["finished"], inf["alive"], K, length_penalty)
+        if margin > EPS_TIE:
+            assert r.tokens == toks, (b, r.tokens, toks)
+            assert abs(r.sum_logprob - sc) <= 1e-3 * max(1.0, abs(sc)), (b, r.sum_logprob, sc)
+    print(f"patience {patience} length_penalty {length_penalty}: replayed {[i['steps'] for i in info]} steps, "
+          f"finished hypotheses per window {fin}, token counts {[len(r.tokens) for r in res]}")
+    assert sum(fin) > 0  # the options were exercised: hypotheses did finish
+    assert max(fin) <= int(round(K * patience))
+
+
+def test_beam_options_replay_wide():
+    """The same at large-v3 width (d 1280, vocab 51866, 4 windows x beam 5 = the bench group's 20 rows), patience 2,
+    length penalty 0.5."""
+    from wmx import engine as E
+    sp = O.special_tokens(WIDE2.n_vocab)
+    m = E.Model(_edims(WIDE2), 0, "bfloat16").init_synthetic(5)
+    _boost_eot(m, WIDE2, 4.0)
+    K, n_new = 5, 48
+    ctx = E.Context(m, max_batch=4, beam_size=K, patience=2.0, length_penalty=0.5, max_new_tokens=n_new,
+                    word_timestamps=False, language=sp.lang0)
+    ctx.record(n_new)
+    audios = [synth.speech_like(100 + i, n) for i, n in enumerate([480000, 150000, 320000, 16000])]
+    res = ctx.transcribe(audios)
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=K, patience=2.0, length_penalty=0.5, max_new_tokens=n_new)
+    lg, sel = ctx.recorded()
+    info = O.search_replay(lg, sel, K, sp, opt, eps=EPS_TIE)
+    fin = [len(i["finished"]) for i in info]
+    for b, (r, inf) in enumerate(zip(res, info)):
+        assert inf["mismatch"] is None, (b, inf["mismatch"])
+        if inf["ties"]:
+            continue
+        toks, sc, margin = O.rank_final(inf["finished"], inf["alive"], K, 0.5)
+        if margin > EPS_TIE:
+            assert r.tokens == toks, (b, r.tokens, toks)
+    print(f"wide patience 2 lp 0.5: replayed {[i['steps'] for i in info]}, finished per window {fin}")
+    assert sum(fin) > 0
 
 
 def test_control_tokens_suppressed_with_boosted_logits():

@@ -32,6 +32,9 @@ class FakeCtx:
                          "n": len(audios)})
         return [self.windows(s, i) for i in range(len(audios))]
 
+    def set_sample_seed(self, seed):
+        self.log.append({"seed": (self.key, seed)})
+
 
 def make_model(windows, max_batch=1):
     m = TR.WhisperModel.__new__(TR.WhisperModel)
@@ -44,6 +47,7 @@ def make_model(windows, max_batch=1):
     m.use_graph = False
     m._ctx = {}
     m.log = []
+    m.sample_seed, m._sample_calls = 1, 0
 
     def context(beam_size, language_token, task, word_timestamps, **kw):
         m.log.append({"context": (beam_size, language_token, task, word_timestamps, kw)})
@@ -193,6 +197,84 @@ def test_stream_batcher_passes_the_adaptive_temperature():
     view.transcribe_kargs.update({"beam_size": 7, "temperature": 0.1})
     OL.StreamBatcher(bm, view).step(_streams(2))
     assert bm.calls[0]["temperature"] == 0.1 and bm.calls[0]["beam"] == 7
+
+
+class StubAdaptive:
+    """speech_rate_audio_processor.AdaptiveWhisperParams stand-in: the kwargs change between steps."""
+
+    def __init__(self, seq):
+        self.seq, self.i = list(seq), 0
+
+    def get_transcribe_kwargs(self):
+        kw = self.seq[min(self.i, len(self.seq) - 1)]
+        self.i += 1
+        return dict(kw)
+
+
+def test_stream_batcher_merges_adaptive_params():
+    """asr_components.py:270-275: adaptive_params.get_transcribe_kwargs() overrides transcribe_kargs on every call,
+    on the batched path as on MI355XWhisperASR.transcribe."""
+    bm = BatchModel()
+    view = ASRView()
+    view.adaptive_params = StubAdaptive([{"beam_size": 7, "temperature": 0.1}, {"beam_size": 3, "temperature": 0.0}])
+    OL.StreamBatcher(bm, view).step(_streams(2))
+    OL.StreamBatcher(bm, view).step(_streams(2))
+    assert [(c["beam"], c["temperature"]) for c in bm.calls] == [(7, 0.1), (3, 0.0)]
+
+
+@pytest.mark.parametrize("extra", [{"vad_filter": True}, {"patience": 2.0}, {"initial_prompt": "x"}])
+def test_stream_batcher_rejects_unsupported_options(extra):
+    bm = BatchModel()
+    view = ASRView()
+    view.transcribe_kargs.update(extra)
+    with pytest.raises(NotImplementedError):
+        OL.StreamBatcher(bm, view).step(_streams(1))
+    view = ASRView()
+    view.adaptive_params = StubAdaptive([extra])
+    with pytest.raises(NotImplementedError):
+        OL.StreamBatcher(bm, view).step(_streams(1))
+
+
+def test_empty_prompt_same_on_both_batch_paths():
+    """An empty-string prompt encodes " " on the multi-window path as on the one-window path (faster-whisper:
+    initial_prompt is not None -> encode(" " + prompt.strip())); None encodes nothing."""
+    class SpaceTok(SyntheticTokenizer):
+        def encode(self, text):
+            return [777] if text == " " else super().encode(text)
+
+    for p, want in (("", [777]), (None, [])):
+        m = make_model(window, max_batch=2)
+        m.tokenizer = SpaceTok(V)
+        m._sample_calls, m.sample_seed = 0, 1
+        m.transcribe_batch([np.zeros(16000 * 40, np.float32), np.zeros(16000 * 5, np.float32)], [p, p])
+        prompts = [e["prompt"] for e in m.log if "prompt" in e]
+        # calls: the 40 s stream's first window (seek loop), its second window, then the 5 s stream (one batch)
+        assert prompts[0] == want and prompts[-1] == want, (p, prompts)
+
+
+def test_sampling_seed_differs_per_call_and_temperature():
+    """Each T > 0 decode call draws with its own seed (fallback retries must not reuse one draw), and the
+    same model seed replays the same sequence of seeds."""
+    seeds = []
+
+    class SeedCtx(FakeCtx):
+        def set_sample_seed(self, s):
+            seeds.append((self.key, s))
+
+    def run():
+        m = make_model(lambda s, i: window(s, i, avg_lp=-2.0))  # every attempt fails the log-prob check
+        m.sample_seed, m._sample_calls = 7, 0
+        m.context = lambda beam_size, language_token, task, word_timestamps, **kw: SeedCtx(
+            m.log, (kw.get("temperature"),), lambda s, i: window(s, i, avg_lp=-2.0))
+        list(m.transcribe(np.zeros(16000 * 40, np.float32), temperature=[0.0, 0.2, 0.4, 0.6])[0])
+        return list(seeds)
+
+    a = run()
+    seeds.clear()
+    b = run()
+    assert a == b and len(a) >= 6  # 2 windows x 3 sampled temperatures
+    assert len({s for _, s in a}) == len(a)
+    assert TR.call_seed(7, 0, 1) != TR.call_seed(7, 0, 2) != TR.call_seed(7, 1, 1)
 
 
 def test_stream_batcher_isolates_a_failing_stream():
