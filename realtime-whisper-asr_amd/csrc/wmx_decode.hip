@@ -420,10 +420,13 @@ __global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ 
   if (lane < KP) {
     const int bi = oi[lane];
     const float bv = ov[lane];
-    out_tok[r * KP + lane] = bi == 0x7FFFFFFF ? o.eot : bi;
+    // no candidate (every key -inf or NaN: the list keeps its (-inf, INT_MAX) init) -> EOT; any id outside the
+    // vocabulary likewise, so a non-finite row can end a hypothesis but never reach the embedding gather
+    const bool none = bi < 0 || bi >= o.V;
+    out_tok[r * KP + lane] = none ? o.eot : bi;
     if (SAMPLE) {  // bv is the sampling key: the log-probability comes from the raw logit of the drawn token
       const int lrow = row_map ? row_map[r] : r;
-      out_lp[r * KP + lane] = bi == 0x7FFFFFFF ? -INFINITY : logits[(long)lrow * ldl + bi] - lse_all;
+      out_lp[r * KP + lane] = none ? -INFINITY : logits[(long)lrow * ldl + bi] - lse_all;
     } else {
       out_lp[r * KP + lane] = bv == -INFINITY ? -INFINITY : bv - lse_all;
     }

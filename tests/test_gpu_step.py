@@ -322,19 +322,33 @@ def test_beam_options_replay_micro(patience, length_penalty):
     from wmx import engine as E
     d = O.DIMS["micro"]
     sp = O.special_tokens(d.n_vocab)
-    m = E.Model("micro", 0, "bfloat16").init_synthetic(1)
-    _boost_eot(m, d, 6.0)
     K = 5
-    ctx = E.Context(m, max_batch=3, beam_size=K, patience=patience,
-                    length_penalty=1.0 if length_penalty is None else length_penalty, max_new_tokens=64,
-                    word_timestamps=False, language=sp.lang0)
-    ctx.record(64)
-    res = ctx.transcribe([synth.speech_like(1201 + i, n) for i, n in enumerate((480000, 200000, 90000))])
+    audios = [synth.speech_like(1201 + i, n) for i, n in enumerate((480000, 200000, 90000))]
     opt = O.DecodeOptions(language=sp.lang0, beam_size=K, patience=patience, length_penalty=length_penalty,
                           max_new_tokens=64)
-    lg, sel = ctx.recorded()
-    info = O.search_replay(lg, sel, K, sp, opt, eps=EPS_TIE)
-    fin = [len(i["finished"]) for i in info]
+    # EOT made competitive: its embedding row (tied to the output projection) becomes a scaled copy of the row of the
+    # token the un-modified beams repeat (random weights lock onto one token), so EOT enters the top K + 1 candidates
+    # and hypotheses finish; the first scale of a fixed ladder at which some hypothesis finishes is used
+    m = E.Model("micro", 0, "bfloat16").init_synthetic(1)
+    ctx = E.Context(m, max_batch=3, beam_size=K, max_new_tokens=16, word_timestamps=False, language=sp.lang0)
+    toks0 = [t for r in ctx.transcribe(audios) for t in r.tokens if t < sp.eot]
+    top = int(np.bincount(toks0).argmax())
+    emb0 = m.get_tensor("decoder.embed_tokens.weight", (d.n_vocab, d.n_text_state))
+    for factor in (0.9, 0.97, 1.02):
+        emb = emb0.copy()
+        emb[sp.eot] = factor * emb0[top]
+        m.set_tensor("decoder.embed_tokens.weight", emb)
+        m.mark_loaded()
+        ctx = E.Context(m, max_batch=3, beam_size=K, patience=patience,
+                        length_penalty=1.0 if length_penalty is None else length_penalty, max_new_tokens=64,
+                        word_timestamps=False, language=sp.lang0)
+        ctx.record(64)
+        res = ctx.transcribe(audios)
+        lg, sel = ctx.recorded()
+        info = O.search_replay(lg, sel, K, sp, opt, eps=EPS_TIE)
+        fin = [len(i["finished"]) for i in info]
+        if sum(fin) > 0:
+            break
     for b, (r, inf) in enumerate(zip(res, info)):
         assert inf["mismatch"] is None, (b, inf["mismatch"])
         if inf["ties"]:
@@ -343,8 +357,9 @@ def test_beam_options_replay_micro(patience, length_penalty):
         if margin > EPS_TIE:
             assert r.tokens == toks, (b, r.tokens, toks)
             assert abs(r.sum_logprob - sc) <= 1e-3 * max(1.0, abs(sc)), (b, r.sum_logprob, sc)
-    print(f"patience {patience} length_penalty {length_penalty}: replayed {[i['steps'] for i in info]} steps, "
-          f"finished hypotheses per window {fin}, token counts {[len(r.tokens) for r in res]}")
+    print(f"patience {patience} length_penalty {length_penalty} (EOT = {factor} x row {top}): replayed "
+          f"{[i['steps'] for i in info]} steps, finished hypotheses per window {fin}, token counts "
+          f"{[len(r.tokens) for r in res]}")
     assert sum(fin) > 0  # the options were exercised: hypotheses did finish
     assert max(fin) <= int(round(K * patience))
 
