@@ -455,6 +455,18 @@ def main():
                                f"every timed decode step, both groups", "samples": sum(insitu[k][1] for k in fams[dom]),
                        "us": {k: round(1000 * insitu[k][0], 2) for k in fams[dom]},
                        "achieved_gbs": round(by / (span * 1e-3) / 1e9, 1) if span > 0 else None}
+    # decode mode (about 1 run in 4 fell into a mode 3-5 % slower, in which the packed GEMMs and the
+    # reduce + LayerNorm launches run 10-25 % longer while the cross attention runs faster): the in-situ ratio of the
+    # cross attention to the rest of the GEMM / reduce chain, calibrated on the r02 runs (fast 0.365-0.372, slow
+    # 0.324-0.334; profiles/r02p_hwq_ab/, r02q_kernarg_ab/)
+    chain = [k for k in ("dec_qkv", "dec_out", "dec_cross_out", "dec_fc1", "dec_fc2", "reduce_ln_out",
+                         "reduce_ln_cross_out", "reduce_ln_fc2") if evs.get(k, (0, 0))[1]]
+    decode_mode = None
+    if chain and evs.get("cross_attn", (0, 0))[1]:
+        ratio = evs["cross_attn"][0] / sum(evs[k][0] for k in chain)
+        decode_mode = {"mode": "fast" if ratio >= 0.35 else "slow", "cross_to_chain_ratio": round(ratio, 4),
+                       "rule": "cross attention / (packed GEMMs + reduce_ln) in situ >= 0.35 -> fast"}
+        log(f"[rank {rank}] decode mode: {decode_mode}")
     # the other named stages: the log-mel front end (north_star: HBM GB/s of the mel path) and the self attention,
     # replayed alone with HIP events on the context stream
     kern_stats = {}
@@ -522,6 +534,7 @@ def main():
                    "parallelism": f"dp{world} (independent streams)", "decode_steps": steps_done,
                    "use_graph": not args.no_graph, "context_groups": G},
         "stage_ms": [round(s, 2) for s in stages],
+        "decode_mode": decode_mode,
         "roofline": roof,
         "encoder": encoder,
         "logmel": logmel,
