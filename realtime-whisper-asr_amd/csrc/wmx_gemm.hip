@@ -316,18 +316,6 @@ __device__ unsigned long long g256_stamps[kG256Stamps][3];
 #ifndef WMX_G256_DIRECT
 #define WMX_G256_DIRECT 1  // LDS-free epilogue for the bf16-output kinds (0: the LDS-image epilogue for all)
 #endif
-constexpr int kTailQpl = 5, kTailRows = 4;
-typedef unsigned int tail_u32x4 __attribute__((ext_vector_type(4)));
-// 16-byte write-through (sc1, aux 16) store / sc1 load through a buffer resource on a wave-uniform base
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tail_rsrc(const float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ void tail_st4(__amdgpu_buffer_rsrc_t r, long idx, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tail_u32x4, v), r, (int)(idx * 4), 0, 16);
-}
-__device__ __forceinline__ float4 tail_ld4(__amdgpu_buffer_rsrc_t r, long idx) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
-}
 constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
 constexpr int kG256Lds = 4 * kG256Slot;     // 128 KiB
 
@@ -517,193 +505,178 @@ __device__ inline void epi_image64_n128(const Epi& e, const float* img, int ldt,
   }
 }
 
-// stream-K hand-off: a finisher waits for the partial of workgroup `w` (flags[w] == epoch), bounded
-__device__ inline bool g256_wait(const G256Sk& sk, int w) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(sk.flags + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != sk.epoch) {
-    __builtin_amdgcn_s_sleep(2);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz: give up, report, never hang
-      __hip_atomic_store(sk.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-  return true;
-}
-
-// range of stream-K slices of workgroup w: [s, e) of the R * nk slices of the remainder tiles
-__host__ __device__ inline long g256_sk_begin(int w, long total, int G) { return (long)w * total / G; }
-
 template <DT T, int KIND>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int M, int N, int K,
-                                                         Epi e, G256Sk sk) {
+                                                         Epi e) {
   constexpr int BM = 256, BN = 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesN = (N + BN - 1) / BN;
   const int tilesM = (M + BM - 1) / BM;
   const int nwg = tilesN * tilesM;
+  // persistent: a workgroup walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8, so a tile stays on
+  // the XCD the remap below assumes); the previous tile's epilogue stores drain while the next tile's first
+  // slices are in flight, and the workgroup's LDS is not released and re-acquired per tile
+  for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
+#ifdef WMX_G256_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
+  int bid = tile;
+  {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  // grouped order inside that range: 4 row panels walk the columns together, so the ~32 tiles an XCD runs at
+  // once share 4 A panels and ~8 W panels in its L2 (row-major order shared 2 A panels but 16+ W panels)
+  constexpr int GM = 4;
+  const int gsz = GM * tilesN;
+  const int grp = bid / gsz, gr = bid - grp * gsz;
+  const int gm = min(GM, tilesM - grp * GM);
+  const int tm = grp * GM + gr % gm, tn = gr / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int nk = K >> 5;
-  const int fr = lane & 15, fq = lane >> 4;
-  // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias
+  // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias, loaded now so its latency hides behind
+  // the main loop (the epilogue's column quads are the same in all four rounds)
   // (direct epilogue kinds: the lane's column quad after the in-quad transpose, wn 64 + 16 (fr & 3) + 4 (fr >> 2))
   constexpr bool kDirect = WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16);
   const int bcol = kDirect ? (wave & 3) * 64 + 16 * (lane & 3) + 4 * ((lane >> 2) & 3) : 4 * (tid & 63);
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (KIND >= 0 && e.bias && n0 + bcol < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
+
   // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
   // Wave w issues pieces w, w + 8, w + 16, w + 24; lane l covers row l >> 2, 16-B column (l & 3).
   const int srow = lane >> 2;
   const int scol = ((lane & 3) ^ ((-(srow >> 2)) & 3)) * 8;  // source k offset of this lane's swizzled piece
+  const uint16_t* src[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pc = wave + 8 * j;
+    if (pc < 16) {
+      src[j] = A + (long)min(m0 + pc * 16 + srow, M - 1) * lda + scol;
+    } else {
+      src[j] = W + (long)min(n0 + (pc - 16) * 16 + srow, N - 1) * ldw + scol;
+    }
+  }
+  // half h of slice kt: pieces 2h, 2h + 1 of this wave (h = 0: A rows, h = 1: W rows)
+  auto issue_half = [&](int kt, int h) {
+#if WMX_G256_MODE == 2
+    return;
+#endif
+    char* slot = smem + (kt & 3) * kG256Slot;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * h + jj;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + kt * 32),
+                                       (__attribute__((address_space(3))) void*)(slot + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+  auto issue = [&](int kt) {
+    issue_half(kt, 0);
+    issue_half(kt, 1);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+
+  const int fr = lane & 15, fq = lane >> 4;
   const int piece = (fq ^ ((-(fr >> 2)) & 3)) << 4;
   const int aoff = (wm * 128 + fr) * 64 + piece;
   const int boff = BM * 64 + (wn * 64 + fr) * 64 + piece;
+
+  // Ping-pong schedule (cdna_hip_programming.md §5 256² template, T3+T4+T5): every 32-deep slice is two phases;
+  // a phase is [memory segment] s_barrier [16-MFMA segment] s_barrier.  Waves 4..7 (wave row 1) run one barrier
+  // behind waves 0..3, so on every SIMD one wave computes while its partner reads LDS / issues DMA.
+  //   phase A of slice t: ds_read B frags 0..3 + A frags 0..3; issue the A half of slice t + 3 into slot (t-1)&3
+  //                       (every memory segment retires its ds_reads with lgkmcnt(0) BEFORE its barrier, so the
+  //                       lagging half's last reads of slice t-1 are done before the leading half restages it)
+  //   phase B of slice t: wait (counted vmcnt) for slice t + 1; ds_read A frags 4..7; issue the W half of t + 3
+  // The wait in phase B of slice t precedes, by at least one barrier, every wave's first read of slice t + 1.
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  if (nk > 2)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
-
-  f32x4 acc[8][4];
-  float4 bias4;
-  int m0 = 0, n0 = 0;
-
-  // tile index -> (m0, n0): bijective XCD remap (§5.5 T1), then 4 row panels walk the columns together inside each
-  // XCD's range, so the ~32 tiles an XCD runs at once share 4 A panels and ~8 W panels in its L2
-  auto coords = [&](int tile) __attribute__((always_inline)) {
-    int bid = tile;
-    {
-      const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-      bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    }
-    constexpr int GM = 4;
-    const int gsz = GM * tilesN;
-    const int grp = bid / gsz, gr = bid - grp * gsz;
-    const int gm = min(GM, tilesM - grp * GM);
-    const int tm = grp * GM + gr % gm, tn = gr / gm;
-    m0 = tm * BM;
-    n0 = tn * BN;
-    // loaded now so its latency hides behind the main loop (the epilogue's column quads are the same in all rounds)
-    bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (KIND >= 0 && e.bias && n0 + bcol < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
+  if (lagging) __builtin_amdgcn_s_barrier();
+  u16x8 af[4], bfr[4];
+  for (int t = 0; t < nk; ++t) {
+    const char* S = smem + (t & 3) * kG256Slot;
+    // ---- phase A ----
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const u16x8*>(S + boff + j * 1024);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-  };
-
-  // main loop over the 32-deep slices [kb, ke) of the tile at (m0, n0), accumulating into acc
-  auto mainloop = [&](int kb, int ke) __attribute__((always_inline)) {
-    const uint16_t* src[4];
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + i * 1024);
+    if (t + 3 < nk) issue_half(t + 3, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pc = wave + 8 * j;
-      if (pc < 16) {
-        src[j] = A + (long)min(m0 + pc * 16 + srow, M - 1) * lda + scol;
-      } else {
-        src[j] = W + (long)min(n0 + (pc - 16) * 16 + srow, N - 1) * ldw + scol;
-      }
-    }
-    // half h of slice kt: pieces 2h, 2h + 1 of this wave (h = 0: A rows, h = 1: W rows)
-    auto issue_half = [&](int kt, int h) __attribute__((always_inline)) {
-#if WMX_G256_MODE == 2
-      return;
-#endif
-      char* slot = smem + (kt & 3) * kG256Slot;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int j = 2 * h + jj;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + kt * 32),
-                                         (__attribute__((address_space(3))) void*)(slot + (wave + 8 * j) * 1024), 16,
-                                         0, 0);
-      }
-    };
-    auto issue = [&](int kt) __attribute__((always_inline)) {
-      issue_half(kt, 0);
-      issue_half(kt, 1);
-    };
-    // Ping-pong schedule (cdna_hip_programming.md §5 256² template, T3+T4+T5): every 32-deep slice is two phases;
-    // a phase is [memory segment] s_barrier [16-MFMA segment] s_barrier.  Waves 4..7 (wave row 1) run one barrier
-    // behind waves 0..3, so on every SIMD one wave computes while its partner reads LDS / issues DMA.
-    //   phase A of slice t: ds_read B frags 0..3 + A frags 0..3; issue the A half of slice t + 3 into slot (t-1)&3
-    //                       (every memory segment retires its ds_reads with lgkmcnt(0) BEFORE its barrier, so the
-    //                       lagging half's last reads of slice t-1 are done before the leading half restages it)
-    //   phase B of slice t: wait (counted vmcnt) for slice t + 1; ds_read A frags 4..7; issue the W half of t + 3
-    // The wait in phase B of slice t precedes, by at least one barrier, every wave's first read of slice t + 1.
-    const int n = ke - kb;
-    issue(kb);
-    if (n > 1) issue(kb + 1);
-    if (n > 2) issue(kb + 2);
-    if (n > 2)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n > 1)
+      for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase B ----
+    // slice t + 1 is complete once only slice t + 2 (4 DMAs) and the first half of t + 3 (2) may be outstanding
+    if (t + 3 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (t + 2 < nk)
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + (i + 4) * 1024);
+    if (t + 3 < nk) issue_half(t + 3, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    if (lagging) __builtin_amdgcn_s_barrier();
-    u16x8 af[4], bfr[4];
-    for (int t = kb; t < ke; ++t) {
-      const char* S = smem + (t & 3) * kG256Slot;
-      // ---- phase A ----
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const u16x8*>(S + boff + j * 1024);
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + i * 1024);
-      if (t + 3 < ke) issue_half(t + 3, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      // ---- phase B ----
-      // slice t + 1 is complete once only slice t + 2 (4 DMAs) and the first half of t + 3 (2) may be outstanding
-      if (t + 3 < ke)
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if (t + 2 < ke)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + (i + 4) * 1024);
-      if (t + 3 < ke) issue_half(t + 3, 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i + 4][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i + 4][j]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-    }
-    if (!lagging) __builtin_amdgcn_s_barrier();
-    __syncthreads();
-  };
-
-  // epilogue of the tile at (m0, n0) from acc
-  auto epilogue = [&]() __attribute__((always_inline)) {
-#if WMX_G256_MODE == 3  // ablation: main loop only (keeps the accumulators live through an untaken store)
-    {
-      float sacc = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-      if (sacc == 1234.5f) reinterpret_cast<float*>(e.out)[tid] = sacc;
-      return;
-    }
+      for (int j = 0; j < 4; ++j) acc[i + 4][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i + 4][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (!lagging) __builtin_amdgcn_s_barrier();
+  __syncthreads();
+#ifdef WMX_G256_STAMPS
+  const unsigned long long st1 = __builtin_amdgcn_s_memtime();
 #endif
-    if constexpr (kDirect) {
-      // LDS-free epilogue: for every (fragment row i, register r) the 16 lanes of a row group hold columns
-      // 16 j + fr (j = 0..3) of one output row; a 4 x 4 transpose inside each lane quad (lane-dependent register
-      // rotation, three DPP quad rotations, rotation back) leaves lane (fr) with the 4 consecutive columns
-      // wn 64 + 16 (fr & 3) + 4 (fr >> 2) .. +3, stored as one 8-byte bf16 quad.  No image, no barriers.
-      const int q = lane & 3;
-      const int n = n0 + bcol;
+
+#if WMX_G256_MODE == 3  // ablation: main loop only (keeps the accumulators live through an untaken store)
+  {
+    float sacc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sacc == 1234.5f) reinterpret_cast<float*>(e.out)[tid] = sacc;
+    continue;
+  }
+#endif
+  if constexpr (kDirect) {
+    // LDS-free epilogue: for every (fragment row i, register r) the 16 lanes of a row group hold columns
+    // 16 j + fr (j = 0..3) of one output row; a 4 x 4 transpose inside each lane quad (lane-dependent register
+    // rotation, three DPP quad rotations, rotation back) leaves lane (fr) with the 4 consecutive columns
+    // wn 64 + 16 (fr & 3) + 4 (fr >> 2) .. +3, stored as one 8-byte bf16 quad.  No image, no barriers.
+    const int q = lane & 3;
+    const int n = n0 + bcol;
+    {  // every lane takes part in the DPP exchanges; only the stores are guarded
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -743,115 +716,44 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
           }
         }
       }
-      __syncthreads();  // the next tile's DMA must not overwrite the ring before every wave left this tile
-      return;
     }
-    // epilogue: 4 rounds of 64 rows through an fp32 LDS image [64][BN + 4]
-    constexpr int LDT = BN + 4;
-    float* img = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int rd = 0; rd < 4; ++rd) {
-      if (wm == (rd >> 1)) {
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const int i = (rd & 1) * 4 + ii;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) img[(ii * 16 + fq * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
-        }
-      }
-      __syncthreads();
-      epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
-      __syncthreads();
+#ifdef WMX_G256_STAMPS
+    if (tid == 0 && tile < kG256Stamps) {
+      g256_stamps[tile][0] = st0;
+      g256_stamps[tile][1] = st1;
+      g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
     }
-  };
-
-  // ---- work items: the data-parallel tiles (whole K each; gridDim.x a multiple of 8, so a tile stays on the XCD
-  // the remap assumes; the previous tile's epilogue stores drain while the next tile's first slices are in flight),
-  // then this workgroup's parts of the stream-K remainder (G256Sk).  One loop, so the main loop and the epilogue
-  // exist once in the code (two inlined copies of each raised the register count into spills).
-  // Stream-K: a tile's slices are held by a run of consecutive workgroups (contributors c = 0, 1, ... in k order).
-  // Each contributor stores its partial image (write-through), then takes a ticket on the tile's counter; all but the
-  // last publish ready[slot] = epoch; the last one sums the parts from memory in k order -- ((0 + p0) + p1) + ...,
-  // bit-exact whoever arrives last -- and runs the epilogue.  The last arriver only waits for workgroups that already
-  // hold a ticket (resident, with only the flag store left), so no dispatch order or co-residency is assumed.
-  const int R = sk.sk_tiles, T0 = nwg - R;
-  const int G = gridDim.x, w = blockIdx.x;
-  const long total = (long)R * nk;
-  const long s0 = R > 0 ? g256_sk_begin(w, total, G) : 0, e0 = R > 0 ? g256_sk_begin(w + 1, total, G) : 0;
-  const int ndp = T0 > w ? (T0 - w + G - 1) / G : 0;               // data-parallel tiles of this workgroup
-  const int nsk = s0 < e0 ? (int)((e0 - 1) / nk - s0 / nk) + 1 : 0;  // stream-K parts (<= 2)
-  const auto wsr = tail_rsrc(sk.ws);
-  __shared__ int sk_last;
-  for (int it = 0; it < ndp + nsk; ++it) {
-    const bool split = it >= ndp;
-    int tile, kb = 0, ke = nk;
-    long tb0 = 0;
-    if (!split) {
-      tile = w + it * G;
-    } else {
-      const int t = (int)(s0 / nk) + (it - ndp);
-      tb0 = (long)t * nk;
-      kb = (int)(max(s0, tb0) - tb0);
-      ke = (int)(min(e0, tb0 + nk) - tb0);
-      tile = T0 + t;
-    }
-    coords(tile);
-    mainloop(kb, ke);
-    if (kb > 0 || ke < nk) {  // a part of a split tile
-      const int t = tile - T0;
-      auto first_wg = [&](long slice) __attribute__((always_inline)) {  // the workgroup whose range holds `slice`
-        int lo = (int)(slice * G / total);
-        while (lo + 1 < G && g256_sk_begin(lo + 1, total, G) <= slice) ++lo;
-        while (lo > 0 && g256_sk_begin(lo, total, G) > slice) --lo;
-        return lo;
-      };
-      // partial slot of workgroup w2's part of tile t: 2 w2 + (0 if t is the first tile w2's range touches, else 1)
-      auto slot_of = [&](int w2) __attribute__((always_inline)) {
-        return 2 * w2 + (int)(g256_sk_begin(w2, total, G) / nk != t);
-      };
-      const int c0 = first_wg(tb0), n = first_wg(tb0 + nk - 1) - c0 + 1, own = slot_of(w);
+#endif
+    __syncthreads();  // the next tile's DMA must not overwrite the ring before every wave left this tile
+    continue;
+  }
+  // epilogue: 4 rounds of 64 rows through an fp32 LDS image [64][BN + 4]
+  constexpr int LDT = BN + 4;
+  float* img = reinterpret_cast<float*>(smem);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+  for (int rd = 0; rd < 4; ++rd) {
+    if (wm == (rd >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = (rd & 1) * 4 + ii;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          tail_st4(wsr, (((long)own * 32 + i * 4 + j) * 512 + tid) * 4, __builtin_bit_cast(float4, acc[i][j]));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drained its write-through stores
-      __syncthreads();
-      if (tid == 0) {
-        sk_last = __hip_atomic_fetch_add(sk.flags + G * 2 + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
-        if (!sk_last) __hip_atomic_store(sk.flags + own, sk.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else __hip_atomic_store(sk.flags + G * 2 + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-      }
-      __syncthreads();
-      if (!sk_last) continue;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-      for (int c = 0; c < n; ++c) {
-        const int slot = slot_of(c0 + c);
-        if (slot != own) {
-          __syncthreads();  // every thread has read the previous sk_last
-          if (tid == 0) sk_last = g256_wait(sk, slot);
-          __syncthreads();
-          if (!sk_last) continue;
-        }
-        // one accumulator row (4 x 16 B) in flight at a time
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float4 p[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) p[j] = tail_ld4(wsr, (((long)slot * 32 + i * 4 + j) * 512 + tid) * 4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] += __builtin_bit_cast(f32x4, p[j]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+          for (int r = 0; r < 4; ++r) img[(ii * 16 + fq * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
       }
     }
-    epilogue();
+    __syncthreads();
+    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
+    __syncthreads();
   }
+#ifdef WMX_G256_STAMPS  // diagnostic build only (tools/mb_gemm256 -DWMX_G256_STAMPS): per-tile phase clocks
+  if (tid == 0 && tile < kG256Stamps) {
+    g256_stamps[tile][0] = st0;
+    g256_stamps[tile][1] = st1;
+    g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
+  }
+#endif
+  }  // tile loop
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1229,6 +1131,18 @@ static void launch_skinny(const GemmCall& g, hipStream_t st) {
 //      group (4 rows x 5 column quads per lane in flight, wave-only reductions), and re-arms it.
 // Requires N % 4 == 0 and N <= 1280 (packed_tail_ok).
 // ------------------------------------------------------------------------------------------------
+constexpr int kTailQpl = 5, kTailRows = 4;
+typedef unsigned int tail_u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte write-through (sc1, aux 16) store / sc1 load through a buffer resource on a wave-uniform base
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tail_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void tail_st4(__amdgpu_buffer_rsrc_t r, long idx, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tail_u32x4, v), r, (int)(idx * 4), 0, 16);
+}
+__device__ __forceinline__ float4 tail_ld4(__amdgpu_buffer_rsrc_t r, long idx) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
+}
 template <DT T, int MT, int NCT, int NW>
 __device__ __forceinline__ void packed_red_tail(const RedTail& rt, const float* part, int M, int N, int S, int m0,
                                                 int t0) {
@@ -1766,45 +1680,15 @@ static int g256_grid(int tiles) {
   return one_tile ? tiles : std::min(tiles, cus);
 }
 
-int g256_grid_for(int tiles) { return g256_grid(tiles); }
-
-// stream-K remainder tiles of a launch: T mod G when the split leaves every workgroup at least kG256SkMin slices
-// (shorter ranges spend more on the pipeline fill and the partial hand-off than the idle CUs cost); WMX_G256_SK=0
-// turns it off (A/B runs)
-constexpr int kG256SkMin = 12;
-int g256_sk_tiles(int tiles, int grid, int nk) {
-  static const bool off = [] {
-    const char* v = getenv("WMX_G256_SK");
-    return v && v[0] == '0';
-  }();
-  if (off || grid <= 0) return 0;
-  const int R = tiles % grid;
-  if (R == 0 || (long)R * nk < (long)kG256SkMin * grid) return 0;
-  return R;
-}
-
 template <DT T>
 static void launch_g256(const GemmCall& g, hipStream_t st) {
   const int ntile = ((g.M + 255) / 256) * ((g.N + 255) / 256);
-  int tiles = g256_grid(ntile);
+  const int tiles = g256_grid(ntile);
   const bool vec = (g.N & 3) == 0 && (g.epi.ldc & 3) == 0;
   const int kind = (vec || g.epi.kind == EPI_CROSSKV) ? g.epi.kind : -1;
-  G256Sk sk;
-  if (g.sk_ws && g.sk_flags && g.sk_err && g.sk_epoch) {
-    // the full persistent grid (one workgroup per CU) whenever the remainder is split, also for fewer tiles than CUs
-    const int full = g256_grid(1 << 30);
-    sk.sk_tiles = g256_sk_tiles(ntile, full, g.K / 32);
-    if (sk.sk_tiles > 0) {
-      tiles = full;
-      sk.ws = g.sk_ws;
-      sk.flags = g.sk_flags;
-      sk.err = g.sk_err;
-      sk.epoch = ++*g.sk_epoch;
-    }
-  }
 #define WMX_G256_LAUNCH(KD)                                                                                    \
   hipLaunchKernelGGL((gemm256_kernel<T, KD>), dim3(tiles), dim3(512), kG256Lds, st, g.A, g.lda, g.W, g.ldw, g.M, \
-                     g.N, g.K, g.epi, sk)
+                     g.N, g.K, g.epi)
   switch (kind) {
     case EPI_STORE16: WMX_G256_LAUNCH(EPI_STORE16); break;
     case EPI_GELU16: WMX_G256_LAUNCH(EPI_GELU16); break;

@@ -67,19 +67,6 @@ __host__ __device__ inline long crossv_off(int t, int c) {
 
 enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3, TILE_256 = 4 };
 
-// Stream-K remainder of the persistent 256² GEMM (TILE_256): with T tiles on a grid of G workgroups, the first
-// T - R tiles run data-parallel (whole K each) and the last R = T mod G tiles are split over K evenly across all G
-// workgroups, so the last round has no idle CUs.  The contributors of a split tile take tickets on its counter; all
-// but the last store their partial accumulator images (512 threads x 32 x 16 B, write-through) and publish a ready
-// flag; the last adds them in a fixed association order and runs the epilogue (gemm256_kernel).
-struct G256Sk {
-  float* ws = nullptr;   // >= 2 * grid * 512 * 128 floats: slot 2 w + p = part p of workgroup w's range
-  int* flags = nullptr;  // >= 3 * grid: [0, 2 grid) ready flags of the slots, [2 grid, 3 grid) tile ticket counters
-  int* err = nullptr;    // set to 1 when a wait gave up (the host reports it)
-  int epoch = 0;         // unique per launch on this workspace (flags compare equal to it)
-  int sk_tiles = 0;      // R (0 = data-parallel only)
-};
-
 struct GemmCall {
   const uint16_t* A;
   long lda;
@@ -91,16 +78,7 @@ struct GemmCall {
   int splits = 1;
   float* ws = nullptr;  // split-K workspace
   long ws_elems = 0;
-  // TILE_256 stream-K remainder (sk_ws null: data-parallel only)
-  float* sk_ws = nullptr;
-  int* sk_flags = nullptr;
-  int* sk_err = nullptr;
-  int* sk_epoch = nullptr;  // host counter, incremented per launch that splits
 };
-
-// grid of the persistent 256² GEMM and its stream-K remainder for an M x N x K launch (host helpers; tests)
-int g256_grid_for(int tiles);
-int g256_sk_tiles(int tiles, int grid, int nk);
 
 void launch_gemm(DT dt, const GemmCall& g, hipStream_t st);
 

@@ -543,22 +543,7 @@ struct Ctx {
   std::vector<float> last_align;
   std::vector<int> last_ntext, last_nframes;
   int last_align_Tn = 0;
-  // stream-K remainder of the 256² GEMM (G256Sk): per-workgroup partial images, publish flags, give-up flag, epoch
-  float* sk_ws = nullptr;
-  int *sk_flags = nullptr, *sk_err = nullptr;
-  int sk_epoch = 0;
 };
-
-// a stream-K GEMM wait that gave up (G256Sk.err, never expected: every wait is on a lower-numbered workgroup's
-// first part) leaves wrong outputs: report it instead of returning them
-static void check_sk(Ctx& c) {
-  int v = 0;
-  WMX_HIP(hipMemcpy(&v, c.sk_err, 4, hipMemcpyDeviceToHost));
-  if (v) {
-    WMX_HIP(hipMemset(c.sk_err, 0, 4));
-    throw Error(WMX_ERR_HIP, "gemm256 stream-K: a partial-sum wait timed out (outputs of this call are invalid)");
-  }
-}
 
 static void sync_at(Ctx& c, int line) {
   const hipError_t e = hipStreamSynchronize(c.st);
@@ -629,13 +614,6 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.pad_win, B);
   P.add(&c.slot, 4);
   P.add(&c.n_done, 4);
-  {  // stream-K partial images: two 256 KiB accumulator images per workgroup of the persistent 256² grid (one per
-     // part of its range), their ready flags, and one ticket counter per remainder tile (G256Sk)
-    const int G = g256_grid_for(1 << 30);
-    P.add(&c.sk_ws, (size_t)2 * G * 512 * 128);
-    P.add(&c.sk_flags, 3 * G);
-    P.add(&c.sk_err, 1);
-  }
   P.add(&c.lang_slot, B);
   P.add(&c.lang_tok, B);
   P.add(&c.row_map, R);
@@ -719,13 +697,8 @@ static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ld
   static const bool no_g256 = getenv("WMX_NO_G256") != nullptr;  // A/B switch for tuning runs
   if (!no_g256 && M >= 4096 && K % 32 == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
       (e.kind != EPI_CROSSKV || e.d % 256 == 0) && e.kind != EPI_QKV_CACHE) {
-    // encoder / conv front end / cross-K/V: 256x256 ping-pong tile, every tile on its own CU; the last partial round
-    // of tiles split over K (stream-K) so that no CU idles
+    // encoder / conv front end / cross-K/V: 256x256 ping-pong tile, every tile on its own CU
     g.tile = TILE_256;
-    g.sk_ws = c.sk_ws;
-    g.sk_flags = c.sk_flags;
-    g.sk_err = c.sk_err;
-    g.sk_epoch = &c.sk_epoch;
     launch_gemm(c.dt, g, c.st);
     return;
   }
@@ -1910,7 +1883,6 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   }
   rec(c, 7);
   WMX_HIP(hipEventSynchronize(c.ev[7]));
-  check_sk(c);
   for (int i = 0; i < 7; ++i) WMX_HIP(hipEventElapsedTime(&c.stage_ms[i], c.ev[i], c.ev[i + 1]));
 
   for (int b = 0; b < B; ++b) {
@@ -2299,7 +2271,6 @@ wmx_status wmx_encode(wmx_ctx* x, const float* mel, int B, float* enc_out) {
       WMX_HIP(hipMemcpyAsync(enc_out, c.ex, n * 4, hipMemcpyDeviceToHost, c.st));
     }
     sync(c);
-    check_sk(c);
   });
 }
 
