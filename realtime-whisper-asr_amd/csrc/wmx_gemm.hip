@@ -1630,6 +1630,199 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
   WMX_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------------------------------------------------------
+// Decode MLP in one launch: fc1 (+bias, GELU) -> fc2 split-K partials, the fc1 -> fc2 edge handed off inside the
+// launch (the persistent-layer engine's premise, MI355X_MICROARCH.md "engine-vs-launches" / "prefetch-credit",
+// tried on this one edge).  Workgroup b (1024 threads, one per CU):
+//   phase A  fc1 column tiles 2b, 2b+1 over the whole K = d (16 waves x up to 3 k-steps);
+//   phase B  fc2 column group cg = b % (d/64) (4 tiles) over K slice sp = b / (d/64) (d/2 wide, 8 slices).
+// The K slice sp of fc2 is exactly the fc1 output of workgroups [sp d/64, (sp+1) d/64), so each slice is one
+// group of d/64 producers and d/64 consumers.  Every workgroup issues its phase-B weight loads together with its
+// phase-A loads (the weights do not depend on the hand-off), stores GELU(fc1) write-through (sc1), drains, and
+// adds 1 to its slice's monotonic counter behind a workgroup barrier; one lane polls the counter with sc1 loads
+// until the slice's generation is complete, and every wave then reads the slice with sc1 loads (the hand-off of
+// MI355X_MICROARCH.md's sc1 table, first row).  Partials part[8][M][d] feed reduce_ln as in the split form.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMlpNW = 16, kMlpS = 8, kMlpKA = 3, kMlpKB = 2;
+typedef unsigned int mlp_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+
+template <DT T>
+__global__ __launch_bounds__(64 * kMlpNW) void mlp_fused_kernel(MlpCall c) {
+  constexpr int MT = 2, NA = 2, NB = 4, NW = kMlpNW;
+  constexpr int LDA_ = 16 * NA + 1, LDB_ = 16 * NB + 1;
+  constexpr int RED = (NW * MT * 16 * LDA_ > (NW / 2) * MT * 16 * LDB_) ? NW * MT * 16 * LDA_ : (NW / 2) * MT * 16 * LDB_;
+  __shared__ float red[RED];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const unsigned long long probe_t0 = (c.tprobe && tid == 0) ? probe_clock() : 0ull;
+  const int d = c.d, M = c.M;
+  const int ksA = d >> 5, ntA = (4 * d) >> 4;          // fc1: K = d, N = 4d
+  const int ksB = (4 * d) >> 5, ntB = d >> 4;          // fc2: K = 4d, N = d
+  const int cgn = d / (16 * NB), kpsB = ksB / kMlpS;   // fc2 column groups (= producers per slice), k-steps per slice
+  const int b = blockIdx.x, sp = b / cgn, cg = b - sp * cgn;
+  // ---- every load that does not depend on the hand-off: fc1 weights + rows, fc2 weights, fc1 bias ----
+  u16x8 wa[kMlpKA][NA], aa[kMlpKA][MT], wb[kMlpKB][NB];
+#pragma unroll
+  for (int j = 0; j < kMlpKA; ++j) {
+    const int k = min(wave + NW * j, ksA - 1);  // clamped; MFMAs of k-steps past the end are skipped
+#pragma unroll
+    for (int t = 0; t < NA; ++t)
+      wa[j][t] = stream_load(reinterpret_cast<const u16x8*>(c.W1 + packed_w_elem(NA * b + t, ntA, ksA, k, lane)));
+#pragma unroll
+    for (int i = 0; i < MT; ++i) aa[j][i] = *reinterpret_cast<const u16x8*>(c.A + packed_a_elem(i * 16 + fr, M, c.lda, k, lane));
+  }
+#pragma unroll
+  for (int j = 0; j < kMlpKB; ++j) {
+    const int k = sp * kpsB + min(wave + NW * j, kpsB - 1);
+#pragma unroll
+    for (int t = 0; t < NB; ++t)
+      wb[j][t] = stream_load(reinterpret_cast<const u16x8*>(c.W2 + packed_w_elem(NB * cg + t, ntB, ksB, k, lane)));
+  }
+  const int qa = tid & (4 * NA - 1);  // phase-A epilogue: the thread's column quad
+  const float4 pbias = *reinterpret_cast<const float4*>(c.b1 + 32 * b + 4 * qa);
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- phase A: fc1 ----
+  {
+    f32x4 acc[MT][NA];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int t = 0; t < NA; ++t) acc[i][t] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kMlpKA; ++j)
+      if (wave + NW * j < ksA)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int t = 0; t < NA; ++t) acc[i][t] = mfma16<T>(aa[j][i], wa[j][t], acc[i][t]);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int t = 0; t < NA; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(wave * MT * 16 + i * 16 + fq * 4 + r) * LDA_ + t * 16 + fr] = acc[i][t][r];
+  }
+  __syncthreads();
+  const auto hr = mlp_rsrc(c.h);
+  if (tid < MT * 16 * 4 * NA) {
+    const int row = tid / (4 * NA), col = 4 * qa;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float s = red[row * LDA_ + col + q];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) s += red[(w * MT * 16 + row) * LDA_ + col + q];
+      v[q] = s;
+    }
+    if (row < M) {
+      const u16x4 h = {from_f32<T>(gelu_erf(v[0] + pbias.x)), from_f32<T>(gelu_erf(v[1] + pbias.y)),
+                       from_f32<T>(gelu_erf(v[2] + pbias.z)), from_f32<T>(gelu_erf(v[3] + pbias.w))};
+      const int off = (row * 4 * d + 32 * b + col) * 2;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mlp_u32x2, h), hr, off, 0, 16);  // sc1
+    }
+  }
+  // ---- hand-off: drain, barrier, one arrival per workgroup; one lane polls the slice's generation ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(c.cnt) + sp, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (old / cgn + 1) * cgn;
+    int spins = 0;
+    while ((int)(__hip_atomic_load(reinterpret_cast<unsigned*>(c.cnt) + sp, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      if (++spins > (1 << 22)) {  // a producer never arrived: flag it and finish (wrong output, no hang)
+        __hip_atomic_store(c.cnt + kMlpS, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  // ---- phase B: fc2 over the slice, h read write-through (sc1) ----
+  u16x8 ha[kMlpKB][MT];
+#pragma unroll
+  for (int j = 0; j < kMlpKB; ++j) {
+    const int k = sp * kpsB + min(wave + NW * j, kpsB - 1);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int off = (int)packed_a_elem(i * 16 + fr, M, 4L * d, k, lane) * 2;
+      ha[j][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(hr, off, 0, 16));
+    }
+  }
+  // k-steps past the slice's end: zero weight operand, MFMA unconditional (a guarded MFMA let the compiler sink
+  // the sc1 loads into the guard, one round trip per k-step)
+#pragma unroll
+  for (int j = 0; j < kMlpKB; ++j) {
+    const bool ok = wave + NW * j < kpsB;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) wb[j][t] = ok ? wb[j][t] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  f32x4 acc[MT][NB];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int t = 0; t < NB; ++t) acc[i][t] = f32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < kMlpKB; ++j)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int t = 0; t < NB; ++t) acc[i][t] = mfma16<T>(ha[j][i], wb[j][t], acc[i][t]);
+  // two-step cross-wave sum: waves 8..15 store, waves 0..7 add theirs, then 8 slots per output
+  constexpr int NH = NW / 2;
+  if (wave >= NH) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int t = 0; t < NB; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[((wave - NH) * MT * 16 + i * 16 + fq * 4 + r) * LDB_ + t * 16 + fr] = acc[i][t][r];
+  }
+  __syncthreads();
+  if (wave < NH) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int t = 0; t < NB; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(wave * MT * 16 + i * 16 + fq * 4 + r) * LDB_ + t * 16 + fr] += acc[i][t][r];
+  }
+  __syncthreads();
+  if (tid < MT * 16 * 4 * NB) {
+    const int row = tid / (4 * NB), col = 4 * (tid & (4 * NB - 1));
+    if (row < M) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float s = red[row * LDB_ + col + q];
+#pragma unroll
+        for (int w = 1; w < NH; ++w) s += red[(w * MT * 16 + row) * LDB_ + col + q];
+        v[q] = s;
+      }
+      *reinterpret_cast<float4*>(c.part + ((long)sp * M + row) * d + NB * 16 * cg + col) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  if (c.tprobe && tid == 0) probe_record(c.tprobe, *c.pslot, probe_t0);
+}
+
+bool mlp_fused_ok(int M, int d) { return M >= 1 && M <= 32 && d % 64 == 0 && d >= 256 && d <= 1536; }
+
+void launch_mlp_fused(DT dt, const MlpCall& c, hipStream_t st) {
+  WMX_CHECK(mlp_fused_ok(c.M, c.d) && c.A && c.W1 && c.b1 && c.W2 && c.h && c.part && c.cnt && c.lda >= c.d,
+            "fused mlp: shape / arguments");
+  const dim3 grid(c.d / 8);  // fc1 column groups of 32 = (d / 64 fc2 column groups) x 8 K slices
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(mlp_fused_kernel<DT::BF16>, grid, dim3(64 * kMlpNW), 0, st, c);
+  else
+    hipLaunchKernelGGL(mlp_fused_kernel<DT::F16>, grid, dim3(64 * kMlpNW), 0, st, c);
+  WMX_HIP(hipGetLastError());
+}
+
 template <DT T, int BM, int BN, int WM, int WN>
 static void launch_cfg(const GemmCall& g, hipStream_t st) {
   constexpr int TILE_BYTES = (BM + BN) * 128;

@@ -147,6 +147,25 @@ struct PackedPlan {
   int MT, NCT, NW, KU, gx, gz;
 };
 PackedPlan packed_plan(int M, int N, int K, int S, int nct = 0);
+// decode MLP in one launch (fc1 + bias + GELU -> fc2 split-K partials, the edge handed off in-launch):
+// part[8][M][d] raw fc2 partials (no bias) for reduce_ln, h [M][4d] the GELU(fc1) rows (write-through),
+// cnt: kMlpCounters zeroed ints per context (8 monotonic slice counters + an error word set on a poll timeout)
+struct MlpCall {
+  const uint16_t* A = nullptr;  // LN(x) rows, 16-bit
+  long lda = 0;
+  const uint16_t* W1 = nullptr;  // packed fc1 [4d][d]
+  const float* b1 = nullptr;
+  const uint16_t* W2 = nullptr;  // packed fc2 [d][4d]
+  uint16_t* h = nullptr;
+  float* part = nullptr;
+  int* cnt = nullptr;
+  int M = 0, d = 0;
+  unsigned long long* tprobe = nullptr;
+  const int* pslot = nullptr;
+};
+constexpr int kMlpCounters = 16, kMlpSlices = 8;
+bool mlp_fused_ok(int M, int d);
+void launch_mlp_fused(DT dt, const MlpCall& c, hipStream_t st);
 // the element offsets a packed-GEMM lane reads, shared by gemm_packed_kernel and the host-side extent check
 // (packed_extent): k-step range of one wave, the B fragment of column tile t (clamped to the last tile) and the A
 // fragment of row `row` (clamped to the last row)

@@ -502,6 +502,7 @@ struct Ctx {
   float* xa_ws = nullptr;
   int* xa_cnt = nullptr;
   int* red_cnt = nullptr;  // RedTail arrival counters (packed GEMM with in-launch reduce + LayerNorm)
+  int* mlp_cnt = nullptr;  // fused-MLP slice counters + error word (launch_mlp_fused)
   uint32_t* mask = nullptr;
   // alignment
   float *scores = nullptr, *align_out = nullptr, *tprob = nullptr;
@@ -531,6 +532,7 @@ struct Ctx {
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   double start_delay_us = 0;    // wmx_ctx_set_phase_offset: idle time before the decode loop (group phase offset)
   bool xq_fused = true;         // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED=0: off)
+  bool mlp_fused = false;       // decode step: fc1 -> fc2 in one launch, in-launch hand-off (WMX_MLP_FUSED=1)
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -647,6 +649,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
   P.add(&c.red_cnt, (size_t)packed_tail_counters());
+  P.add(&c.mlp_cnt, (size_t)kMlpCounters);
   P.add(&c.probe_buf, (size_t)kProbeLaunches * T * kProbeWG * 2);
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
@@ -1054,6 +1057,26 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     probe(kProbeCrossOut);
     gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b, pbuf(kProbeRedCrossOut));
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
+    if (c.mlp_fused && mlp_fused_ok(R, dt)) {  // one launch for fc1 -> fc2 (its span is recorded as the fc1 probe), then reduce_ln
+      MlpCall mc;
+      mc.A = c.dhb;
+      mc.lda = dt;
+      mc.W1 = L.wfc1;
+      mc.b1 = L.bfc1;
+      mc.W2 = L.wfc2;
+      mc.h = c.df1;
+      mc.part = c.part;
+      mc.cnt = c.mlp_cnt;
+      mc.M = R;
+      mc.d = dt;
+      mc.tprobe = pbuf(kProbeFc1);
+      mc.pslot = c.slot;
+      launch_mlp_fused(c.dt, mc, c.st);
+      launch_reduce_ln(c.dt, c.part, kMlpSlices, L.bfc2, c.dx, last ? m.lng : m.dec[l + 1].ln1g,
+                       last ? m.lnb : m.dec[l + 1].ln1b, c.dhb, R, dt, c.st,
+                       probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr, c.slot);
+      continue;
+    }
     probe(kProbeFc1);
     gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
     probe(kProbeFc2);
@@ -1884,6 +1907,12 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   rec(c, 7);
   WMX_HIP(hipEventSynchronize(c.ev[7]));
   for (int i = 0; i < 7; ++i) WMX_HIP(hipEventElapsedTime(&c.stage_ms[i], c.ev[i], c.ev[i + 1]));
+  if (c.mlp_fused) {  // the fused MLP's bounded poll flags a producer that never arrived instead of hanging
+    int err = 0;
+    WMX_HIP(hipMemcpyAsync(&err, c.mlp_cnt + kMlpSlices, sizeof(int), hipMemcpyDeviceToHost, c.st));
+    WMX_HIP(hipStreamSynchronize(c.st));
+    WMX_CHECK(err == 0, "fused mlp: a slice producer never arrived (poll timeout)");
+  }
 
   for (int b = 0; b < B; ++b) {
     wmx_window_result& w = res->win[b];
@@ -2183,6 +2212,7 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       // fused cross-q is the default (397-398 vs 383-384x real time, gpurun_out/r02za); WMX_XQ_FUSED=0 restores the
       // separate split-K launch (A/B runs)
       c.xq_fused = !(getenv("WMX_XQ_FUSED") && atoi(getenv("WMX_XQ_FUSED")) == 0);
+      c.mlp_fused = getenv("WMX_MLP_FUSED") && atoi(getenv("WMX_MLP_FUSED")) == 1;
       gemm_init_attributes();
       alloc_ctx(c);
     } catch (...) {

@@ -453,6 +453,27 @@ def test_separate_cross_q_step_parity():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
+@pytest.mark.timeout(900)
+def test_fused_mlp_step_parity():
+    """The decode MLP as one launch (WMX_MLP_FUSED=1, wmx_gemm.hip mlp_fused_kernel: fc1 + GELU -> fc2 partials with
+    the fc1 -> fc2 edge handed off inside the launch, write-through stores + slice counters): this file's teacher-forced
+    step tests, search replays and full-depth tests (d 1280 at 20 rows, d 384 at 3 rows; rows <= 32 take the fused
+    form) and the two-group concurrency test rerun in a child process with the switch set (read at context
+    creation)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WMX_MLP_FUSED="1")
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+           "-k", "forced_steps or search_replay or full_depth or concurrent", "tests/test_gpu_step.py",
+           "tests/test_gpu_concurrent.py"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=880)
+    print(r.stdout[-1500:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # BASELINE config 1 on the HIP path: Whisper tiny at full depth (4 + 4 layers, d 384, 80 mels), greedy
 # ---------------------------------------------------------------------------------------------------------------
