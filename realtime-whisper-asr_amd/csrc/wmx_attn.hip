@@ -239,11 +239,15 @@ __device__ inline int enc_sw(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) <<
 
 constexpr int kEncTile = 64;                       // keys per step
 constexpr int kEncTileBytes = kEncTile * 64 * 2;   // one K or V tile
-template <DT T>
-__global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
+// NWV waves x 32 queries per workgroup share every K/V tile: the kernel is bound by the rate at which a CU fills
+// its LDS from L2 (~11-13 B/clk/CU, MI355X_MICROARCH.md 'prologue HBM burst'; 4 waves: 10.6 B/clk measured), so
+// the K/V bytes per query set its speed -- 8 waves halve them
+template <DT T, int NWV, int MINW>
+__global__ __launch_bounds__(64 * NWV, MINW) void enc_attn_kernel(AttnArgs a) {
+  constexpr int QB = 32 * NWV, NP = 8 / NWV;  // queries per workgroup; K (and V) pieces each wave stages per tile
   // 1-D grid, XCD-grouped (§5.5 T1): the query tiles of one (window, head) run on one XCD, so its K/V stream is
   // fetched into that XCD's L2 once instead of once per tile
-  const int nqt = (a.Tq + 127) / 128, nwg = nqt * a.H * a.B;
+  const int nqt = (a.Tq + QB - 1) / QB, nwg = nqt * a.H * a.B;
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -257,36 +261,37 @@ __global__ __launch_bounds__(256, 2) void enc_attn_kernel(AttnArgs a) {
   const uint16_t* qb = a.q + (long)b * a.q_bstride + (long)h * a.head_stride;
   const uint16_t* kb = a.k + (long)b * a.k_bstride + (long)h * a.head_stride;
   const uint16_t* vb = a.v + (long)b * a.v_bstride + (long)h * a.head_stride;
-  const int q0 = qt * 128 + wave * 32;
+  const int q0 = qt * QB + wave * 32;
   const int Tk = a.Tk;
   const int ntiles = (Tk + kEncTile - 1) / kEncTile;
 
-  // DMA staging: a tile is 8 pieces of 1 KiB (8 rows x 128 B); wave w stages K pieces w, w+4 and V pieces w, w+4.
-  // Lane l covers row l >> 3 of its piece and reads source chunk (l & 7) ^ enc_sw(row).
+  // DMA staging: a tile is 8 pieces of 1 KiB (8 rows x 128 B); wave w stages K pieces w, w + NWV, .. and the same
+  // V pieces.  Lane l covers row l >> 3 of its piece and reads source chunk (l & 7) ^ enc_sw(row).
   const int srow = lane >> 3;
-  const int schunk0 = ((lane & 7) ^ enc_sw(wave * 8 + srow)) * 8, schunk1 = ((lane & 7) ^ enc_sw((wave + 4) * 8 + srow)) * 8;
+  int schunk[NP];
   // per-lane source pointers of tile 0, advanced by a wave-uniform 64 rows per tile; only the last tile clamps
-  const uint16_t* ksrc[2];
-  const uint16_t* vsrc[2];
+  const uint16_t* ksrc[NP];
+  const uint16_t* vsrc[NP];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = (wave + 4 * i) * 8 + srow;
-    ksrc[i] = kb + (long)r * a.k_ld + (i ? schunk1 : schunk0);
-    vsrc[i] = vb + (long)r * a.v_ld + (i ? schunk1 : schunk0);
+  for (int i = 0; i < NP; ++i) {
+    const int r = (wave + NWV * i) * 8 + srow;
+    schunk[i] = ((lane & 7) ^ enc_sw(r)) * 8;
+    ksrc[i] = kb + (long)r * a.k_ld + schunk[i];
+    vsrc[i] = vb + (long)r * a.v_ld + schunk[i];
   }
   auto stage = [&](int t, int buf) {
     char* kd = lds + buf * 2 * kEncTileBytes;
     char* vd = kd + kEncTileBytes;
     const bool edge = (t + 1) * kEncTile > Tk;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int piece = wave + 4 * i;
+    for (int i = 0; i < NP; ++i) {
+      const int piece = wave + NWV * i;
       const uint16_t* ks = ksrc[i] + (long)t * kEncTile * a.k_ld;
       const uint16_t* vs = vsrc[i] + (long)t * kEncTile * a.v_ld;
       if (edge) {  // rows past Tk re-read row Tk - 1 (finite data; their scores are masked)
         const int key = min(t * kEncTile + piece * 8 + srow, Tk - 1);
-        ks = kb + (long)key * a.k_ld + (i ? schunk1 : schunk0);
-        vs = vb + (long)key * a.v_ld + (i ? schunk1 : schunk0);
+        ks = kb + (long)key * a.k_ld + schunk[i];
+        vs = vb + (long)key * a.v_ld + schunk[i];
       }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ks,
                                        (__attribute__((address_space(3))) void*)(kd + piece * 1024), 16, 0, 0);
@@ -472,11 +477,23 @@ void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) {
     launch_attn_flash(dt, a, 0, 0, nullptr, st);
     return;
   }
-  dim3 grid(cdiv(a.Tq, 128) * a.H * a.B);
-  if (dt == DT::BF16)
-    hipLaunchKernelGGL(enc_attn_kernel<DT::BF16>, grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(enc_attn_kernel<DT::F16>, grid, dim3(256), 0, st, a);
+  // A/B switch (WMX_ENC_ATTN): 4 = 4-wave (128-query) workgroups, 82 = 8 waves at <= 256 VGPRs (one workgroup
+  // per CU), default 8 waves at <= 128 VGPRs (two per CU)
+  static const int form = getenv("WMX_ENC_ATTN") ? atoi(getenv("WMX_ENC_ATTN")) : 8;
+  const bool bf = dt == DT::BF16;
+  if (form == 4) {
+    dim3 grid(cdiv(a.Tq, 128) * a.H * a.B);
+    if (bf) hipLaunchKernelGGL((enc_attn_kernel<DT::BF16, 4, 2>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((enc_attn_kernel<DT::F16, 4, 2>), grid, dim3(256), 0, st, a);
+  } else if (form == 82) {
+    dim3 grid(cdiv(a.Tq, 256) * a.H * a.B);
+    if (bf) hipLaunchKernelGGL((enc_attn_kernel<DT::BF16, 8, 2>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((enc_attn_kernel<DT::F16, 8, 2>), grid, dim3(512), 0, st, a);
+  } else {
+    dim3 grid(cdiv(a.Tq, 256) * a.H * a.B);
+    if (bf) hipLaunchKernelGGL((enc_attn_kernel<DT::BF16, 8, 4>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((enc_attn_kernel<DT::F16, 8, 4>), grid, dim3(512), 0, st, a);
+  }
   WMX_HIP(hipGetLastError());
 }
 

@@ -17,5 +17,7 @@ best = None
 for _ in range(3):
     ms, _, fl = ctx.bench_kernel("encoder", 8, iters=3)
     best = ms if best is None else min(best, ms)
+at, _, afl = ctx.bench_kernel("enc_attn", 8, iters=20)
 print(f"{os.path.basename(os.environ.get('WMX_LIB', 'libwmx.so'))} {ct}: encoder {best:.2f} ms "
-      f"{fl / best / 1e9:.1f} TF/s {fl / best / 1e9 / 2500:.4f}", flush=True)
+      f"{fl / best / 1e9:.1f} TF/s {fl / best / 1e9 / 2500:.4f}; enc_attn {1000 * at:.1f} us "
+      f"{afl / at / 1e9:.1f} TF/s", flush=True)
