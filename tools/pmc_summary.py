@@ -1,23 +1,18 @@
-"""Average rocprofv3 --pmc counters per (kernel, grid) from a run_counter_collection.csv (tuning aid).
-Usage: python tools/pmc_summary.py <run_counter_collection.csv> [kernel-substring ...]"""
+"""Averages rocprofv3 counter_collection.csv rows per (kernel, counter) for kernels matching a pattern:
+python tools/pmc_summary.py <dir> <kernel substring>"""
 import collections
 import csv
+import glob
+import os
 import sys
 
-
-def main():
-    rows = list(csv.DictReader(open(sys.argv[1])))
-    pats = sys.argv[2:]
-    agg = collections.defaultdict(lambda: collections.defaultdict(list))
-    for r in rows:
-        k = r["Kernel_Name"]
-        if pats and not any(p in k for p in pats):
-            continue
-        agg[(k.split("(")[0][-40:], r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for (k, g), d in sorted(agg.items()):
-        m = {c: sum(v) / len(v) for c, v in d.items()}
-        print(k, "grid", g, " ".join(f"{c}={m[c]:.3g}" for c in sorted(m)))
-
-
-if __name__ == "__main__":
-    main()
+root, pat = sys.argv[1], sys.argv[2]
+acc = collections.defaultdict(list)
+for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row.get("Kernel_Name", "")
+            if pat in name:
+                acc[(name[:60], row["Counter_Name"])].append(float(row["Counter_Value"]))
+for (k, c), v in sorted(acc.items()):
+    print(f"{k:60s} {c:28s} n={len(v):3d} mean={sum(v) / len(v):.6g}")
