@@ -10,7 +10,11 @@
 // Epilogues are fused: bias, exact-erf GELU, fp32 residual add (the residual stream stays fp32), conv2's
 // GELU + sinusoidal position add, the decoder QKV scatter straight into the self-attention KV cache, and
 // split-K fp32 partial slabs reduced deterministically (fixed order) by gemm_splitk_reduce.
+#include <array>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "wmx_common.h"
 #include "wmx_kernels.h"
@@ -1449,6 +1453,20 @@ static int packed_mt(int M) {
 int packed_nct(int M, int N, int K) {
   const int mt = packed_mt(M);
   if (mt > 4) return 2;
+  // tuning override (WMX_PACKED_NCT="N:K:nct,..."): the column tiles per workgroup of one projection shape
+  static const std::vector<std::array<int, 3>> ov = [] {
+    std::vector<std::array<int, 3>> v;
+    const char* e = getenv("WMX_PACKED_NCT");
+    for (const char* q = e; q && *q;) {
+      std::array<int, 3> t{};
+      if (sscanf(q, "%d:%d:%d", &t[0], &t[1], &t[2]) == 3 && (t[2] == 1 || t[2] == 2 || t[2] == 4)) v.push_back(t);
+      q = strchr(q, ',');
+      if (q) ++q;
+    }
+    return v;
+  }();
+  for (const auto& t : ov)
+    if (t[0] == N && t[1] == K) return t[2];
   return (N >= 16384 || K >= 4096) ? 4 : 2;
 }
 
