@@ -424,7 +424,7 @@ def main():
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
     # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py: FETCH_SIZE x2 +
     # WRITE_SIZE, separate passes) of the same launches replayed alone at this context's batch
-    for tag in ("r02", "r01g"):
+    for tag in ("r03", "r02", "r01g"):
         pmc = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")
         if not os.path.exists(pmc):
             continue

@@ -705,9 +705,11 @@ static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ld
     launch_gemm(c.dt, g, c.st);
     return;
   }
-  static const int m128 = [] {  // rows from which the 128x128 tile is used; WMX_GEMM_M128 overrides (tuning runs)
+  // rows from which the 128x128 tile is used (the word-alignment forward, ~900 rows per context group: align stage
+  // 15.7-16.3 vs 16.9-18.8 ms with 64x64 tiles, profiles/r03r_align_m128_ab.txt); WMX_GEMM_M128 overrides
+  static const int m128 = [] {
     const char* v = getenv("WMX_GEMM_M128");
-    return v ? atoi(v) : 1024;
+    return v ? atoi(v) : 512;
   }();
   if (M >= m128) {
     g.tile = TILE_128x128;
@@ -1369,29 +1371,35 @@ static void set_slot(Ctx& c, int v) {
 // DTW (openai timing.dtw_cpu + backtrace), float32 cost accumulation like the oracle
 // ------------------------------------------------------------------------------------------------
 static void dtw(const float* x, int N, int Mc, int ld, std::vector<int>& ti, std::vector<int>& tj) {
-  std::vector<float> cost((size_t)(N + 1) * (Mc + 1), INFINITY);
+  // the cost matrix as two rolling columns, the trace column-major (the j-outer / i-inner sweep of dtw_cpu then walks
+  // contiguous memory), the three-way choice without branches: same comparisons, same tie rule as dtw_cpu
+  std::vector<float> colA(N + 1, INFINITY), colB(N + 1, INFINITY);
   std::vector<signed char> tr((size_t)(N + 1) * (Mc + 1), -1);
-  auto C = [&](int i, int j) -> float& { return cost[(size_t)i * (Mc + 1) + j]; };
-  auto Tr = [&](int i, int j) -> signed char& { return tr[(size_t)i * (Mc + 1) + j]; };
-  C(0, 0) = 0.f;
-  for (int j = 1; j <= Mc; ++j)
+  auto Tr = [&](int i, int j) -> signed char& { return tr[(size_t)j * (N + 1) + i]; };
+  // x transposed to [j][i] in blocks of 16 frames, so the i-inner sweep reads contiguously
+  std::vector<float> xt((size_t)Mc * N);
+  for (int j0 = 0; j0 < Mc; j0 += 16)
+    for (int i = 0; i < N; ++i)
+      for (int j = j0; j < std::min(Mc, j0 + 16); ++j) xt[(size_t)j * N + i] = x[(size_t)i * ld + j];
+  float* prev = colA.data();  // column j - 1
+  float* cur = colB.data();   // column j
+  prev[0] = 0.f;              // C(0, 0)
+  for (int j = 1; j <= Mc; ++j) {
+    cur[0] = INFINITY;  // C(0, j)
+    signed char* tcol = &Tr(0, j);
+    const float* xj = xt.data() + (size_t)(j - 1) * N;
+    float up = cur[0];  // C(i - 1, j)
     for (int i = 1; i <= N; ++i) {
-      const float c0 = C(i - 1, j - 1), c1 = C(i - 1, j), c2 = C(i, j - 1);
-      float v;
-      signed char t;
-      if (c0 < c1 && c0 < c2) {
-        v = c0;
-        t = 0;
-      } else if (c1 < c0 && c1 < c2) {
-        v = c1;
-        t = 1;
-      } else {
-        v = c2;
-        t = 2;
-      }
-      C(i, j) = -x[(size_t)(i - 1) * ld + (j - 1)] + v;
-      Tr(i, j) = t;
+      const float c0 = prev[i - 1], c1 = up, c2 = prev[i];
+      const bool p0 = c0 < c1 && c0 < c2, p1 = c1 < c0 && c1 < c2;
+      const float v = p0 ? c0 : (p1 ? c1 : c2);
+      const signed char t = p0 ? 0 : (p1 ? 1 : 2);
+      up = -xj[i - 1] + v;
+      cur[i] = up;
+      tcol[i] = t;
     }
+    std::swap(prev, cur);
+  }
   for (int j = 0; j <= Mc; ++j) Tr(0, j) = 2;
   for (int i = 0; i <= N; ++i) Tr(i, 0) = 1;
   int i = N, j = Mc;
