@@ -975,6 +975,7 @@ struct FwdArgs {
   bool prefill;
   const int* anc;
   bool align = false;
+  int win_rows = 0;  // decode step: rows per window of the cross attention (0: the context's beam width)
 };
 
 // Decode step (Tn == 1): every projection runs on packed weights with split-K partials, and the reductions are
@@ -1040,7 +1041,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.x_wstride = (long)kXS * dt;
     x.x_hstride = (long)kXS * 64;
     x.Tk = 1500;
-    x.rows_per_win = c.K;
+    x.rows_per_win = f.win_rows > 0 ? f.win_rows : c.K;
     x.qpart = c.part;
     x.qS = S;
     x.qpart_stride = (long)R * dt;
@@ -1631,8 +1632,16 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     f.pad_seq = nullptr;
     f.prefill = true;
     f.anc = nullptr;
-    dec_forward(c, f);
-    dec_logits(c, nullptr, B);
+    if (!m.fold) {
+      // the split-K decode step, one row per window (it writes cache slot 0 of rows 0 .. B-1, which the prompt
+      // prefill rewrites or no hypothesis reads) instead of dec_forward's unsplit projections
+      f.win_rows = 1;
+      dec_step_fast(c, f);
+      dec_logits(c, nullptr, B, true);
+    } else {
+      dec_forward(c, f);
+      dec_logits(c, nullptr, B);
+    }
     launch_lang_detect(c.logits, c.ldl, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st);
     debug_sync(c, "lang_detect", -1);
   }

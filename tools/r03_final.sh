@@ -7,10 +7,12 @@ cd "$(dirname "$0")/.."
 O=gpurun_out/${1:-r03z}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
-timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/gputest.log 2>&1
-rc=$?; tail -3 $O/gputest.log
-if [ $rc -ne 0 ]; then echo "gpu tests failed (rc $rc): stopping"; exit 1; fi
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; exit 1; }
+if [ "${2:-tests}" = tests ]; then
+  timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/gputest.log 2>&1
+  rc=$?; tail -3 $O/gputest.log
+  if [ $rc -ne 0 ]; then echo "gpu tests failed (rc $rc): stopping"; exit 1; fi
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; exit 1; }
+fi
 timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { echo bench failed; exit 1; }
 head -c 300 $O/bench_default.json; echo
 timeout -k 10 300 python bench.py --dtype f16 --steps 5 --no-cpu-baseline --no-stream > $O/bench_f16.json \
@@ -21,8 +23,10 @@ timeout -k 10 300 python bench.py --dtype fp8 --task translate --batch 16 --step
 timeout -k 10 300 python bench.py --batch 16 --steps 3 --no-cpu-baseline --no-stream > $O/bench_bf16_b16.json \
   2> $O/bench_bf16_b16.err || { echo bf16 b16 bench failed; exit 1; }
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 3 --warmup 1 \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 3 --warmup 1 \
   --no-cpu-baseline --no-stream > $O/bench_prof.json 2> $O/bench_prof.err || { echo profiled bench failed; exit 1; }
 find $O/prof -name '*kernel_trace.csv' -delete
+find $O/prof -name '*.db' -delete
+du -sh $O
 find $O/prof -type f | head -20
 exit 0
