@@ -11,8 +11,9 @@ for f in 4 8; do
   i=0
   for P in "$P1" "$P2"; do
     i=$((i+1))
-    WMX_ENC_ATTN=$f timeout -s KILL 90 rocprofv3 --pmc $P -d $O/f${f}_p$i -o pmc -- python3 tools/attn_pmc.py \
+    WMX_ENC_ATTN=$f timeout -s KILL 90 rocprofv3 --kernel-include-regex enc_attn --pmc $P -d $O/f${f}_p$i -o pmc -- python3 tools/attn_pmc.py \
       > $O/f${f}_p$i.log 2>&1 || { echo "pmc pass f$f p$i failed"; tail -5 $O/f${f}_p$i.log; exit 1; }
   done
 done
-find $O -name '*counter_collection.csv' | head
+python tools/pmc_summary.py $O enc_attn | tee $O/summary.txt
+find $O -name '*.csv' ! -name '*counter_collection.csv' -delete
