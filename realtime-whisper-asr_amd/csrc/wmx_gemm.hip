@@ -321,7 +321,7 @@ __device__ unsigned long long g256_stamps[kG256Stamps][3];
 #define WMX_G256_DIRECT 1  // LDS-free epilogue for the bf16-output kinds (0: the LDS-image epilogue for all)
 #endif
 constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
-constexpr int kG256Lds = 4 * kG256Slot;     // 128 KiB
+constexpr int kG256Lds = 4 * kG256Slot + 256 * 8;  // 128 KiB ring + the LayerNorm-folded kinds' row (mean, rstd)
 
 // apply the epilogue to `rows` rows of an fp32 LDS image [rows][ldt] holding output rows mb.. and columns n0..n0+BN
 template <DT T, int BN, int NT>
@@ -361,6 +361,11 @@ __device__ inline void epi_from_image(const Epi& e, const float* img, int ldt, i
 template <DT T, int KIND>
 __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
                                   const float4* bpre = nullptr) {
+  // the LayerNorm-statistics producers (encoder fold) are their base kind plus a 16-bit copy of x and the row's
+  // (mean, M2) over this tile's 256 columns: a wave holds one whole tile row (64 lanes x 4 columns), so both are
+  // two wave sums; the host guarantees N % 256 == 0 for them, so no lane leaves early and the row test is uniform
+  constexpr bool kLns = KIND == EPI_RESID32_LNS || KIND == EPI_GELU_POS32_LNS;
+  constexpr int KD = KIND == EPI_RESID32_LNS ? EPI_RESID32 : KIND == EPI_GELU_POS32_LNS ? EPI_GELU_POS32 : KIND;
   const int c4 = (tid & 63) * 4, r0 = tid >> 6;
   const int n = n0 + c4;
   if (n >= N) return;
@@ -375,9 +380,9 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
     const int row = r0 + 8 * u, m = mb + row;
     v[u] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
     v[u] = make_float4(v[u].x + b.x, v[u].y + b.y, v[u].z + b.z, v[u].w + b.w);
-    if (KIND == EPI_RESID32 && m < M)
+    if (KD == EPI_RESID32 && m < M)
       aux[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
-    if (KIND == EPI_GELU_POS32 && m < M)
+    if (KD == EPI_GELU_POS32 && m < M)
       aux[u] = *reinterpret_cast<const float4*>(e.pos + (long)(m % e.posT) * e.ldc + n);
   }
 #pragma unroll
@@ -385,11 +390,11 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
     const int m = mb + r0 + 8 * u;
     if (m >= M) continue;
     float4 x = v[u];
-    if (KIND == EPI_GELU16 || KIND == EPI_GELU_POS32 || KIND == EPI_GELU_MX8)
+    if (KD == EPI_GELU16 || KD == EPI_GELU_POS32 || KD == EPI_GELU_MX8)
       x = make_float4(gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w));
-    if (KIND == EPI_RESID32 || KIND == EPI_GELU_POS32)
+    if (KD == EPI_RESID32 || KD == EPI_GELU_POS32)
       x = make_float4(x.x + aux[u].x, x.y + aux[u].y, x.z + aux[u].z, x.w + aux[u].w);
-    if (KIND == EPI_GELU_MX8) {
+    if (KD == EPI_GELU_MX8) {
       // the 8 lanes of a 32-column block (c4 = 4 * (tid & 63)) agree on the block scale; every lane of the wave
       // is on the same row, so the shuffles never cross an inactive lane
       const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)))));
@@ -397,13 +402,21 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
       *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(e.out) + (long)m * e.ldc + n) =
           mx8_pack4(x.x * is, x.y * is, x.z * is, x.w * is);
       if ((tid & 7) == 0) e.out2[(long)m * e.ldc2 + (n >> 5)] = (uint8_t)(ex + 127);
-    } else if (KIND == EPI_STORE16 || KIND == EPI_GELU16 || KIND == EPI_CROSSKV) {
+    } else if (KD == EPI_STORE16 || KD == EPI_GELU16 || KD == EPI_CROSSKV) {
       const u16x4 h = {from_f32<T>(x.x), from_f32<T>(x.y), from_f32<T>(x.z), from_f32<T>(x.w)};
-      uint16_t* dst = KIND == EPI_CROSSKV ? reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)
-                                          : reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n;
+      uint16_t* dst = KD == EPI_CROSSKV ? reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)
+                                        : reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n;
       *reinterpret_cast<u16x4*>(dst) = h;
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n) = x;
+      if constexpr (kLns) {
+        const u16x4 h = {from_f32<T>(x.x), from_f32<T>(x.y), from_f32<T>(x.z), from_f32<T>(x.w)};
+        *reinterpret_cast<u16x4*>(e.out16 + (long)m * e.ldc + n) = h;
+        const float mu = wave_sum((x.x + x.y) + (x.z + x.w)) * (1.0f / 256.0f);
+        const float a = x.x - mu, bb = x.y - mu, cc = x.z - mu, dd = x.w - mu;
+        const float q = wave_sum((a * a + bb * bb) + (cc * cc + dd * dd));
+        if ((tid & 63) == 0) e.stats[(long)(n0 >> 8) * e.stats_ld + m] = make_float2(mu, q);
+      }
     }
   }
 }
@@ -544,10 +557,22 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias, loaded now so its latency hides behind
   // the main loop (the epilogue's column quads are the same in all four rounds)
   // (direct epilogue kinds: the lane's column quad after the in-quad transpose, wn 64 + 16 (fr & 3) + 4 (fr >> 2))
-  constexpr bool kDirect = WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16);
+  // LayerNorm-folded consumers (encoder): out = rstd_m (acc - mean_m c1[n]) + c2[n] with c2 passed as the bias;
+  // (mean, rstd) of the tile's 256 rows are merged from the producer's per-256-column statistics at tile start
+  // into LDS past the ring, and c1's column quad is loaded with the bias
+  constexpr bool kLnf = KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GELU16;
+  constexpr bool kGelu = KIND == EPI_GELU16 || KIND == EPI_LNF_GELU16;
+  constexpr bool kDirect = kLnf || (WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16));
   const int bcol = kDirect ? (wave & 3) * 64 + 16 * (lane & 3) + 4 * ((lane >> 2) & 3) : 4 * (tid & 63);
-  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f), c14 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (KIND >= 0 && e.bias && n0 + bcol < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
+  if (kLnf && n0 + bcol < N) c14 = *reinterpret_cast<const float4*>(e.c1 + n0 + bcol);
+  float2 lsv[8];
+  if constexpr (kLnf) {
+    const int mr = min(m0 + tid, M - 1);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) lsv[g] = g < e.lng && tid < 256 ? e.stats[(long)g * e.stats_ld + mr] : make_float2(0.f, 0.f);
+  }
 
   // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
   // Wave w issues pieces w, w + 8, w + 16, w + 24; lane l covers row l >> 2, 16-B column (l & 3).
@@ -610,6 +635,22 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (kLnf) {  // Chan merge of the equal-count (256-column) groups; the epilogue reads it after the loop
+    if (tid < 256) {
+      float mean = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) mean += g < e.lng ? lsv[g].x : 0.f;
+      mean /= (float)e.lng;
+      float m2 = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const float dm = lsv[g].x - mean;
+        m2 += g < e.lng ? lsv[g].y + 256.f * dm * dm : 0.f;
+      }
+      reinterpret_cast<float2*>(smem + 4 * kG256Slot)[tid] =
+          make_float2(mean, 1.0f / sqrtf(m2 / (256.f * (float)e.lng) + 1e-5f));
+    }
+  }
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
@@ -712,8 +753,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
             x0 = x2, x2 = t;
             t = x1, x1 = x3, x3 = t;
           }
-          float4 o = make_float4(x0 + bias4.x, x1 + bias4.y, x2 + bias4.z, x3 + bias4.w);
-          if (KIND == EPI_GELU16) o = make_float4(gelu_erf(o.x), gelu_erf(o.y), gelu_erf(o.z), gelu_erf(o.w));
+          float4 o;
+          if constexpr (kLnf) {
+            const float2 ls = reinterpret_cast<const float2*>(smem + 4 * kG256Slot)[m - m0];
+            o = make_float4(ls.y * (x0 - ls.x * c14.x) + bias4.x, ls.y * (x1 - ls.x * c14.y) + bias4.y,
+                            ls.y * (x2 - ls.x * c14.z) + bias4.z, ls.y * (x3 - ls.x * c14.w) + bias4.w);
+          } else {
+            o = make_float4(x0 + bias4.x, x1 + bias4.y, x2 + bias4.z, x3 + bias4.w);
+          }
+          if (kGelu) o = make_float4(gelu_erf(o.x), gelu_erf(o.y), gelu_erf(o.z), gelu_erf(o.w));
           if (m < M && n < N) {
             const u16x4 h = {from_f32<T>(o.x), from_f32<T>(o.y), from_f32<T>(o.z), from_f32<T>(o.w)};
             *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
@@ -1877,6 +1925,10 @@ static void g256_attr() {
   g256_attr_one<T, EPI_STORE32>();
   g256_attr_one<T, EPI_GELU_MX8>();
   g256_attr_one<T, EPI_CROSSKV>();
+  g256_attr_one<T, EPI_RESID32_LNS>();
+  g256_attr_one<T, EPI_GELU_POS32_LNS>();
+  g256_attr_one<T, EPI_LNF_STORE16>();
+  g256_attr_one<T, EPI_LNF_GELU16>();
 }
 // persistent grid: one workgroup per CU (the 128 KiB ring allows no second one), a multiple of 8 workgroups
 static int g256_grid(int tiles) {
@@ -1908,6 +1960,10 @@ static void launch_g256(const GemmCall& g, hipStream_t st) {
     case EPI_STORE32: WMX_G256_LAUNCH(EPI_STORE32); break;
     case EPI_GELU_MX8: WMX_G256_LAUNCH(EPI_GELU_MX8); break;
     case EPI_CROSSKV: WMX_G256_LAUNCH(EPI_CROSSKV); break;
+    case EPI_RESID32_LNS: WMX_G256_LAUNCH(EPI_RESID32_LNS); break;
+    case EPI_GELU_POS32_LNS: WMX_G256_LAUNCH(EPI_GELU_POS32_LNS); break;
+    case EPI_LNF_STORE16: WMX_G256_LAUNCH(EPI_LNF_STORE16); break;
+    case EPI_LNF_GELU16: WMX_G256_LAUNCH(EPI_LNF_GELU16); break;
     default: WMX_G256_LAUNCH(-1); break;
   }
 #undef WMX_G256_LAUNCH
@@ -1922,6 +1978,13 @@ static void launch_t(const GemmCall& g, hipStream_t st) {
   if (g.tile == TILE_256) {
     WMX_CHECK(g.K % 32 == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm256: K / leading dimensions");
     WMX_CHECK(g.epi.kind != EPI_CROSSKV || (g.epi.d % 256 == 0 && g.epi.xt % 4 == 0), "gemm256: cross K/V shape");
+    const bool lns = g.epi.kind == EPI_RESID32_LNS || g.epi.kind == EPI_GELU_POS32_LNS;
+    const bool lnf = g.epi.kind == EPI_LNF_STORE16 || g.epi.kind == EPI_LNF_GELU16;
+    WMX_CHECK(!lns || (g.N % 256 == 0 && g.epi.ldc % 4 == 0 && g.epi.out16 && g.epi.stats && g.epi.stats_ld >= g.M),
+              "gemm256: LayerNorm-statistics epilogue shape");
+    WMX_CHECK(!lnf || (g.N % 4 == 0 && g.epi.ldc % 4 == 0 && g.epi.c1 && g.epi.bias && g.epi.stats &&
+                       g.epi.lng >= 1 && g.epi.lng <= 8 && g.epi.stats_ld >= g.M),
+              "gemm256: LayerNorm-folded epilogue shape");
     launch_g256<T>(g, st);
     return;
   }

@@ -16,6 +16,11 @@ enum EpiKind {
   // decode step, LayerNorm folded into the projections (packed GEMM, S == 1; row_ln_from_stats):
   EPI_RESID_STATS = 8,  // x32 = out += acc + bias; out16 = 16-bit(x32); stats[n / 16][m] = (mean, M2) of x32
   EPI_LNFOLD_GELU16 = 9,  // out16 = gelu(rstd_m (acc - mean_m c1[n]) + c2[n]), (mean, rstd) from stats
+  // encoder, LayerNorm folded into the projections (gemm256 only, N % 256 == 0 for the producers):
+  EPI_RESID32_LNS = 10,     // EPI_RESID32 + out16 = 16-bit(x32) + stats[n / 256][m] = (mean, M2) of x32's 256 columns
+  EPI_GELU_POS32_LNS = 11,  // EPI_GELU_POS32 + the same out16 / stats
+  EPI_LNF_STORE16 = 12,     // out16 = rstd_m (acc - mean_m c1[n]) + bias[n], (mean, rstd) merged from stats[lng][m]
+  EPI_LNF_GELU16 = 13,      // out16 = gelu(rstd_m (acc - mean_m c1[n]) + bias[n])
 };
 
 struct Epi {
@@ -41,6 +46,7 @@ struct Epi {
   uint16_t* out16 = nullptr;
   const float* c1 = nullptr;
   const float* c2 = nullptr;
+  int lng = 0;  // EPI_LNF_*: 256-column groups of the row statistics (the LayerNorm width / 256)
 };
 
 // padded key stride of the cross K/V images (a multiple of 32 keys; the pad stays zero)
@@ -232,8 +238,9 @@ void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, co
 // one wave idles on the stream for `ticks` device wall-clock ticks (a phase offset between context groups)
 void launch_spin(unsigned long long ticks, hipStream_t st);
 // LayerNorm (g, b) folded into the projection W (+ bias): packed Wp = W diag(g), c1 = Wp 1, c2 = bias + W b
+// (rowmajor: Wp is written row-major [N][K] instead of packed: the encoder's gemm256 operand)
 void launch_fold_ln(DT dt, const uint16_t* Wrm, const float* g, const float* b, const float* bias, int N, int K,
-                    uint16_t* Wp, float* c1, float* c2, hipStream_t st);
+                    uint16_t* Wp, float* c1, float* c2, hipStream_t st, bool rowmajor = false);
 
 // attention
 struct AttnArgs {

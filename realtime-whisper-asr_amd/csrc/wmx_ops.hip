@@ -389,14 +389,14 @@ template <DT T>
 __global__ __launch_bounds__(256) void fold_ln_kernel(const uint16_t* __restrict__ Wrm, const float* __restrict__ g,
                                                       const float* __restrict__ b, const float* __restrict__ bias,
                                                       int K, uint16_t* __restrict__ Wp, float* __restrict__ c1,
-                                                      float* __restrict__ c2) {
+                                                      float* __restrict__ c2, int rowmajor) {
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __shared__ float red[2][4];
   float s1 = 0.f, s2 = 0.f;
   for (int k = tid; k < K; k += 256) {
     const float w = to_f32<T>(Wrm[(long)n * K + k]);
     const uint16_t wf = from_f32<T>(w * g[k]);
-    Wp[packed_index(n, k, K)] = wf;
+    Wp[rowmajor ? (long)n * K + k : packed_index(n, k, K)] = wf;
     s1 += to_f32<T>(wf);
     s2 += b[k] * w;
   }
@@ -414,12 +414,13 @@ __global__ __launch_bounds__(256) void fold_ln_kernel(const uint16_t* __restrict
 }
 
 void launch_fold_ln(DT dt, const uint16_t* Wrm, const float* g, const float* b, const float* bias, int N, int K,
-                    uint16_t* Wp, float* c1, float* c2, hipStream_t st) {
+                    uint16_t* Wp, float* c1, float* c2, hipStream_t st, bool rowmajor) {
   WMX_CHECK(N % 16 == 0 && K % 32 == 0, "fold_ln: shape");
+  const int rm = rowmajor ? 1 : 0;
   if (dt == DT::BF16)
-    hipLaunchKernelGGL(fold_ln_kernel<DT::BF16>, dim3(N), dim3(256), 0, st, Wrm, g, b, bias, K, Wp, c1, c2);
+    hipLaunchKernelGGL(fold_ln_kernel<DT::BF16>, dim3(N), dim3(256), 0, st, Wrm, g, b, bias, K, Wp, c1, c2, rm);
   else
-    hipLaunchKernelGGL(fold_ln_kernel<DT::F16>, dim3(N), dim3(256), 0, st, Wrm, g, b, bias, K, Wp, c1, c2);
+    hipLaunchKernelGGL(fold_ln_kernel<DT::F16>, dim3(N), dim3(256), 0, st, Wrm, g, b, bias, K, Wp, c1, c2, rm);
   WMX_HIP(hipGetLastError());
 }
 

@@ -120,6 +120,9 @@ struct EncLayer {
   // MX-fp8 copies of the four projections (model dtype WMX_DTYPE_MX8): e4m3 [N][K] + e8m0 scales [N][K/32]
   uint8_t *qkv8 = nullptr, *qkv8s = nullptr, *o8 = nullptr, *o8s = nullptr, *fc18 = nullptr, *fc18s = nullptr,
           *fc28 = nullptr, *fc28s = nullptr;
+  // LayerNorm folded into qkv (LN1) and fc1 (LN2) (Model::enc_fold): row-major W diag(g), c1 = W' 1, c2 = bias + W b
+  uint16_t *fqkv = nullptr, *ffc1 = nullptr;
+  float *c1qkv = nullptr, *c2qkv = nullptr, *c1fc1 = nullptr, *c2fc1 = nullptr;
 };
 struct DecLayer {
   float *ln1g, *ln1b, *bqkv, *bo, *ln2g, *ln2b, *bcq, *bco, *ln3g, *ln3b, *bfc1, *bfc2;
@@ -155,6 +158,9 @@ struct Model {
   bool initialized = false;
   bool dirty = false;  // a tensor was set since the derived copies (row-major, MX-fp8, folded) were made
   bool fold = false;   // decode step on the LayerNorm-folded projections (WMX_FOLD=1; default: reduce_ln form)
+  // encoder: the two LayerNorms of every layer folded into qkv / fc1 (the residual producers leave x's 16-bit copy
+  // and per-256-column statistics); 16-bit models with a width multiple of 256 (WMX_ENC_FOLD=0 turns it off)
+  bool enc_fold = false;
   hipStream_t st = nullptr;
 };
 
@@ -211,6 +217,15 @@ static void build_model(Model& m) {
       P.add(&L.fc28, (size_t)4 * da * da);
       P.add(&L.fc28s, (size_t)4 * da * da / 32);
     }
+  }
+  for (auto& L : m.enc) {
+    if (!m.enc_fold) break;
+    P.add(&L.fqkv, (size_t)3 * da * da);
+    P.add(&L.ffc1, (size_t)4 * da * da);
+    P.add(&L.c1qkv, 3 * da);
+    P.add(&L.c2qkv, 3 * da);
+    P.add(&L.c1fc1, 4 * da);
+    P.add(&L.c2fc1, 4 * da);
   }
   P.add(&m.lnpg, da);
   P.add(&m.lnpb, da);
@@ -409,6 +424,14 @@ static void debug_device(const char* what) {
 }
 
 static void prepare_fold(Model& m) {
+  if (m.enc_fold) {
+    const int da = m.d.n_audio_state;
+    for (auto& L : m.enc) {
+      launch_fold_ln(m.dt, L.wqkv, L.ln1g, L.ln1b, L.bqkv, 3 * da, da, L.fqkv, L.c1qkv, L.c2qkv, m.st, true);
+      launch_fold_ln(m.dt, L.wfc1, L.ln2g, L.ln2b, L.bfc1, 4 * da, da, L.ffc1, L.c1fc1, L.c2fc1, m.st, true);
+    }
+    WMX_HIP(hipStreamSynchronize(m.st));
+  }
   if (!m.fold) return;
   const int dt = m.d.n_text_state;
   for (auto& L : m.dec) {
@@ -488,6 +511,7 @@ struct Ctx {
   float* ws = nullptr;
   long ws_elems = 0;
   float* part = nullptr;  // split-K partials of the packed decode GEMMs [S][rows][N]
+  float2* est = nullptr;    // encoder fold: per-256-column (mean, M2) of the residual rows [da / 256][maxB * 1500]
   float2* rstat = nullptr;  // LayerNorm-folded step: per-16-column (mean, M2) of the residual rows [dt / 16][R]
   long part_elems = 0;
   int *hist = nullptr, *hist_tmp = nullptr, *anc = nullptr, *anc_tmp = nullptr, *pad_row = nullptr, *pad_win = nullptr;
@@ -585,6 +609,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.eao, (size_t)B * 1500 * da);
   P.add(&c.ef1, (size_t)B * 1500 * 4 * da);
   P.add(&c.enc_out, (size_t)B * 1500 * da);
+  if (c.m->enc_fold) P.add(&c.est, (size_t)(da / 256) * B * 1500);
   if (c.m->mx8) {
     P.add(&c.eh8, (size_t)B * 1500 * da);
     P.add(&c.eh8s, (size_t)B * 1500 * da / 32);
@@ -901,14 +926,43 @@ static void encode_layers_mx8(Ctx& c, int B) {
   }
 }
 
+// encoder pass on the 256 x 256 GEMM with the LayerNorms folded (Model::enc_fold): the residual producers (conv2,
+// out-proj, fc2) leave x in fp32, its 16-bit copy in ehb and the row statistics per 256 columns in est; qkv and fc1
+// multiply the 16-bit x by W diag(g) and finish LN in their epilogue, rstd (acc - mean c1) + c2 (wmx_gemm.hip).
+// No LayerNorm launches inside the stack; the final one (ln_post) stays.  Numerics: x enters the projections
+// rounded to 16 bits before the mean is removed, which adds ~2^-9 |mean| / std relative error per projection input
+// on top of the unfolded form's LN-output rounding ("Encoder LayerNorm fold").
+static bool enc_fold_rows(const Ctx& c, long rows) {
+  static const bool no_g256 = getenv("WMX_NO_G256") != nullptr;
+  return c.m->enc_fold && c.est && rows >= 4096 && !no_g256;  // the gemm256 dispatch condition of gemm()
+}
+
+static Epi epi_lns(Ctx& c, int kind, const float* bias, long rows) {
+  Epi e = epi(kind, bias, c.ex, c.m->d.n_audio_state);
+  e.out16 = c.ehb;
+  e.stats = c.est;
+  e.stats_ld = rows;
+  return e;
+}
+
+static Epi epi_lnf(Ctx& c, int kind, const float* c1, const float* c2, void* out, long ldc, long rows) {
+  Epi e = epi(kind, c2, out, ldc);
+  e.c1 = c1;
+  e.stats = c.est;
+  e.stats_ld = rows;
+  e.lng = c.m->d.n_audio_state / 256;
+  return e;
+}
+
 static void encode(Ctx& c, int B) {
   Model& m = *c.m;
   const int da = m.d.n_audio_state, H = m.d.n_audio_head, M = m.d.n_mels;
   const long rows = (long)B * 1500;
+  const bool fold = !m.mx8 && enc_fold_rows(c, rows);
   launch_im2col_conv1(c.dt, c.mel, B, M, m.K1p, c.im1, c.st);
   gemm(c, c.im1, m.K1p, m.conv1w, m.K1p, B * 3000, da, m.K1p, epi(EPI_GELU16, m.conv1b, c.h1, da));
   launch_im2col_conv2(c.dt, c.h1, B, da, c.im2, c.st);
-  Epi e2 = epi(EPI_GELU_POS32, m.conv2b, c.ex, da);
+  Epi e2 = fold ? epi_lns(c, EPI_GELU_POS32_LNS, m.conv2b, rows) : epi(EPI_GELU_POS32, m.conv2b, c.ex, da);
   e2.pos = m.enc_pos;
   e2.posT = 1500;
   gemm(c, c.im2, 3 * da, m.conv2w, 3 * da, (int)rows, da, 3 * da, e2);
@@ -917,9 +971,16 @@ static void encode(Ctx& c, int B) {
     launch_layernorm(c.dt, c.ex, m.lnpg, m.lnpb, c.enc_out, (int)rows, da, c.st);
     return;
   }
-  for (auto& L : m.enc) {
-    launch_layernorm(c.dt, c.ex, L.ln1g, L.ln1b, c.ehb, (int)rows, da, c.st);
-    gemm(c, c.ehb, da, L.wqkv, da, (int)rows, 3 * da, da, epi(EPI_STORE16, L.bqkv, c.eqkv, 3 * da));
+  for (size_t l = 0; l < m.enc.size(); ++l) {
+    const EncLayer& L = m.enc[l];
+    const bool last = l + 1 == m.enc.size();
+    if (fold) {
+      gemm(c, c.ehb, da, L.fqkv, da, (int)rows, 3 * da, da,
+           epi_lnf(c, EPI_LNF_STORE16, L.c1qkv, L.c2qkv, c.eqkv, 3 * da, rows));
+    } else {
+      launch_layernorm(c.dt, c.ex, L.ln1g, L.ln1b, c.ehb, (int)rows, da, c.st);
+      gemm(c, c.ehb, da, L.wqkv, da, (int)rows, 3 * da, da, epi(EPI_STORE16, L.bqkv, c.eqkv, 3 * da));
+    }
     AttnArgs a{};
     a.q = c.eqkv;
     a.k = c.eqkv + da;
@@ -934,10 +995,18 @@ static void encode(Ctx& c, int B) {
     a.Tq = a.Tk = 1500;
     a.head_stride = 64;
     launch_attn_encoder(c.dt, a, c.st);
-    gemm(c, c.eao, da, L.wo, da, (int)rows, da, da, epi(EPI_RESID32, L.bo, c.ex, da));
-    launch_layernorm(c.dt, c.ex, L.ln2g, L.ln2b, c.ehb, (int)rows, da, c.st);
-    gemm(c, c.ehb, da, L.wfc1, da, (int)rows, 4 * da, da, epi(EPI_GELU16, L.bfc1, c.ef1, 4 * da));
-    gemm(c, c.ef1, 4 * da, L.wfc2, 4 * da, (int)rows, da, 4 * da, epi(EPI_RESID32, L.bfc2, c.ex, da));
+    if (fold) {
+      gemm(c, c.eao, da, L.wo, da, (int)rows, da, da, epi_lns(c, EPI_RESID32_LNS, L.bo, rows));
+      gemm(c, c.ehb, da, L.ffc1, da, (int)rows, 4 * da, da,
+           epi_lnf(c, EPI_LNF_GELU16, L.c1fc1, L.c2fc1, c.ef1, 4 * da, rows));
+      gemm(c, c.ef1, 4 * da, L.wfc2, 4 * da, (int)rows, da, 4 * da,
+           last ? epi(EPI_RESID32, L.bfc2, c.ex, da) : epi_lns(c, EPI_RESID32_LNS, L.bfc2, rows));
+    } else {
+      gemm(c, c.eao, da, L.wo, da, (int)rows, da, da, epi(EPI_RESID32, L.bo, c.ex, da));
+      launch_layernorm(c.dt, c.ex, L.ln2g, L.ln2b, c.ehb, (int)rows, da, c.st);
+      gemm(c, c.ehb, da, L.wfc1, da, (int)rows, 4 * da, da, epi(EPI_GELU16, L.bfc1, c.ef1, 4 * da));
+      gemm(c, c.ef1, 4 * da, L.wfc2, 4 * da, (int)rows, da, 4 * da, epi(EPI_RESID32, L.bfc2, c.ex, da));
+    }
   }
   launch_layernorm(c.dt, c.ex, m.lnpg, m.lnpb, c.enc_out, (int)rows, da, c.st);
 }
@@ -2008,6 +2077,10 @@ wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_mod
       // opt-in (WMX_FOLD=1): the LayerNorm-folded decode step passes every parity test but measured slower than
       // the split-K + reduce_ln step (356-390 vs 389-393x real time, interleaved on one box)
       w->m.fold = getenv("WMX_FOLD") != nullptr;
+      {
+        const char* ef = getenv("WMX_ENC_FOLD");
+        w->m.enc_fold = !w->m.mx8 && w->m.d.n_audio_state % 256 == 0 && !(ef && ef[0] == '0');
+      }
       WMX_HIP(hipSetDevice(device));
       WMX_HIP(hipStreamCreateWithFlags(&w->m.st, hipStreamNonBlocking));
       build_model(w->m);

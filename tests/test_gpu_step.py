@@ -279,6 +279,35 @@ def test_full_depth_large_v3_one_window(large_v3):
     _replay_and_compare("large-v3 full depth greedy", ctx, res, 1, opt, sp, 1)
 
 
+def test_full_depth_large_v3_encoder_layernorm_fold(large_v3):
+    """The encoder with its LayerNorms folded into qkv / fc1 (Model::enc_fold, on from 4096 rows: 3 windows here), all
+    32 layers, against the oracle's unfolded fp32 LayerNorms; and against the same device model with the fold off
+    (WMX_ENC_FOLD=0, read at model creation) -- the fold's own numerical cost, bf16."""
+    import os
+    from wmx import engine as E
+    d = O.DIMS["large-v3"]
+    m, W = large_v3
+    audios = [synth.speech_like(521, 480000), synth.speech_like(522, 300000), synth.speech_like(523, 480000)]
+    mels = np.stack([O.logmel_segment(a, d.n_mels) for a in audios])
+    ctx = E.Context(m, max_batch=3, beam_size=1, max_new_tokens=8, word_timestamps=False)
+    got = ctx.encode(mels)
+    os.environ["WMX_ENC_FOLD"] = "0"
+    try:
+        m0 = E.Model("large-v3", 0, "bfloat16").init_synthetic(1)
+    finally:
+        del os.environ["WMX_ENC_FOLD"]
+    ctx0 = E.Context(m0, max_batch=3, beam_size=1, max_new_tokens=8, word_timestamps=False)
+    got0 = ctx0.encode(mels)
+    for b in (0, 1):
+        ref = O.encoder(W, d, mels[b])
+        e, e0, ef = rel_l2(got[b], ref), rel_l2(got0[b], ref), rel_l2(got[b], got0[b])
+        print(f"large-v3 encoder window {b}: folded rel_l2 {e:.3e}, unfolded {e0:.3e}, folded vs unfolded {ef:.3e}")
+        assert e <= REL["bf16"], e
+        assert e <= 3 * e0 + 2e-3, (e, e0)  # the fold may not dominate the error budget
+    del ctx0
+    m0.close()
+
+
 def test_full_depth_large_v3_beam5_two_windows(large_v3):
     """Beam 5 (the reference default, asr_components.py:282; BASELINE config 3) through all 32 + 32 layers: 2 windows x
     5 rows, 16 teacher-forced steps with the beams re-parented every step (every row's logits vs the oracle), then a
