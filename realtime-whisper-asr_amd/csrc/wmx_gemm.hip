@@ -321,7 +321,9 @@ __device__ unsigned long long g256_stamps[kG256Stamps][3];
 #define WMX_G256_DIRECT 1  // LDS-free epilogue for the bf16-output kinds (0: the LDS-image epilogue for all)
 #endif
 constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
-constexpr int kG256Lds = 4 * kG256Slot + 256 * 8;  // 128 KiB ring + the LayerNorm-folded kinds' row (mean, rstd)
+// 128 KiB ring + the LayerNorm-folded kinds' raw row statistics [8 groups][256 rows] float2 and merged (mean, rstd)
+constexpr int kG256StatRaw = 4 * kG256Slot, kG256StatRow = kG256StatRaw + 8 * 256 * 8;
+constexpr int kG256Lds = kG256StatRow + 256 * 8;
 
 // apply the epilogue to `rows` rows of an fp32 LDS image [rows][ldt] holding output rows mb.. and columns n0..n0+BN
 template <DT T, int BN, int NT>
@@ -361,11 +363,7 @@ __device__ inline void epi_from_image(const Epi& e, const float* img, int ldt, i
 template <DT T, int KIND>
 __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
                                   const float4* bpre = nullptr) {
-  // the LayerNorm-statistics producers (encoder fold) are their base kind plus a 16-bit copy of x and the row's
-  // (mean, M2) over this tile's 256 columns: a wave holds one whole tile row (64 lanes x 4 columns), so both are
-  // two wave sums; the host guarantees N % 256 == 0 for them, so no lane leaves early and the row test is uniform
-  constexpr bool kLns = KIND == EPI_RESID32_LNS || KIND == EPI_GELU_POS32_LNS;
-  constexpr int KD = KIND == EPI_RESID32_LNS ? EPI_RESID32 : KIND == EPI_GELU_POS32_LNS ? EPI_GELU_POS32 : KIND;
+  constexpr int KD = KIND;
   const int c4 = (tid & 63) * 4, r0 = tid >> 6;
   const int n = n0 + c4;
   if (n >= N) return;
@@ -409,16 +407,93 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
       *reinterpret_cast<u16x4*>(dst) = h;
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n) = x;
-      if constexpr (kLns) {
-        const u16x4 h = {from_f32<T>(x.x), from_f32<T>(x.y), from_f32<T>(x.z), from_f32<T>(x.w)};
-        *reinterpret_cast<u16x4*>(e.out16 + (long)m * e.ldc + n) = h;
-        const float mu = wave_sum((x.x + x.y) + (x.z + x.w)) * (1.0f / 256.0f);
-        const float a = x.x - mu, bb = x.y - mu, cc = x.z - mu, dd = x.w - mu;
-        const float q = wave_sum((a * a + bb * bb) + (cc * cc + dd * dd));
-        if ((tid & 63) == 0) e.stats[(long)(n0 >> 8) * e.stats_ld + m] = make_float2(mu, q);
-      }
     }
   }
+}
+
+// eight per-lane values v[u] (u = row of the wave's 8) -> the sum over the wave's 64 lanes of row (lane >> 3), in
+// every lane of that row's 8-lane group: permlane32 / permlane16 swaps halve the rows a lane carries (4 + 2 swaps),
+// a row_ror:8 exchange picks one, and an 8-lane DPP sum finishes (10 cross-lane steps instead of 8 wave sums' 48)
+__device__ inline float rows8_sum(const float (&v)[8], int lane) {
+  float w[4], w2[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // lanes < 32: rows j, lanes >= 32: rows j + 4, each summed over l and l ^ 32
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + 4]), false, false);
+    w[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {  // 16-lane rows with bit 4 clear keep j, set keep j + 2, summed over l ^ 16
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[j]), __float_as_uint(w[j + 2]), false, false);
+    w2[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const bool b3 = (lane >> 3) & 1;  // bit 3 keeps w2[1]
+  const float keep = b3 ? w2[1] : w2[0], send = b3 ? w2[0] : w2[1];
+  return sum8_lanes(keep + dpp_mov<kDppXor8>(send));
+}
+
+// LayerNorm-statistics producers of the encoder fold (host: N % 256 == 0): a 64-row x 256-column LDS image, thread =
+// column quad (tid & 63) of rows r0 + 8u (r0 = wave).  x = acc + bias + hi + lo (RESID) or gelu(acc + bias) + pos
+// (conv2); x is stored back as the 16-bit planes hi = 16-bit(x) (e.out16, the A operand of the LayerNorm-folded
+// projection that follows) and lo = 16-bit(x - hi) (e.out), the same bytes as the fp32 row; per row, this tile's
+// (mean, M2) over its 256 columns goes to stats[n0 / 256][m] (Chan's pairwise form; two rows8_sum passes).
+template <DT T, int KIND>
+__device__ inline void epi_rows64_lns(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int tid,
+                                      const float4* bpre) {
+  const int lane = tid & 63, c4 = lane * 4, r0 = tid >> 6;
+  const int n = n0 + c4;
+  const float4 b = *bpre;
+  uint16_t* hi = e.out16;
+  uint16_t* lo = reinterpret_cast<uint16_t*>(e.out);
+  float4 x[8];
+  u16x4 ah[8], al[8];
+  float4 pp[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int row = r0 + 8 * u, mm = min(mb + row, M - 1);
+    x[u] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
+    x[u] = make_float4(x[u].x + b.x, x[u].y + b.y, x[u].z + b.z, x[u].w + b.w);
+    if (KIND == EPI_RESID32_LNS) {
+      ah[u] = *reinterpret_cast<const u16x4*>(hi + (long)mm * e.ldc + n);
+      al[u] = *reinterpret_cast<const u16x4*>(lo + (long)mm * e.ldc + n);
+    } else {
+      pp[u] = *reinterpret_cast<const float4*>(e.pos + (long)(mm % e.posT) * e.ldc + n);
+    }
+  }
+  float s[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = mb + r0 + 8 * u;
+    float4 v = x[u];
+    if (KIND == EPI_RESID32_LNS) {
+      v.x += to_f32<T>(ah[u][0]) + to_f32<T>(al[u][0]);
+      v.y += to_f32<T>(ah[u][1]) + to_f32<T>(al[u][1]);
+      v.z += to_f32<T>(ah[u][2]) + to_f32<T>(al[u][2]);
+      v.w += to_f32<T>(ah[u][3]) + to_f32<T>(al[u][3]);
+    } else {
+      v = make_float4(gelu_erf(v.x) + pp[u].x, gelu_erf(v.y) + pp[u].y, gelu_erf(v.z) + pp[u].z,
+                      gelu_erf(v.w) + pp[u].w);
+    }
+    x[u] = v;
+    const u16x4 h = {from_f32<T>(v.x), from_f32<T>(v.y), from_f32<T>(v.z), from_f32<T>(v.w)};
+    const u16x4 l = {from_f32<T>(v.x - to_f32<T>(h[0])), from_f32<T>(v.y - to_f32<T>(h[1])),
+                     from_f32<T>(v.z - to_f32<T>(h[2])), from_f32<T>(v.w - to_f32<T>(h[3]))};
+    if (m < M) {  // uniform over the wave (one row)
+      *reinterpret_cast<u16x4*>(hi + (long)m * e.ldc + n) = h;
+      *reinterpret_cast<u16x4*>(lo + (long)m * e.ldc + n) = l;
+    }
+    s[u] = (v.x + v.y) + (v.z + v.w);
+  }
+  const float mean_own = rows8_sum(s, lane) * (1.0f / 256.0f);  // the mean of row (lane >> 3)
+  float q[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const float mean_u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mean_own), 8 * u));
+    const float a = x[u].x - mean_u, bb = x[u].y - mean_u, cc = x[u].z - mean_u, dd = x[u].w - mean_u;
+    q[u] = (a * a + bb * bb) + (cc * cc + dd * dd);
+  }
+  const float m2 = rows8_sum(q, lane);
+  const int m = mb + r0 + 8 * (lane >> 3);
+  if ((lane & 7) == 0 && m < M) e.stats[(long)(n0 >> 8) * e.stats_ld + m] = make_float2(mean_own, m2);
 }
 
 template <DT T, int KIND>
@@ -440,6 +515,9 @@ __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int 
         *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + crosskv_index(e, m, n)) = h;
       }
     }
+    return;
+  } else if constexpr (KIND == EPI_RESID32_LNS || KIND == EPI_GELU_POS32_LNS) {
+    epi_rows64_lns<T, KIND>(e, img, ldt, mb, n0, M, tid, bpre);
     return;
   } else if constexpr (KIND >= 0) {  // specialised launch: the host checked the vector conditions
     epi_rows64<T, KIND>(e, img, ldt, mb, n0, M, N, tid, bpre);
@@ -565,13 +643,24 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   constexpr bool kDirect = kLnf || (WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16));
   const int bcol = kDirect ? (wave & 3) * 64 + 16 * (lane & 3) + 4 * ((lane >> 2) & 3) : 4 * (tid & 63);
   float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f), c14 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (KIND >= 0 && e.bias && n0 + bcol < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
-  if (kLnf && n0 + bcol < N) c14 = *reinterpret_cast<const float4*>(e.c1 + n0 + bcol);
-  float2 lsv[8];
   if constexpr (kLnf) {
-    const int mr = min(m0 + tid, M - 1);
+    // the tile's raw statistics go to LDS by DMA ahead of the ring's first slices (wave g < lng: group g's 256 rows,
+    // two 1 KiB pieces; rows past M clamped, never stored), so the counted vmcnt of the main loop covers them and no
+    // VGPR load is waited for; merged after the loop
+    if (wave < e.lng) {
 #pragma unroll
-    for (int g = 0; g < 8; ++g) lsv[g] = g < e.lng && tid < 256 ? e.stats[(long)g * e.stats_ld + mr] : make_float2(0.f, 0.f);
+      for (int pc = 0; pc < 2; ++pc) {
+        const int mr = min(m0 + 128 * pc + 2 * lane, M - 2);
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(e.stats + (long)wave * e.stats_ld + mr),
+            (__attribute__((address_space(3))) void*)(smem + kG256StatRaw + (wave * 256 + 128 * pc) * 8), 16, 0, 0);
+      }
+    }
+    const int bc = min(n0 + bcol, N - 4);
+    bias4 = *reinterpret_cast<const float4*>(e.bias + bc);
+    c14 = *reinterpret_cast<const float4*>(e.c1 + bc);
+  } else if (KIND >= 0 && e.bias && n0 + bcol < N) {
+    bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
   }
 
   // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
@@ -635,22 +724,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (kLnf) {  // Chan merge of the equal-count (256-column) groups; the epilogue reads it after the loop
-    if (tid < 256) {
-      float mean = 0.f;
-#pragma unroll
-      for (int g = 0; g < 8; ++g) mean += g < e.lng ? lsv[g].x : 0.f;
-      mean /= (float)e.lng;
-      float m2 = 0.f;
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const float dm = lsv[g].x - mean;
-        m2 += g < e.lng ? lsv[g].y + 256.f * dm * dm : 0.f;
-      }
-      reinterpret_cast<float2*>(smem + 4 * kG256Slot)[tid] =
-          make_float2(mean, 1.0f / sqrtf(m2 / (256.f * (float)e.lng) + 1e-5f));
-    }
-  }
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
@@ -699,6 +772,23 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   }
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
+  if constexpr (kLnf) {  // Chan merge of the equal-count (256-column) groups of each of the tile's rows
+    if (tid < 256) {
+      const float2* raw = reinterpret_cast<const float2*>(smem + kG256StatRaw);
+      float mean = 0.f;
+      for (int g = 0; g < e.lng; ++g) mean += raw[g * 256 + tid].x;
+      mean /= (float)e.lng;
+      float m2 = 0.f;
+      for (int g = 0; g < e.lng; ++g) {
+        const float2 v = raw[g * 256 + tid];
+        const float dm = v.x - mean;
+        m2 += v.y + 256.f * dm * dm;
+      }
+      reinterpret_cast<float2*>(smem + kG256StatRow)[tid] =
+          make_float2(mean, 1.0f / sqrtf(m2 / (256.f * (float)e.lng) + 1e-5f));
+    }
+    __syncthreads();
+  }
 #ifdef WMX_G256_STAMPS
   const unsigned long long st1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -724,6 +814,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     {  // every lane takes part in the DPP exchanges; only the stores are guarded
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
+        float4 lsr[2];
+        if constexpr (kLnf) {
+          const float4* l4 = reinterpret_cast<const float4*>(smem + kG256StatRow) + (wm * 128 + i * 16 + fq * 4) / 2;
+          lsr[0] = l4[0];
+          lsr[1] = l4[1];
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * 128 + i * 16 + fq * 4 + r;
@@ -755,7 +851,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
           }
           float4 o;
           if constexpr (kLnf) {
-            const float2 ls = reinterpret_cast<const float2*>(smem + 4 * kG256Slot)[m - m0];
+            const float2 ls = (r & 1) ? make_float2(lsr[r >> 1].z, lsr[r >> 1].w) : make_float2(lsr[r >> 1].x, lsr[r >> 1].y);
             o = make_float4(ls.y * (x0 - ls.x * c14.x) + bias4.x, ls.y * (x1 - ls.x * c14.y) + bias4.y,
                             ls.y * (x2 - ls.x * c14.z) + bias4.z, ls.y * (x3 - ls.x * c14.w) + bias4.w);
           } else {

@@ -17,8 +17,10 @@ enum EpiKind {
   EPI_RESID_STATS = 8,  // x32 = out += acc + bias; out16 = 16-bit(x32); stats[n / 16][m] = (mean, M2) of x32
   EPI_LNFOLD_GELU16 = 9,  // out16 = gelu(rstd_m (acc - mean_m c1[n]) + c2[n]), (mean, rstd) from stats
   // encoder, LayerNorm folded into the projections (gemm256 only, N % 256 == 0 for the producers):
-  EPI_RESID32_LNS = 10,     // EPI_RESID32 + out16 = 16-bit(x32) + stats[n / 256][m] = (mean, M2) of x32's 256 columns
-  EPI_GELU_POS32_LNS = 11,  // EPI_GELU_POS32 + the same out16 / stats
+  // the residual stream is two 16-bit planes, x = out16 (hi = 16-bit(x)) + out (lo = 16-bit(x - hi)): hi is the next
+  // projection's A operand, and the pair keeps ~17 significant bits through the residual adds
+  EPI_RESID32_LNS = 10,     // x = hi + lo + acc + bias -> (hi, lo); stats[n / 256][m] = (mean, M2) of x's 256 columns
+  EPI_GELU_POS32_LNS = 11,  // x = gelu(acc + bias) + pos[m % posT] -> (hi, lo); the same stats
   EPI_LNF_STORE16 = 12,     // out16 = rstd_m (acc - mean_m c1[n]) + bias[n], (mean, rstd) merged from stats[lng][m]
   EPI_LNF_GELU16 = 13,      // out16 = gelu(rstd_m (acc - mean_m c1[n]) + bias[n])
 };
@@ -220,6 +222,9 @@ void launch_logmel(const float* pcm, long stride, const long* lens_dev, const in
 // elementwise / norm / layout
 void launch_layernorm(DT dt, const float* x, const float* g, const float* b, uint16_t* out, int rows, int d,
                       hipStream_t st);
+// LayerNorm of residual rows held as two 16-bit planes x = hi + lo (the encoder fold's residual stream)
+void launch_layernorm_split(DT dt, const uint16_t* xhi, const uint16_t* xlo, const float* g, const float* b,
+                            uint16_t* out, int rows, int d, hipStream_t st);
 void launch_layernorm_rows(DT dt, const float* x, const int* row_idx, const float* g, const float* b, uint16_t* out,
                            int rows, int d, hipStream_t st);
 void launch_im2col_conv1(DT dt, const float* mel, int B, int n_mels, int Kp, uint16_t* out, hipStream_t st);

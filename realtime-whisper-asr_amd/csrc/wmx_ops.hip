@@ -20,17 +20,37 @@ __device__ __forceinline__ void row_load8(const float4* __restrict__ p, int n4, 
     if (i < nit) v[i] = p[min(lane + i * 64, n4 - 1)];
 }
 
+// the encoder fold's residual rows are two 16-bit planes, x = hi + lo (wmx_gemm.hip epi_rows64_lns): XLO != nullptr
+// reads them instead of an fp32 row
 template <DT T>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const int* __restrict__ rows_idx,
                                                         const float* __restrict__ g, const float* __restrict__ bb,
-                                                        uint16_t* __restrict__ out, int rows, int d) {
+                                                        uint16_t* __restrict__ out, int rows, int d,
+                                                        const uint16_t* __restrict__ xlo) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows) return;
   const int src = rows_idx ? rows_idx[row] : row;
   const int n4 = d >> 2, nit = (n4 + 63) >> 6;  // d <= 2048
   float4 v[8], gg[8], be[8];
-  row_load8(reinterpret_cast<const float4*>(x + (long)src * d), n4, lane, v);
+  if (xlo) {
+    const u16x4* ph = reinterpret_cast<const u16x4*>(reinterpret_cast<const uint16_t*>(x) + (long)src * d);
+    const u16x4* pl = reinterpret_cast<const u16x4*>(xlo + (long)src * d);
+    u16x4 h[8], l[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < nit) {
+        h[i] = ph[min(lane + i * 64, n4 - 1)];
+        l[i] = pl[min(lane + i * 64, n4 - 1)];
+      }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i < nit)
+        v[i] = make_float4(to_f32<T>(h[i][0]) + to_f32<T>(l[i][0]), to_f32<T>(h[i][1]) + to_f32<T>(l[i][1]),
+                           to_f32<T>(h[i][2]) + to_f32<T>(l[i][2]), to_f32<T>(h[i][3]) + to_f32<T>(l[i][3]));
+  } else {
+    row_load8(reinterpret_cast<const float4*>(x + (long)src * d), n4, lane, v);
+  }
   row_load8(reinterpret_cast<const float4*>(g), n4, lane, gg);
   row_load8(reinterpret_cast<const float4*>(bb), n4, lane, be);
   float s = 0.f;
@@ -68,9 +88,22 @@ void launch_layernorm_rows(DT dt, const float* x, const int* rows_idx, const flo
   WMX_CHECK(d % 4 == 0 && d <= 2048, "layernorm: d");
   dim3 grid(cdiv(rows, 4));
   if (dt == DT::BF16)
-    hipLaunchKernelGGL(layernorm_kernel<DT::BF16>, grid, dim3(256), 0, st, x, rows_idx, g, b, out, rows, d);
+    hipLaunchKernelGGL(layernorm_kernel<DT::BF16>, grid, dim3(256), 0, st, x, rows_idx, g, b, out, rows, d, nullptr);
   else
-    hipLaunchKernelGGL(layernorm_kernel<DT::F16>, grid, dim3(256), 0, st, x, rows_idx, g, b, out, rows, d);
+    hipLaunchKernelGGL(layernorm_kernel<DT::F16>, grid, dim3(256), 0, st, x, rows_idx, g, b, out, rows, d, nullptr);
+  WMX_HIP(hipGetLastError());
+}
+
+void launch_layernorm_split(DT dt, const uint16_t* xhi, const uint16_t* xlo, const float* g, const float* b,
+                            uint16_t* out, int rows, int d, hipStream_t st) {
+  if (rows <= 0) return;
+  WMX_CHECK(d % 4 == 0 && d <= 2048, "layernorm: d");
+  const float* x = reinterpret_cast<const float*>(xhi);
+  dim3 grid(cdiv(rows, 4));
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(layernorm_kernel<DT::BF16>, grid, dim3(256), 0, st, x, nullptr, g, b, out, rows, d, xlo);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<DT::F16>, grid, dim3(256), 0, st, x, nullptr, g, b, out, rows, d, xlo);
   WMX_HIP(hipGetLastError());
 }
 

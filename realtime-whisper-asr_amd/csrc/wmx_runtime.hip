@@ -926,12 +926,13 @@ static void encode_layers_mx8(Ctx& c, int B) {
   }
 }
 
-// encoder pass on the 256 x 256 GEMM with the LayerNorms folded (Model::enc_fold): the residual producers (conv2,
-// out-proj, fc2) leave x in fp32, its 16-bit copy in ehb and the row statistics per 256 columns in est; qkv and fc1
-// multiply the 16-bit x by W diag(g) and finish LN in their epilogue, rstd (acc - mean c1) + c2 (wmx_gemm.hip).
-// No LayerNorm launches inside the stack; the final one (ln_post) stays.  Numerics: x enters the projections
-// rounded to 16 bits before the mean is removed, which adds ~2^-9 |mean| / std relative error per projection input
-// on top of the unfolded form's LN-output rounding ("Encoder LayerNorm fold").
+// encoder pass on the 256 x 256 GEMM with the LayerNorms folded (Model::enc_fold): the residual stream is two 16-bit
+// planes x = hi + lo (hi in ehb, lo in ex's storage; ~17 significant bits, the fp32 row's bytes), which the residual
+// producers (conv2, out-proj, fc2) update together with the row statistics per 256 columns (est); qkv and fc1
+// multiply hi by W diag(g) and finish LN in their epilogue, rstd (acc - mean c1) + c2 (wmx_gemm.hip).  No LayerNorm
+// launches inside the stack; the final one (ln_post) reads the planes.  Numerics: x enters the projections rounded
+// to 16 bits before the mean is removed, which adds ~2^-9 |mean| / std relative error per projection input on top of
+// the unfolded form's LN-output rounding ("Encoder LayerNorm fold").
 static bool enc_fold_rows(const Ctx& c, long rows) {
   static const bool no_g256 = getenv("WMX_NO_G256") != nullptr;
   return c.m->enc_fold && c.est && rows >= 4096 && !no_g256;  // the gemm256 dispatch condition of gemm()
@@ -973,7 +974,6 @@ static void encode(Ctx& c, int B) {
   }
   for (size_t l = 0; l < m.enc.size(); ++l) {
     const EncLayer& L = m.enc[l];
-    const bool last = l + 1 == m.enc.size();
     if (fold) {
       gemm(c, c.ehb, da, L.fqkv, da, (int)rows, 3 * da, da,
            epi_lnf(c, EPI_LNF_STORE16, L.c1qkv, L.c2qkv, c.eqkv, 3 * da, rows));
@@ -999,8 +999,7 @@ static void encode(Ctx& c, int B) {
       gemm(c, c.eao, da, L.wo, da, (int)rows, da, da, epi_lns(c, EPI_RESID32_LNS, L.bo, rows));
       gemm(c, c.ehb, da, L.ffc1, da, (int)rows, 4 * da, da,
            epi_lnf(c, EPI_LNF_GELU16, L.c1fc1, L.c2fc1, c.ef1, 4 * da, rows));
-      gemm(c, c.ef1, 4 * da, L.wfc2, 4 * da, (int)rows, da, 4 * da,
-           last ? epi(EPI_RESID32, L.bfc2, c.ex, da) : epi_lns(c, EPI_RESID32_LNS, L.bfc2, rows));
+      gemm(c, c.ef1, 4 * da, L.wfc2, 4 * da, (int)rows, da, 4 * da, epi_lns(c, EPI_RESID32_LNS, L.bfc2, rows));
     } else {
       gemm(c, c.eao, da, L.wo, da, (int)rows, da, da, epi(EPI_RESID32, L.bo, c.ex, da));
       launch_layernorm(c.dt, c.ex, L.ln2g, L.ln2b, c.ehb, (int)rows, da, c.st);
@@ -1008,7 +1007,11 @@ static void encode(Ctx& c, int B) {
       gemm(c, c.ef1, 4 * da, L.wfc2, 4 * da, (int)rows, da, 4 * da, epi(EPI_RESID32, L.bfc2, c.ex, da));
     }
   }
-  launch_layernorm(c.dt, c.ex, m.lnpg, m.lnpb, c.enc_out, (int)rows, da, c.st);
+  if (fold)
+    launch_layernorm_split(c.dt, c.ehb, reinterpret_cast<const uint16_t*>(c.ex), m.lnpg, m.lnpb, c.enc_out, (int)rows,
+                           da, c.st);
+  else
+    launch_layernorm(c.dt, c.ex, m.lnpg, m.lnpb, c.enc_out, (int)rows, da, c.st);
 }
 
 // layer l's cross K / V in the head-major layout written by EPI_CROSSKV
