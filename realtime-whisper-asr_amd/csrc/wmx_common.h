@@ -118,6 +118,29 @@ __device__ __forceinline__ int load_uniform_i32(const int* p) {
   return *(cint4*)p;
 }
 
+// the same GELU on two values with packed f32 math (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth per issue, for
+// epilogues that run outside any MFMA shadow); the transcendental and select steps stay per element
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ inline f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 ax = __builtin_elementwise_abs(x);
+  const f32x2 d = __builtin_elementwise_fma(ax, f32x2{0.3275911f * 0.70710678118654752f, 0.3275911f * 0.70710678118654752f},
+                                            f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = __builtin_elementwise_fma(f32x2{0.5f * 1.061405429f, 0.5f * 1.061405429f}, t,
+                                      f32x2{0.5f * -1.453152027f, 0.5f * -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * 1.421413741f, 0.5f * 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * -0.284496736f, 0.5f * -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * 0.254829592f, 0.5f * 0.254829592f});
+  const f32x2 e2 = x * (x * f32x2{-0.72134752044448170f, -0.72134752044448170f});
+  const f32x2 q = p * t * f32x2{__builtin_amdgcn_exp2f(e2.x), __builtin_amdgcn_exp2f(e2.y)};
+  const f32x2 phi = {x.x >= 0.f ? 1.0f - q.x : q.x, x.y >= 0.f ? 1.0f - q.y : q.y};
+  return x * phi;
+}
+__device__ inline float4 gelu_erf4(float4 v) {
+  const f32x2 a = gelu_erf2(f32x2{v.x, v.y}), b = gelu_erf2(f32x2{v.z, v.w});
+  return make_float4(a.x, a.y, b.x, b.y);
+}
+
 __device__ inline float gelu_erf(float x) {
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, fabsf(x), 1.0f));
   float p = fmaf(0.5f * 1.061405429f, t, 0.5f * -1.453152027f);

@@ -317,6 +317,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
 constexpr int kG256Stamps = 16384;
 __device__ unsigned long long g256_stamps[kG256Stamps][3];
 #endif
+#ifndef WMX_G256_PHASES
+#define WMX_G256_PHASES 2  // barrier-separated MFMA segments per 32-deep slice (1: one 32-MFMA segment per slice)
+#endif
 #ifndef WMX_G256_DIRECT
 #define WMX_G256_DIRECT 1  // LDS-free epilogue for the bf16-output kinds (0: the LDS-image epilogue for all)
 #endif
@@ -360,9 +363,31 @@ __device__ inline void epi_from_image(const Epi& e, const float* img, int ldt, i
 // fast form of epi_from_image for a 64-row x 256-column image and 512 threads: a thread owns one column quad
 // and rows r0, r0 + 8, ... (r0 = tid / 64): the bias is loaded once, and every row's loads (image, residual,
 // position) are issued before its stores, so the store tail is not a chain of dependent global round trips.
+// the residual rows of one 64-row epilogue round of the 256-column image (thread: column quad (tid & 63), rows
+// (tid >> 6) + 8u), loaded one round ahead so the RMW epilogues (fp32 / hi-lo residual) do not wait one memory
+// round trip per round; rows past M are clamped (their results are not stored)
+struct Resid8 {
+  float4 f[8];
+  u16x4 h[8], l[8];
+};
+template <int KIND>
+__device__ inline void resid_load(Resid8& R, const Epi& e, int mb, int n0, int M, int tid) {
+  const int n = n0 + (tid & 63) * 4, r0 = tid >> 6;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const long mm = min(mb + r0 + 8 * u, M - 1);
+    if (KIND == EPI_RESID32) {
+      R.f[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + mm * e.ldc + n);
+    } else {
+      R.h[u] = *reinterpret_cast<const u16x4*>(e.out16 + mm * e.ldc + n);
+      R.l[u] = *reinterpret_cast<const u16x4*>(reinterpret_cast<const uint16_t*>(e.out) + mm * e.ldc + n);
+    }
+  }
+}
+
 template <DT T, int KIND>
 __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
-                                  const float4* bpre = nullptr) {
+                                  const float4* bpre = nullptr, const Resid8* pre = nullptr) {
   constexpr int KD = KIND;
   const int c4 = (tid & 63) * 4, r0 = tid >> 6;
   const int n = n0 + c4;
@@ -378,7 +403,9 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
     const int row = r0 + 8 * u, m = mb + row;
     v[u] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
     v[u] = make_float4(v[u].x + b.x, v[u].y + b.y, v[u].z + b.z, v[u].w + b.w);
-    if (KD == EPI_RESID32 && m < M)
+    if (KD == EPI_RESID32 && pre)
+      aux[u] = pre->f[u];
+    else if (KD == EPI_RESID32 && m < M)
       aux[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
     if (KD == EPI_GELU_POS32 && m < M)
       aux[u] = *reinterpret_cast<const float4*>(e.pos + (long)(m % e.posT) * e.ldc + n);
@@ -388,8 +415,7 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
     const int m = mb + r0 + 8 * u;
     if (m >= M) continue;
     float4 x = v[u];
-    if (KD == EPI_GELU16 || KD == EPI_GELU_POS32 || KD == EPI_GELU_MX8)
-      x = make_float4(gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w));
+    if (KD == EPI_GELU16 || KD == EPI_GELU_POS32 || KD == EPI_GELU_MX8) x = gelu_erf4(x);
     if (KD == EPI_RESID32 || KD == EPI_GELU_POS32)
       x = make_float4(x.x + aux[u].x, x.y + aux[u].y, x.z + aux[u].z, x.w + aux[u].w);
     if (KD == EPI_GELU_MX8) {
@@ -438,7 +464,7 @@ __device__ inline float rows8_sum(const float (&v)[8], int lane) {
 // (mean, M2) over its 256 columns goes to stats[n0 / 256][m] (Chan's pairwise form; two rows8_sum passes).
 template <DT T, int KIND>
 __device__ inline void epi_rows64_lns(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int tid,
-                                      const float4* bpre) {
+                                      const float4* bpre, const Resid8* pre) {
   const int lane = tid & 63, c4 = lane * 4, r0 = tid >> 6;
   const int n = n0 + c4;
   const float4 b = *bpre;
@@ -453,8 +479,8 @@ __device__ inline void epi_rows64_lns(const Epi& e, const float* img, int ldt, i
     x[u] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
     x[u] = make_float4(x[u].x + b.x, x[u].y + b.y, x[u].z + b.z, x[u].w + b.w);
     if (KIND == EPI_RESID32_LNS) {
-      ah[u] = *reinterpret_cast<const u16x4*>(hi + (long)mm * e.ldc + n);
-      al[u] = *reinterpret_cast<const u16x4*>(lo + (long)mm * e.ldc + n);
+      ah[u] = pre->h[u];
+      al[u] = pre->l[u];
     } else {
       pp[u] = *reinterpret_cast<const float4*>(e.pos + (long)(mm % e.posT) * e.ldc + n);
     }
@@ -470,8 +496,8 @@ __device__ inline void epi_rows64_lns(const Epi& e, const float* img, int ldt, i
       v.z += to_f32<T>(ah[u][2]) + to_f32<T>(al[u][2]);
       v.w += to_f32<T>(ah[u][3]) + to_f32<T>(al[u][3]);
     } else {
-      v = make_float4(gelu_erf(v.x) + pp[u].x, gelu_erf(v.y) + pp[u].y, gelu_erf(v.z) + pp[u].z,
-                      gelu_erf(v.w) + pp[u].w);
+      v = gelu_erf4(v);
+      v = make_float4(v.x + pp[u].x, v.y + pp[u].y, v.z + pp[u].z, v.w + pp[u].w);
     }
     x[u] = v;
     const u16x4 h = {from_f32<T>(v.x), from_f32<T>(v.y), from_f32<T>(v.z), from_f32<T>(v.w)};
@@ -498,7 +524,7 @@ __device__ inline void epi_rows64_lns(const Epi& e, const float* img, int ldt, i
 
 template <DT T, int KIND>
 __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
-                                   const float4* bpre = nullptr) {
+                                   const float4* bpre = nullptr, const Resid8* pre = nullptr) {
   if constexpr (KIND == EPI_CROSSKV) {  // specialised cross-K/V launch (host: d % 256 == 0, xt % 4 == 0)
     if (((n0 / e.d) & 1) == 0) {
       epi_rows64<T, EPI_CROSSKV>(e, img, ldt, mb, n0, M, N, tid, bpre);
@@ -517,10 +543,10 @@ __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int 
     }
     return;
   } else if constexpr (KIND == EPI_RESID32_LNS || KIND == EPI_GELU_POS32_LNS) {
-    epi_rows64_lns<T, KIND>(e, img, ldt, mb, n0, M, tid, bpre);
+    epi_rows64_lns<T, KIND>(e, img, ldt, mb, n0, M, tid, bpre, pre);
     return;
   } else if constexpr (KIND >= 0) {  // specialised launch: the host checked the vector conditions
-    epi_rows64<T, KIND>(e, img, ldt, mb, n0, M, N, tid, bpre);
+    epi_rows64<T, KIND>(e, img, ldt, mb, n0, M, N, tid, bpre, pre);
     return;
   }
   const bool vec = (N & 3) == 0 && (e.ldc & 3) == 0;
@@ -572,7 +598,7 @@ __device__ inline void epi_rows64_n128(const Epi& e, const float* img, int ldt, 
     if (m >= M) continue;  // uniform over each 32-lane half (same row)
     float4 x = v[u];
     if (KIND == EPI_GELU_MX8) {
-      x = make_float4(gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w));
+      x = gelu_erf4(x);
       const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)))));
       const float is = mx8_inv_scale(ex);
       *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(e.out) + (long)m * e.ldc + n) =
@@ -727,6 +753,36 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
+#if WMX_G256_PHASES == 1
+  // one phase per slice: [12 ds_reads (A 0..7, B 0..3) + the 4 DMAs of slice t + 3 + counted wait for t + 1]
+  // s_barrier [32 MFMAs] s_barrier; waves 4..7 one barrier behind, as in the two-phase form
+  u16x8 af[8], bfr[4];
+  for (int t = 0; t < nk; ++t) {
+    const char* S = smem + (t & 3) * kG256Slot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const u16x8*>(S + boff + j * 1024);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + i * 1024);
+    if (t + 3 < nk) issue(t + 3);
+    if (t + 3 < nk)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (t + 2 < nk)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+#else
   u16x8 af[4], bfr[4];
   for (int t = 0; t < nk; ++t) {
     const char* S = smem + (t & 3) * kG256Slot;
@@ -770,6 +826,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
+#endif
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
   if constexpr (kLnf) {  // Chan merge of the equal-count (256-column) groups of each of the tile's rows
@@ -857,7 +914,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
           } else {
             o = make_float4(x0 + bias4.x, x1 + bias4.y, x2 + bias4.z, x3 + bias4.w);
           }
-          if (kGelu) o = make_float4(gelu_erf(o.x), gelu_erf(o.y), gelu_erf(o.z), gelu_erf(o.w));
+          if (kGelu) o = gelu_erf4(o);  // packed: the epilogue runs outside the MFMA shadow
           if (m < M && n < N) {
             const u16x4 h = {from_f32<T>(o.x), from_f32<T>(o.y), from_f32<T>(o.z), from_f32<T>(o.w)};
             *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
@@ -875,9 +932,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     __syncthreads();  // the next tile's DMA must not overwrite the ring before every wave left this tile
     continue;
   }
-  // epilogue: 4 rounds of 64 rows through an fp32 LDS image [64][BN + 4]
+  // epilogue: 4 rounds of 64 rows through an fp32 LDS image [64][BN + 4]; the residual-RMW kinds load the next
+  // round's residual rows while this round runs
   constexpr int LDT = BN + 4;
+  constexpr bool kPre = KIND == EPI_RESID32 || KIND == EPI_RESID32_LNS;
   float* img = reinterpret_cast<float*>(smem);
+  Resid8 pre;  // one buffer: round rd + 1's rows are requested as soon as round rd has consumed its own (double
+              // buffering spilled: the prologue's reloads drained the DMA pipeline with vmcnt(0))
+  if constexpr (kPre) resid_load<KIND>(pre, e, m0, n0, M, tid);
 #pragma unroll
   for (int rd = 0; rd < 4; ++rd) {
     if (wm == (rd >> 1)) {
@@ -891,7 +953,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
       }
     }
     __syncthreads();
-    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
+    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4, kPre ? &pre : nullptr);
+    if constexpr (kPre) {
+      if (rd < 3) resid_load<KIND>(pre, e, m0 + (rd + 1) * 64, n0, M, tid);
+    }
     __syncthreads();
   }
 #ifdef WMX_G256_STAMPS  // diagnostic build only (tools/mb_gemm256 -DWMX_G256_STAMPS): per-tile phase clocks
