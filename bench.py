@@ -484,7 +484,8 @@ def main():
                       "spectra, power and filterbank in LDS; HBM would allow ~2 us per window"}
     # encoder MFMA utilisation (north_star: >= 40 % in the encoder): one whole encoder pass over a context's
     # windows, isolated (HIP events), and the in-situ encoder stage of the timed region (all groups concurrent)
-    e_ms, _, e_fl = ctx.bench_kernel("encoder", Bg, iters=3)
+    # best of three 3-pass averages (the clock the chip holds after the decode-heavy timed region varies by a few %)
+    e_ms, _, e_fl = min(ctx.bench_kernel("encoder", Bg, iters=3) for _ in range(3))
     e_tf = e_fl / (e_ms * 1e-3) / 1e12
     insitu_tf = G * e_fl / (stages[1] * 1e-3) / 1e12 if stages[1] > 0 else None
     # the same pass over the whole per-GPU batch (B windows in one launch sequence), in a scratch context
@@ -492,7 +493,7 @@ def main():
     if G > 1:
         scratch = engine.Context(model, max_batch=B, beam_size=1, max_new_tokens=8, word_timestamps=False,
                                  use_graph=False)
-        e_ms_b, _, e_fl_b = scratch.bench_kernel("encoder", B, iters=3)
+        e_ms_b, _, e_fl_b = min(scratch.bench_kernel("encoder", B, iters=3) for _ in range(3))
         scratch.close()
     e_tf_b = e_fl_b / (e_ms_b * 1e-3) / 1e12
     encoder = {"windows": Bg, "gflop_per_window": round(e_fl / Bg / 1e9, 1), "isolated_ms": round(e_ms, 2),
@@ -503,6 +504,7 @@ def main():
                "insitu_tflops": round(insitu_tf, 1) if insitu_tf else None,
                "insitu_mfma_util": round(insitu_tf / MFMA_BF16_PEAK_TFLOPS, 4) if insitu_tf else None,
                "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
+               "timing": "isolated: HIP events, best of three 3-pass averages after one warm pass",
                "note": ("fp8: the projections run on the MX-fp8 MFMA (5 PF dense peak), attention and convs bf16; "
                         "utilisation quoted against the bf16 peak" if args.dtype == "fp8" else "bf16 MFMA")}
     log(f"[rank {rank}] encoder: {encoder}")
