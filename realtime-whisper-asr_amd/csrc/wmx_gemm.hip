@@ -327,6 +327,29 @@ constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
 // 128 KiB ring + the LayerNorm-folded kinds' raw row statistics [8 groups][256 rows] float2 and merged (mean, rstd)
 constexpr int kG256StatRaw = 4 * kG256Slot, kG256StatRow = kG256StatRaw + 8 * 256 * 8;
 constexpr int kG256Lds = kG256StatRow + 256 * 8;
+#ifndef WMX_G256_SLOTS
+#define WMX_G256_SLOTS 4  // ring slots of the kinds without the LayerNorm-folded statistics (4 or 5: 160 KiB)
+#endif
+template <int KIND>
+constexpr bool g256_lnf() { return KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GELU16; }
+template <int KIND>
+constexpr int g256_slots() { return (g256_lnf<KIND>() || WMX_G256_PHASES == 1) ? 4 : WMX_G256_SLOTS; }
+template <int KIND>
+constexpr int g256_lds() { return g256_lnf<KIND>() ? kG256Lds : g256_slots<KIND>() * kG256Slot; }
+static_assert(5 * kG256Slot <= 163840 && kG256Lds <= 163840, "gemm256 LDS");
+// s_waitcnt vmcnt(n) for a runtime n in {0, 2, ..., 14} (uniform): the count must be an immediate
+__device__ inline void vmcnt_even(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+  }
+}
 
 // apply the epilogue to `rows` rows of an fp32 LDS image [rows][ldt] holding output rows mb.. and columns n0..n0+BN
 template <DT T, int BN, int NT>
@@ -658,6 +681,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int nk = K >> 5;
+  constexpr int NS = g256_slots<KIND>();  // ring slots: NS - 1 slices in flight ahead of the one being read
   // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias, loaded now so its latency hides behind
   // the main loop (the epilogue's column quads are the same in all four rounds)
   // (direct epilogue kinds: the lane's column quad after the in-quad transpose, wn 64 + 16 (fr & 3) + 4 (fr >> 2))
@@ -708,7 +732,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
 #if WMX_G256_MODE == 2
     return;
 #endif
-    char* slot = smem + (kt & 3) * kG256Slot;
+    char* slot = smem + (kt % NS) * kG256Slot;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int j = 2 * h + jj;
@@ -741,15 +765,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   //                       lagging half's last reads of slice t-1 are done before the leading half restages it)
   //   phase B of slice t: wait (counted vmcnt) for slice t + 1; ds_read A frags 4..7; issue the W half of t + 3
   // The wait in phase B of slice t precedes, by at least one barrier, every wave's first read of slice t + 1.
-  issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 2) issue(2);
-  if (nk > 2)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (nk > 1)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < nk) issue(q);
+  vmcnt_even(4 * (min(nk, NS - 1) - 1));  // slice 0 landed (every younger slice may still fly)
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
@@ -757,6 +776,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   // one phase per slice: [12 ds_reads (A 0..7, B 0..3) + the 4 DMAs of slice t + 3 + counted wait for t + 1]
   // s_barrier [32 MFMAs] s_barrier; waves 4..7 one barrier behind, as in the two-phase form
   u16x8 af[8], bfr[4];
+  static_assert(NS == 4, "one-phase loop: 4 slots");
   for (int t = 0; t < nk; ++t) {
     const char* S = smem + (t & 3) * kG256Slot;
 #pragma unroll
@@ -785,13 +805,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
 #else
   u16x8 af[4], bfr[4];
   for (int t = 0; t < nk; ++t) {
-    const char* S = smem + (t & 3) * kG256Slot;
+    const char* S = smem + (t % NS) * kG256Slot;
     // ---- phase A ----
 #pragma unroll
     for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const u16x8*>(S + boff + j * 1024);
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + i * 1024);
-    if (t + 3 < nk) issue_half(t + 3, 0);
+    if (t + NS - 1 < nk) issue_half(t + NS - 1, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -804,16 +824,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     // ---- phase B ----
-    // slice t + 1 is complete once only slice t + 2 (4 DMAs) and the first half of t + 3 (2) may be outstanding
-    if (t + 3 < nk)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (t + 2 < nk)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // slice t + 1 is complete once only slices t + 2 .. t + NS - 2 (4 DMAs each) and the first half of t + NS - 1 (2)
+    // may be outstanding
+    vmcnt_even(4 * max(0, min(nk - 1, t + NS - 2) - (t + 1)) + (t + NS - 1 < nk ? 2 : 0));
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + (i + 4) * 1024);
-    if (t + 3 < nk) issue_half(t + 3, 1);
+    if (t + NS - 1 < nk) issue_half(t + NS - 1, 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -2074,7 +2090,7 @@ static void launch_cfg(const GemmCall& g, hipStream_t st) {
 template <DT T, int KIND>
 static void g256_attr_one() {
   WMX_HIP(hipFuncSetAttribute((const void*)gemm256_kernel<T, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kG256Lds));
+                              g256_lds<KIND>()));
 }
 template <DT T>
 static void g256_attr() {
@@ -2111,7 +2127,7 @@ static void launch_g256(const GemmCall& g, hipStream_t st) {
   const bool vec = (g.N & 3) == 0 && (g.epi.ldc & 3) == 0;
   const int kind = (vec || g.epi.kind == EPI_CROSSKV) ? g.epi.kind : -1;
 #define WMX_G256_LAUNCH(KD)                                                                                    \
-  hipLaunchKernelGGL((gemm256_kernel<T, KD>), dim3(tiles), dim3(512), kG256Lds, st, g.A, g.lda, g.W, g.ldw, g.M, \
+  hipLaunchKernelGGL((gemm256_kernel<T, KD>), dim3(tiles), dim3(512), g256_lds<KD>(), st, g.A, g.lda, g.W, g.ldw, g.M, \
                      g.N, g.K, g.epi)
   switch (kind) {
     case EPI_STORE16: WMX_G256_LAUNCH(EPI_STORE16); break;
