@@ -1,6 +1,6 @@
 """Kernel time of the stage that follows the decode loop (word alignment), per queue, from a rocprofv3
 --kernel-trace CSV: for every queue, the kernels after the last decode-step kernel (`embed_ln_kernel`) of each
-transcribe call up to the next `logmel_raw_kernel`, summed by kernel name (tuning aid).
+transcribe call up to the next `logmel_finalize_kernel`, summed by kernel name (tuning aid).
 
   python tools/stage_kernels.py <run_kernel_trace.csv>"""
 import collections
@@ -26,7 +26,7 @@ def main():
         while i < n:
             # find next logmel or end
             j = i
-            while j < n and "logmel_raw" not in ks[j][2]:
+            while j < n and "logmel_finalize" not in ks[j][2]:
                 j += 1
             last = max((k for k in range(i, j) if "embed_ln" in ks[k][2]), default=None)
             if last is not None:
