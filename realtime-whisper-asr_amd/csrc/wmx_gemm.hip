@@ -1183,10 +1183,240 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
   }  // tile loop
 }
 
+// ------------------------------------------------------------------------------------------------
+// MX-fp8 GEMM, 256 x 256 tile (the gemm256 structure at the fp8 rate): v_mfma_scale_f32_32x32x64_f8f6f4 takes K = 64
+// per instruction, so a 64-deep slice is 64 bytes of e4m3 per row -- the same 32 KiB slot, 1 KiB pieces and
+// source-side swizzle as the bf16 ring -- plus the slice's two e8m0 scale bytes per row (A then W, 1 KiB, staged
+// by one dword-per-lane DMA per wave: the dword holding this slice's two bytes).  8 waves (2 M x 4 N), wave tile 128 x 64 = 4 x 2 blocks of 32 x 32 (f32x16
+// accumulators), two phases per slice of 4 MFMAs (64 cycles each) with the ping-pong stagger of gemm256, 4 slots.
+// Fragment of 32 rows: lane l holds row (l & 31), k = 16g .. 16g + 15 in bytes 0..15 and 32 + 16g .. in bytes
+// 16..31 (g = l >> 5), i.e. 16-B pieces g and 2 + g of its 64-B row; its scale operand is the byte of (row l & 31,
+// 32-k block g) (tools/mx8_check32.hip measures both maps).  Epilogues through the 64 x 256 fp32 LDS image.
+// ------------------------------------------------------------------------------------------------
+constexpr int kMx8bSlot = 512 * 64 + 512 * 4;  // 256 A + 256 W rows x 64 B, + the scale dword of each row
+constexpr int kMx8bNS = 4;
+constexpr int kMx8bLds = kMx8bNS * kMx8bSlot;  // 132 KiB
+static_assert(kMx8bLds <= 163840 && 64 * (256 + 4) * 4 <= kMx8bLds, "gemm_mx8_256 LDS");
+// s_waitcnt vmcnt(n), n in 0..15 (uniform)
+__device__ inline void vmcnt_upto15(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
+
+template <DT T, int KIND>
+__global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __restrict__ A, long lda,
+                                                              const uint8_t* __restrict__ AS, long ldas,
+                                                              const uint8_t* __restrict__ W, long ldw,
+                                                              const uint8_t* __restrict__ WS, long ldws, int M, int N,
+                                                              int K, Epi e) {
+  constexpr int BM = 256, BN = 256, NS = kMx8bNS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tilesN = (N + BN - 1) / BN;
+  const int tilesM = (M + BM - 1) / BM;
+  const int nwg = tilesN * tilesM;
+  for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
+  int bid = tile;
+  {  // bijective XCD remap, then 4 row panels walk the columns together (as gemm256)
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  constexpr int GM = 4;
+  const int gsz = GM * tilesN;
+  const int grp = bid / gsz, gr = bid - grp * gsz;
+  const int gm = min(GM, tilesM - grp * GM);
+  const int tm = grp * GM + gr % gm, tn = gr / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nk = K >> 6;
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e.bias && n0 + 4 * (tid & 63) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (tid & 63));
+
+  // staging as gemm256: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 A rows, 16..31 W rows; wave w
+  // issues pieces w, w + 8 (A) and w + 16, w + 24 (W); lane l: row l >> 2, 16-B column (l & 3) swizzled at the source
+  const int srow = lane >> 2;
+  const int scol = ((lane & 3) ^ ((-(srow >> 2)) & 3)) * 16;
+  const uint8_t* src[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int pc = wave + 8 * j;
+    src[j] = pc < 16 ? A + (long)min(m0 + pc * 16 + srow, M - 1) * lda + scol
+                     : W + (long)min(n0 + (pc - 16) * 16 + srow, N - 1) * ldw + scol;
+  }
+  // scales: wave w < 4 stages A rows 64 w + lane, wave w >= 4 W rows 64 (w - 4) + lane: the dword (kt / 2) of the row's
+  // e8m0 bytes, which holds slice kt's two 32-k blocks at bytes 2 (kt & 1), + 1 (rows are 4-B aligned: K % 128 == 0)
+  const uint8_t* ssrc = wave < 4 ? AS + (long)min(m0 + 64 * wave + lane, M - 1) * ldas
+                                 : WS + (long)min(n0 + 64 * (wave - 4) + lane, N - 1) * ldws;
+  const int sdst = 512 * 64 + wave * 256;
+  auto issue_half = [&](int kt, int h) {
+    char* slot = smem + (kt % NS) * kMx8bSlot;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * h + jj;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + kt * 64),
+                                       (__attribute__((address_space(3))) void*)(slot + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    }
+    if (h == 0)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc + (kt >> 1) * 4),
+                                       (__attribute__((address_space(3))) void*)(slot + sdst), 4, 0, 0);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int fr = lane & 31, g = lane >> 5;
+  // 16-B pieces g and 2 + g of the lane's row, at their swizzled LDS positions (p ^ sw(row), sw = (-(row >> 2)) & 3;
+  // every fragment row offset below is a multiple of 32, so sw depends on fr only)
+  const int sw = (-(fr >> 2)) & 3;
+  const int p0 = (g ^ sw) << 4, p1 = ((2 + g) ^ sw) << 4;
+  const int arow = wm * 128 + fr, brow = 256 + wn * 64 + fr;  // brow: W rows follow the 256 A rows in the slot
+  auto frag = [&](const char* S, int row) {
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(S + row * 64 + p0);
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(S + row * 64 + p1);
+    return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto scale = [&](const char* S, int row, int kt) {
+    return (int)*reinterpret_cast<const uint8_t*>(S + 512 * 64 + row * 4 + 2 * (kt & 1) + g);
+  };
+
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q)
+    if (q < nk) {
+      issue_half(q, 0);
+      issue_half(q, 1);
+    }
+  vmcnt_upto15(5 * (min(nk, NS - 1) - 1));  // slice 0 landed
+  __builtin_amdgcn_s_barrier();
+  const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  if (lagging) __builtin_amdgcn_s_barrier();
+  i32x8 af[2], bfr[2];
+  int sa[2], sb[2];
+  for (int t = 0; t < nk; ++t) {
+    const char* S = smem + (t % NS) * kMx8bSlot;
+    // ---- phase A: B blocks 0, 1 and A blocks 0, 1; the A half (+ scales) of slice t + NS - 1 ----
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bfr[j] = frag(S, brow + 32 * j);
+      sb[j] = scale(S, brow + 32 * j, t);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      af[i] = frag(S, arow + 32 * i);
+      sa[i] = scale(S, arow + 32 * i, t);
+    }
+    if (t + NS - 1 < nk) issue_half(t + NS - 1, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sa[i], 0, sb[j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase B: slice t + 1 complete once only slices t + 2 .. t + NS - 2 (5 DMAs each) and the A half of
+    // t + NS - 1 (3) may be outstanding; A blocks 2, 3; the W half of t + NS - 1 ----
+    vmcnt_upto15(5 * max(0, min(nk - 1, t + NS - 2) - (t + 1)) + (t + NS - 1 < nk ? 3 : 0));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      af[i] = frag(S, arow + 64 + 32 * i);
+      sa[i] = scale(S, arow + 64 + 32 * i, t);
+    }
+    if (t + NS - 1 < nk) issue_half(t + NS - 1, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i + 2][j] =
+            __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[i], bfr[j], acc[i + 2][j], 0, 0, 0, sa[i], 0, sb[j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (!lagging) __builtin_amdgcn_s_barrier();
+  __syncthreads();
+
+  // epilogue: 4 rounds of 64 rows through the fp32 LDS image [64][BN + 4]; 32 x 32 block (i, j) register r of lane l
+  // is row 32 i + 8 (r / 4) + 4 (l / 32) + r % 4, column 32 j + l % 32 of the wave tile
+  constexpr int LDT = BN + 4;
+  constexpr bool kPre = false;  // (the residual prefetch spilled here: 256 VGPRs with the f32x16 accumulators)
+  float* img = reinterpret_cast<float*>(smem);
+  Resid8 pre;
+  if constexpr (kPre) resid_load<KIND>(pre, e, m0, n0, M, tid);
+#pragma unroll
+  for (int rd = 0; rd < 4; ++rd) {
+    if (wm == (rd >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = (rd & 1) * 2 + ii;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            img[(ii * 32 + 8 * (r >> 2) + 4 * g + (r & 3)) * LDT + wn * 64 + j * 32 + fr] = acc[i][j][r];
+      }
+    }
+    __syncthreads();
+    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4, kPre ? &pre : nullptr);
+    if constexpr (kPre) {
+      if (rd < 3) resid_load<KIND>(pre, e, m0 + (rd + 1) * 64, n0, M, tid);
+    }
+    __syncthreads();
+  }
+  }  // tile loop
+}
+
 static int g256_grid(int tiles);
+
+// the 256 x 256 / 32x32x64 form for the encoder shapes (WMX_MX8_256=0: the 256 x 128 / 16x16x128 form everywhere)
+static bool mx8_256_ok(const Mx8Call& g) {
+  static const bool off = getenv("WMX_MX8_256") && atoi(getenv("WMX_MX8_256")) == 0;
+  return !off && g.M >= 4096 && g.N % 256 == 0 && g.K % 64 == 0 && g.ldas % 2 == 0 && g.ldws % 2 == 0 &&
+         (g.epi.kind == EPI_STORE16 || g.epi.kind == EPI_RESID32 || g.epi.kind == EPI_GELU_MX8);
+}
 
 template <DT T>
 static void launch_mx8_t(const Mx8Call& g, hipStream_t st) {
+  if (mx8_256_ok(g)) {
+    const int tiles = g256_grid(((g.M + 255) / 256) * (g.N / 256));
+#define WMX_MX8B_LAUNCH(KD)                                                                                         \
+  hipLaunchKernelGGL((gemm_mx8_256_kernel<T, KD>), dim3(tiles), dim3(512), kMx8bLds, st, g.A, g.lda, g.AS, g.ldas, \
+                     g.W, g.ldw, g.WS, g.ldws, g.M, g.N, g.K, g.epi)
+    switch (g.epi.kind) {
+      case EPI_STORE16: WMX_MX8B_LAUNCH(EPI_STORE16); break;
+      case EPI_RESID32: WMX_MX8B_LAUNCH(EPI_RESID32); break;
+      default: WMX_MX8B_LAUNCH(EPI_GELU_MX8); break;
+    }
+#undef WMX_MX8B_LAUNCH
+    return;
+  }
   const int tiles = ((g.M + 255) / 256) * ((g.N + 127) / 128);
   hipLaunchKernelGGL((gemm_mx8_kernel<T>), dim3(g256_grid(tiles)), dim3(512), kMx8Lds, st, g.A, g.lda, g.AS, g.ldas,
                      g.W, g.ldw, g.WS, g.ldws, g.M, g.N, g.K, g.epi);
@@ -1329,6 +1559,18 @@ void gemm_init_attributes() {
                               kMx8Lds));
   WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_kernel<DT::F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kMx8Lds));
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_256_kernel<DT::BF16, EPI_STORE16>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kMx8bLds));
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_256_kernel<DT::BF16, EPI_RESID32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kMx8bLds));
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_256_kernel<DT::BF16, EPI_GELU_MX8>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kMx8bLds));
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_256_kernel<DT::F16, EPI_STORE16>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kMx8bLds));
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_256_kernel<DT::F16, EPI_RESID32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kMx8bLds));
+  WMX_HIP(hipFuncSetAttribute((const void*)gemm_mx8_256_kernel<DT::F16, EPI_GELU_MX8>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kMx8bLds));
   done = true;
 }
 

@@ -68,7 +68,7 @@ def test_mx8_translate_greedy_matches_oracle():
 
 
 def test_mx8_full_depth_large_v3_translate():
-    """Config 5's model at full depth: large-v3 with the MX-fp8 encoder (32 layers) on one window against the
+    """Config 5's model at full depth: large-v3 with the MX-fp8 encoder (32 layers), window 0 of three, against the
     oracle's MX rule, then the translate task's first greedy steps replayed token-exact on the recorded logits."""
     from wmx import engine as E
     import test_gpu_step as S
@@ -79,8 +79,11 @@ def test_mx8_full_depth_large_v3_translate():
     W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
     audio = synth.speech_like(511, 480000)
     mel = O.logmel_segment(audio, d.n_mels)
-    ctx = E.Context(m, max_batch=1, beam_size=1, max_new_tokens=8, task="translate", word_timestamps=False)
-    got = ctx.encode(mel[None])[0]
+    # three windows (4500 rows): the encoder projections run on the 256 x 256 / 32x32x64 MX-fp8 GEMM (from 4096
+    # rows); window 0 is compared
+    mels = np.stack([mel] + [O.logmel_segment(synth.speech_like(s, 240000), d.n_mels) for s in (512, 513)])
+    ctx = E.Context(m, max_batch=3, beam_size=1, max_new_tokens=8, task="translate", word_timestamps=False)
+    got = ctx.encode(mels)[0]
     ref = O.encoder(W, d, mel, mx8=True)
     e = rel_l2(got, ref)
     e16 = rel_l2(got, O.encoder(W, d, mel))
