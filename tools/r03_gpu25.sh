@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 3 (session 2), GPU call 25: decode mode under stream priorities: default vs WMX_STREAM_PRIO=1 (one group's
-# stream at the highest priority), 6 interleaved pairs of short bench runs
+# round 3 (session 2), GPU call 25: decode mode, default vs WMX_LOCKSTEP=1 (the two context groups start every decode
+# chunk together), 6 interleaved pairs of short bench runs (first used for the stream-priority A/B)
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/${1:-r03zj}
@@ -19,5 +19,5 @@ PY
 }
 for r in 1 2 3 4 5 6; do
   run default WMX_X=1
-  run prio WMX_STREAM_PRIO=1
+  run lockstep WMX_LOCKSTEP=1
 done
