@@ -16,7 +16,8 @@ def per_kind(path):
     with open(path) as f:
         for r in csv.DictReader(f):
             d = disp[r["Dispatch_Id"]]
-            d["name"] = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("wmx::", "").replace("(wmx::DT)", "")
+            nm = r["Kernel_Name"].replace("void ", "").replace("wmx::", "").replace("(DT)", "")
+            d["name"] = nm[:nm.find(">(") + 1] if ">(" in nm else nm.split("(")[0]
             d["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
