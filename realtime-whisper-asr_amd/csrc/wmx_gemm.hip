@@ -545,6 +545,40 @@ __device__ inline void epi_rows64_lns(const Epi& e, const float* img, int ldt, i
   if ((lane & 7) == 0 && m < M) e.stats[(long)(n0 >> 8) * e.stats_ld + m] = make_float2(mean_own, m2);
 }
 
+// GELU -> MX-fp8 epilogue for a 64-row x 256-column image with one MX block per thread: wave w takes the 32-column
+// block w and lane l row l, so the block's amax is thread-local (no lane shuffles), the 32 e4m3 bytes leave as two
+// 16-byte stores and the bias of the block is wave-uniform; row r's 16-B reads sit at bank 4r (row stride 260 floats),
+// conflict-free for ds_read_b128's lane groups.  Same arithmetic per element as the quad form in epi_rows64.
+template <DT T>
+__device__ inline void epi_gelu_mx8_blocks(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int tid) {
+  const int lane = tid & 63, blk = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = mb + lane, n = n0 + 32 * blk;
+  const float* src = img + lane * ldt + 32 * blk;
+  const float4* b4 = reinterpret_cast<const float4*>(e.bias + n);
+  float4 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 x = *reinterpret_cast<const float4*>(src + 4 * q);
+    const float4 b = e.bias ? b4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[q] = gelu_erf4(make_float4(x.x + b.x, x.y + b.y, x.z + b.z, x.w + b.w));
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[q].x), fabsf(v[q].y)), fmaxf(fabsf(v[q].z), fabsf(v[q].w))));
+  const int ex = mx8_exp(amax);
+  const float is = mx8_inv_scale(ex);
+  uint32_t w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) w[q] = mx8_pack4(v[q].x * is, v[q].y * is, v[q].z * is, v[q].w * is);
+  if (m < M) {
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(e.out) + (long)m * e.ldc + n);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    e.out2[(long)m * e.ldc2 + (n >> 5)] = (uint8_t)(ex + 127);
+  }
+}
+
 template <DT T, int KIND>
 __device__ inline void epi_image64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
                                    const float4* bpre = nullptr, const Resid8* pre = nullptr) {
@@ -1384,7 +1418,10 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
       }
     }
     __syncthreads();
-    epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4, kPre ? &pre : nullptr);
+    if constexpr (KIND == EPI_GELU_MX8)
+      epi_gelu_mx8_blocks<T>(e, img, LDT, m0 + rd * 64, n0, M, tid);
+    else
+      epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4, kPre ? &pre : nullptr);
     if constexpr (kPre) {
       if (rd < 3) resid_load<KIND>(pre, e, m0 + (rd + 1) * 64, n0, M, tid);
     }
