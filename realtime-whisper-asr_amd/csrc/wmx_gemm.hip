@@ -320,6 +320,16 @@ __device__ unsigned long long g256_stamps[kG256Stamps][3];
 #ifndef WMX_G256_PHASES
 #define WMX_G256_PHASES 2  // barrier-separated MFMA segments per 32-deep slice (1: one 32-MFMA segment per slice)
 #endif
+#ifndef WMX_G256_PRIO
+#define WMX_G256_PRIO 1  // 1: static priority 1 for waves 4..7 only (19.52-19.58 vs 19.81-19.84 ms per encoder pass); 0: s_setprio 1 around every MFMA segment (T5)
+#endif
+#if WMX_G256_PRIO == 0
+#define WMX_G256_PRIO_ON __builtin_amdgcn_s_setprio(1)
+#define WMX_G256_PRIO_OFF __builtin_amdgcn_s_setprio(0)
+#else
+#define WMX_G256_PRIO_ON (void)0
+#define WMX_G256_PRIO_OFF (void)0
+#endif
 #ifndef WMX_G256_DIRECT
 #define WMX_G256_DIRECT 1  // LDS-free epilogue for the bf16-output kinds (0: the LDS-image epilogue for all)
 #endif
@@ -806,6 +816,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
+#if WMX_G256_PRIO == 1
+  if (lagging) __builtin_amdgcn_s_setprio(1);  // static priority for the lagging half (MI355X_MICROARCH.md item 4)
+#endif
 #if WMX_G256_PHASES == 1
   // one phase per slice: [12 ds_reads (A 0..7, B 0..3) + the 4 DMAs of slice t + 3 + counted wait for t + 1]
   // s_barrier [32 MFMAs] s_barrier; waves 4..7 one barrier behind, as in the two-phase form
@@ -827,12 +840,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
+    WMX_G256_PRIO_OFF;
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
@@ -849,12 +862,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
+    WMX_G256_PRIO_OFF;
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     // ---- phase B ----
@@ -867,12 +880,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i + 4][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i + 4][j]);
-    __builtin_amdgcn_s_setprio(0);
+    WMX_G256_PRIO_OFF;
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
@@ -1128,6 +1141,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
+#if WMX_G256_PRIO == 1
+  if (lagging) __builtin_amdgcn_s_setprio(1);  // static priority for the lagging half (as gemm256)
+#endif
   i32x8 af[2], bfr[4];
   int sa[2], sb[4];
   for (int t = 0; t < nk; ++t) {
@@ -1151,14 +1167,14 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sa[i], 0,
                                                                      sb[j]);
-    __builtin_amdgcn_s_setprio(0);
+    WMX_G256_PRIO_OFF;
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     // ---- phase B: A fragments 2, 3; W half of slice t + 2 ----
@@ -1177,14 +1193,14 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i + 2][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i + 2][j], 0, 0, 0, sa[i],
                                                                          0, sb[j]);
-    __builtin_amdgcn_s_setprio(0);
+    WMX_G256_PRIO_OFF;
     if (!lagging) {  // the same barrier, seen from the leading half
       if (more)
         asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
@@ -1343,6 +1359,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
+#if WMX_G256_PRIO == 1
+  if (lagging) __builtin_amdgcn_s_setprio(1);  // static priority for the lagging half (as gemm256)
+#endif
   i32x8 af[2], bfr[2];
   int sa[2], sb[2];
   for (int t = 0; t < nk; ++t) {
@@ -1362,13 +1381,13 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sa[i], 0, sb[j]);
-    __builtin_amdgcn_s_setprio(0);
+    WMX_G256_PRIO_OFF;
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     // ---- phase B: slice t + 1 complete once only slices t + 2 .. t + NS - 2 (5 DMAs each) and the A half of
@@ -1383,14 +1402,14 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i + 2][j] =
             __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[i], bfr[j], acc[i + 2][j], 0, 0, 0, sa[i], 0, sb[j]);
-    __builtin_amdgcn_s_setprio(0);
+    WMX_G256_PRIO_OFF;
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
