@@ -5,8 +5,7 @@ torch.cuda.init()
 from wmx.engine import Model, Context
 for ct in ("bfloat16", "float8"):
     m = Model("large-v3", 0, ct)
-    m.init_synthetic(1)  # random weights (zero-filled operands run faster: DVFS)
-m.init_synthetic(1)  # random weights: zero-filled operands run ~10 % faster (DVFS), not representative
+    m.init_synthetic(1)  # random weights: zero-filled operands run ~10 % faster (DVFS), not representative
     ctx = Context(m, max_batch=8, beam_size=1, max_new_tokens=8)
     for B in (4, 8):
         ms, by, fl = ctx.bench_kernel("encoder", B, iters=3)

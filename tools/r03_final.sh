@@ -7,8 +7,12 @@ cd "$(dirname "$0")/.."
 O=gpurun_out/${1:-r03z}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
+# the subprocess-rerun tests print nothing for minutes: a heartbeat file keeps the box's silence watchdog informed
+(while sleep 50; do date >> $O/heartbeat.txt; done) &
+HB=$!
+trap "kill $HB" EXIT
 if [ "${2:-tests}" = tests ]; then
-  timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/gputest.log 2>&1
+  timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread --durations=25 -m gpu tests > $O/gputest.log 2>&1
   rc=$?; tail -3 $O/gputest.log
   if [ $rc -ne 0 ]; then echo "gpu tests failed (rc $rc): stopping"; exit 1; fi
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; exit 1; }
