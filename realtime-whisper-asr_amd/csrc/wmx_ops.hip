@@ -153,11 +153,59 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const float* __restr
   }
 }
 
+// the same for d == 256 * NIT (d 1024, 1280): unguarded loads, and the gain / bias vectors read in the store loop
+// (L2-resident) instead of held beside the row, so a wave keeps 4 * NIT data registers and more waves fit a SIMD
+#ifndef WMX_LNMX_T
+#define WMX_LNMX_T 1
+#endif
+template <int NIT>
+__global__ __launch_bounds__(256) void layernorm_mx8_exact_kernel(const float* __restrict__ x,
+                                                                  const float* __restrict__ g,
+                                                                  const float* __restrict__ bb, uint8_t* __restrict__ q,
+                                                                  uint8_t* __restrict__ sc, int rows) {
+  constexpr int d = 256 * NIT;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const float4* xr = reinterpret_cast<const float4*>(x + (long)row * d);
+  float4 v[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) v[i] = xr[lane + i * 64];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = wave_sum(s) / d;
+  float qq = 0.f;
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, e = v[i].w - mean;
+    qq += a * a + b * b + cc * cc + e * e;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(qq) / d + 1e-5f);
+  uint32_t* qo = reinterpret_cast<uint32_t*>(q + (long)row * d);
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int c = lane + i * 64;
+    const float4 gg = reinterpret_cast<const float4*>(g)[c], be = reinterpret_cast<const float4*>(bb)[c];
+    const float y0 = (v[i].x - mean) * rstd * gg.x + be.x, y1 = (v[i].y - mean) * rstd * gg.y + be.y;
+    const float y2 = (v[i].z - mean) * rstd * gg.z + be.z, y3 = (v[i].w - mean) * rstd * gg.w + be.w;
+    const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3)))));
+    const float is = mx8_inv_scale(ex);
+    qo[c] = mx8_pack4(y0 * is, y1 * is, y2 * is, y3 * is);
+    if ((lane & 7) == 0) sc[(long)row * (d >> 5) + (c >> 3)] = (uint8_t)(ex + 127);
+  }
+}
+
 void launch_layernorm_mx8(const float* x, const float* g, const float* b, uint8_t* q, uint8_t* s, int rows, int d,
                           hipStream_t st) {
   if (rows <= 0) return;
   WMX_CHECK(d % 32 == 0 && d <= 2048, "layernorm_mx8: d");
-  hipLaunchKernelGGL(layernorm_mx8_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows, d);
+  if (WMX_LNMX_T && d == 1280)
+    hipLaunchKernelGGL(layernorm_mx8_exact_kernel<5>, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows);
+  else if (WMX_LNMX_T && d == 1024)
+    hipLaunchKernelGGL(layernorm_mx8_exact_kernel<4>, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows);
+  else
+    hipLaunchKernelGGL(layernorm_mx8_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows, d);
   WMX_HIP(hipGetLastError());
 }
 
