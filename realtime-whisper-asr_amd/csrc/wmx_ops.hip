@@ -154,45 +154,64 @@ __global__ __launch_bounds__(256) void layernorm_mx8_kernel(const float* __restr
 }
 
 // the same for d == 256 * NIT (d 1024, 1280): unguarded loads, and the gain / bias vectors read in the store loop
-// (L2-resident) instead of held beside the row, so a wave keeps 4 * NIT data registers and more waves fit a SIMD
+// (L2-resident) instead of held beside the row (46 VGPRs at R = 1 against the generic kernel's 110).  A wave takes R
+// rows with all their loads in one batch: at R = 2 the 12000 rows of 8 large-v3 windows are 6000 waves, which fit the
+// chip's wave slots in one round instead of 1.5
 #ifndef WMX_LNMX_T
 #define WMX_LNMX_T 1
 #endif
-template <int NIT>
+#ifndef WMX_LNMX_R
+#define WMX_LNMX_R 1
+#endif
+template <int NIT, int R>
 __global__ __launch_bounds__(256) void layernorm_mx8_exact_kernel(const float* __restrict__ x,
                                                                   const float* __restrict__ g,
                                                                   const float* __restrict__ bb, uint8_t* __restrict__ q,
                                                                   uint8_t* __restrict__ sc, int rows) {
   constexpr int d = 256 * NIT;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + wave;
-  if (row >= rows) return;
-  const float4* xr = reinterpret_cast<const float4*>(x + (long)row * d);
-  float4 v[NIT];
+  const int row0 = (blockIdx.x * 4 + wave) * R;
+  if (row0 >= rows) return;
+  float4 v[R][NIT];
 #pragma unroll
-  for (int i = 0; i < NIT; ++i) v[i] = xr[lane + i * 64];
-  float s = 0.f;
+  for (int j = 0; j < R; ++j) {
+    const float4* xr = reinterpret_cast<const float4*>(x + (long)min(row0 + j, rows - 1) * d);
 #pragma unroll
-  for (int i = 0; i < NIT; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-  const float mean = wave_sum(s) / d;
-  float qq = 0.f;
-#pragma unroll
-  for (int i = 0; i < NIT; ++i) {
-    const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, e = v[i].w - mean;
-    qq += a * a + b * b + cc * cc + e * e;
+    for (int i = 0; i < NIT; ++i) v[j][i] = xr[lane + i * 64];
   }
-  const float rstd = 1.0f / sqrtf(wave_sum(qq) / d + 1e-5f);
-  uint32_t* qo = reinterpret_cast<uint32_t*>(q + (long)row * d);
+  float mean[R], rstd[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) s += (v[j][i].x + v[j][i].y) + (v[j][i].z + v[j][i].w);
+    mean[j] = wave_sum(s) / d;
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    float qq = 0.f;
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const float a = v[j][i].x - mean[j], b = v[j][i].y - mean[j], cc = v[j][i].z - mean[j], e = v[j][i].w - mean[j];
+      qq += a * a + b * b + cc * cc + e * e;
+    }
+    rstd[j] = 1.0f / sqrtf(wave_sum(qq) / d + 1e-5f);
+  }
 #pragma unroll
   for (int i = 0; i < NIT; ++i) {
     const int c = lane + i * 64;
     const float4 gg = reinterpret_cast<const float4*>(g)[c], be = reinterpret_cast<const float4*>(bb)[c];
-    const float y0 = (v[i].x - mean) * rstd * gg.x + be.x, y1 = (v[i].y - mean) * rstd * gg.y + be.y;
-    const float y2 = (v[i].z - mean) * rstd * gg.z + be.z, y3 = (v[i].w - mean) * rstd * gg.w + be.w;
-    const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3)))));
-    const float is = mx8_inv_scale(ex);
-    qo[c] = mx8_pack4(y0 * is, y1 * is, y2 * is, y3 * is);
-    if ((lane & 7) == 0) sc[(long)row * (d >> 5) + (c >> 3)] = (uint8_t)(ex + 127);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (row0 + j >= rows) break;
+      const float m = mean[j], r = rstd[j];
+      const float y0 = (v[j][i].x - m) * r * gg.x + be.x, y1 = (v[j][i].y - m) * r * gg.y + be.y;
+      const float y2 = (v[j][i].z - m) * r * gg.z + be.z, y3 = (v[j][i].w - m) * r * gg.w + be.w;
+      const int ex = mx8_exp(max8_lanes(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3)))));
+      const float is = mx8_inv_scale(ex);
+      reinterpret_cast<uint32_t*>(q + (long)(row0 + j) * d)[c] = mx8_pack4(y0 * is, y1 * is, y2 * is, y3 * is);
+      if ((lane & 7) == 0) sc[(long)(row0 + j) * (d >> 5) + (c >> 3)] = (uint8_t)(ex + 127);
+    }
   }
 }
 
@@ -200,10 +219,13 @@ void launch_layernorm_mx8(const float* x, const float* g, const float* b, uint8_
                           hipStream_t st) {
   if (rows <= 0) return;
   WMX_CHECK(d % 32 == 0 && d <= 2048, "layernorm_mx8: d");
+  constexpr int R = WMX_LNMX_R;
   if (WMX_LNMX_T && d == 1280)
-    hipLaunchKernelGGL(layernorm_mx8_exact_kernel<5>, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows);
+    hipLaunchKernelGGL((layernorm_mx8_exact_kernel<5, R>), dim3(cdiv(rows, 4 * R)), dim3(256), 0, st, x, g, b, q, s,
+                       rows);
   else if (WMX_LNMX_T && d == 1024)
-    hipLaunchKernelGGL(layernorm_mx8_exact_kernel<4>, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows);
+    hipLaunchKernelGGL((layernorm_mx8_exact_kernel<4, R>), dim3(cdiv(rows, 4 * R)), dim3(256), 0, st, x, g, b, q, s,
+                       rows);
   else
     hipLaunchKernelGGL(layernorm_mx8_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, st, x, g, b, q, s, rows, d);
   WMX_HIP(hipGetLastError());
