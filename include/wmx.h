@@ -37,10 +37,17 @@ enum {
   WMX_ERR_HIP = 2,      /* HIP runtime error */
   WMX_ERR_STATE = 3,    /* call in the wrong state (e.g. decode before encode) */
   WMX_ERR_NOMEM = 4,
+  WMX_ERR_NUMERIC = 5,  /* the decode produced non-finite logits (wmx_last_error names the step and row) */
 };
 
-/* WMX_DTYPE_MX8: bf16 everywhere except the encoder projections (q/k/v, out, fc1, fc2), which run on the
- * CDNA4 MX-fp8 MFMA (OCP e4m3 elements, e8m0 scale per 32 K) with MX-fp8 activations (BASELINE config 5). */
+/* WMX_DTYPE_MX8 (BASELINE config 5, "large-v3 fp8"): bf16 storage and activations, with
+ *  - the encoder projections (q/k/v, out, fc1, fc2) on the CDNA4 MX-fp8 MFMA (OCP e4m3 elements, e8m0 scale per
+ *    32 K) with MX-fp8 activations;
+ *  - the fp8 decode: every decoder projection and the logits projection on 8-bit weights (e4m3, one power-of-two
+ *    scale per weight row, widened to bf16 in registers) and the cross-attention K / V images in e4m3 (one
+ *    power-of-two scale per (layer, window, head) image).  WMX_DEC_FP8=0 in the environment keeps the decode bf16.
+ * The reference's own 8-bit GPU mode is CTranslate2's int8_float16 (int8 weights with per-row scales): the host
+ * layer maps compute_type "int8_float16" / "int8" to this dtype (wmx/engine.py). */
 enum { WMX_DTYPE_BF16 = 0, WMX_DTYPE_F16 = 1, WMX_DTYPE_MX8 = 2 };
 enum { WMX_TASK_TRANSCRIBE = 0, WMX_TASK_TRANSLATE = 1 };
 
@@ -126,9 +133,11 @@ wmx_status wmx_model_set_tensor(wmx_model* m, const char* name, const float* dat
 /* read back one tensor (logical HF layout, values as stored) — tests / checkpoint export */
 wmx_status wmx_model_get_tensor(wmx_model* m, const char* name, float* out, int64_t n);
 int64_t wmx_model_n_params(const wmx_model* m);
-/* the weight arena: one device allocation holding every parameter (for RCCL broadcast of weights) */
+/* the parameter region of the weight arena: [device_ptr, device_ptr + bytes) holds every parameter (what an RCCL
+ * broadcast of the weights must carry); the derived copies (row-major, MX-fp8, 8-bit, LayerNorm-folded, log-mel
+ * constants) live after it and are rebuilt on each rank by wmx_model_arena_loaded */
 wmx_status wmx_model_arena(wmx_model* m, void** device_ptr, size_t* bytes);
-/* after the arena was overwritten externally (e.g. ncclBroadcast), mark weights as initialised */
+/* after the parameter region was overwritten externally (e.g. ncclBroadcast): derive the copies, mark initialised */
 wmx_status wmx_model_arena_loaded(wmx_model* m);
 
 /* ---- context ---- */

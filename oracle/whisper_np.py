@@ -150,16 +150,61 @@ def e4m3_round(v: np.ndarray) -> np.ndarray:
     return (np.sign(v) * q).astype(np.float32)
 
 
-def mx8_quantize(x: np.ndarray) -> np.ndarray:
-    """MX-fp8 round trip along the last axis (blocks of 32): the dequantized float32 values the MFMA consumes."""
+def mx8_quantize(x: np.ndarray, block: int = 32) -> np.ndarray:
+    """MX-fp8 round trip along the last axis (blocks of `block`, default 32; the fp8 decode's weights use the whole row,
+    w8_rows): the dequantized float32 values the MFMA consumes."""
     x = np.ascontiguousarray(x, dtype=np.float32)
     K = x.shape[-1]
-    assert K % 32 == 0
-    b = x.reshape(x.shape[:-1] + (K // 32, 32))
+    assert K % block == 0
+    b = x.reshape(x.shape[:-1] + (K // block, block))
     e = mx8_exp(np.abs(b).max(-1))[..., None]
     inv = np.ldexp(np.float32(1.0), -e).astype(np.float32)
     q = e4m3_round((b * inv).astype(np.float32))
     return (q.astype(np.float64) * np.ldexp(1.0, e)).astype(np.float32).reshape(x.shape)
+
+
+# ----------------------------------------------------------------------------------------------
+# The fp8 decode of the same model dtype (csrc/wmx_ops.hip w8_quantize_kernel / crosskv_quant_kernel).  Restated
+# from this build's own rule -- no reference fixture exists (faster-whisper/CT2 have no fp8 mode; their 8-bit mode,
+# int8_float16, quantizes each weight ROW with its own scale, which is the granularity kept here):
+#   * every decoder projection (self q/k/v/out, cross q/out, fc1, fc2) and the logits projection (the token
+#     embedding, tied) is e4m3 with ONE power-of-two scale per weight row, chosen by the MX rule above over the row;
+#     the embedding LOOKUP keeps the 16-bit table;
+#   * the cross-attention K / V of every (layer, head) are rounded to the model dtype (the device stores 16-bit images
+#     first) and then e4m3 with one power-of-two scale per (layer, window, head) image (1500 keys x 64 dims);
+#   * activations, LayerNorms, biases and the self-attention cache are unchanged.
+# The device multiplies the fp32 products by the scales outside the MFMA (exact: powers of two).
+# ----------------------------------------------------------------------------------------------
+FP8_DEC_LINEARS = ("self_attn.q_proj", "self_attn.k_proj", "self_attn.v_proj", "self_attn.out_proj",
+                   "encoder_attn.q_proj", "encoder_attn.out_proj", "fc1", "fc2")
+
+
+def w8_rows(w: np.ndarray) -> np.ndarray:
+    """A weight matrix [N][K] through the fp8 decode's rule: e4m3 with one MX power-of-two scale per row."""
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    return mx8_quantize(w, block=w.shape[-1])
+
+
+def fp8_decoder_weights(W: dict, d: Dims) -> dict:
+    """The weights the fp8 decode computes with: a copy of W whose decoder projections are w8_rows-quantized, with
+    the quantized embedding as the separate logits projection ("decoder.proj_out.weight") and the cross-K/V image
+    rule switched on ("decoder.kv8", read by DecoderCache)."""
+    V = dict(W)
+    for i in range(d.n_text_layer):
+        for n in FP8_DEC_LINEARS:
+            k = f"decoder.layers.{i}.{n}.weight"
+            V[k] = w8_rows(W[k])
+    V["decoder.proj_out.weight"] = w8_rows(W["decoder.embed_tokens.weight"])
+    V["decoder.kv8"] = True
+    return V
+
+
+def kv8_images(x: np.ndarray, n_head: int) -> np.ndarray:
+    """Cross K or V [T][d] of one window through the fp8 image rule: bf16, then e4m3 with one MX scale per head."""
+    T, dm = x.shape
+    xh = round_bf16(x).reshape(T, n_head, dm // n_head).transpose(1, 0, 2).reshape(n_head, -1)
+    q = mx8_quantize(xh, block=xh.shape[-1])
+    return q.reshape(n_head, T, dm // n_head).transpose(1, 0, 2).reshape(T, dm)
 
 
 def linear_mx8(x, W, p, bias=True):
@@ -386,10 +431,14 @@ class DecoderCache:
         self.k = [np.zeros((0, d.n_text_state), np.float32) for _ in range(d.n_text_layer)]
         self.v = [np.zeros((0, d.n_text_state), np.float32) for _ in range(d.n_text_layer)]
         self.ck, self.cv = [], []
+        kv8 = bool(W.get("decoder.kv8", False))  # the fp8 decode's image rule (fp8_decoder_weights)
         for i in range(d.n_text_layer):
             p = f"decoder.layers.{i}.encoder_attn"
-            self.ck.append(linear(enc, W, p + ".k_proj", bias=False))
-            self.cv.append(linear(enc, W, p + ".v_proj"))
+            k, v = linear(enc, W, p + ".k_proj", bias=False), linear(enc, W, p + ".v_proj")
+            if kv8:
+                k, v = kv8_images(k, d.n_text_head), kv8_images(v, d.n_text_head)
+            self.ck.append(k)
+            self.cv.append(v)
 
     @property
     def length(self):
@@ -430,7 +479,8 @@ def decoder_forward(W, d: Dims, tokens, cache: DecoderCache, align_heads=None):
         h = layer_norm(x, W[p + ".final_layer_norm.weight"], W[p + ".final_layer_norm.bias"])
         x = x + linear(gelu(linear(h, W, p + ".fc1")), W, p + ".fc2")
     x = layer_norm(x, W["decoder.layer_norm.weight"], W["decoder.layer_norm.bias"])
-    logits = (x @ W["decoder.embed_tokens.weight"].T).astype(np.float32)
+    # (the fp8 decode's logits projection is the quantized embedding, fp8_decoder_weights)
+    logits = (x @ W.get("decoder.proj_out.weight", W["decoder.embed_tokens.weight"]).T).astype(np.float32)
     if align_heads is not None:
         return logits, np.stack(qk_store) if qk_store else np.zeros((0, T, cache.ck[0].shape[0]), np.float32)
     return logits

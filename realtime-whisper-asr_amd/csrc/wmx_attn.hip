@@ -633,7 +633,9 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
       if (key == slot_q) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += p * vcur[c * 8 + e];
-      } else {
+      } else if (key < slot_q) {
+        // (keys past slot_q re-read slot_q's cache entry, which this launch is still writing: whatever a previous
+        // call left there -- NaN after a non-finite call -- must not meet their zero weights, 0 x NaN = NaN)
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += p * to_f32<T>(vv[j][e]);
       }
@@ -691,7 +693,12 @@ typedef __attribute__((address_space(1))) float gf32;
 // chunk records [nwin][H][KS][nq][66]; one arrival counter per (window, head) in DecAttnArgs::xcnt
 inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long)nwin * H * KS * nq * 66; }
 
-template <DT T, int KPW, int NWV, bool XQ = false>
+// F8 (the fp8 decode of model dtype MX8): the K / V^T images are e4m3 (launch_crosskv_quant: one 16-byte lane piece
+// = both dim halves of a key pair / two dim blocks of a key block, so half the wave loads of the 16-bit images),
+// widened to the 16-bit MFMA operands in registers; the image scales enter exactly -- the K scale (a power of two)
+// multiplies the queries before their 16-bit rounding, the V scale the merged output -- and with XQ the fused
+// query projection's weights are 8-bit too (packed8_index, per-row scales a.wq_scale)
+template <DT T, int KPW, int NWV, bool XQ = false, bool F8 = false>
 __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   constexpr int NT = 64 * NWV;
   int h = blockIdx.x, w = blockIdx.y, zz = blockIdx.z;
@@ -725,17 +732,26 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const int kc0 = ks * chunk, kc1 = min(a.Tk, kc0 + chunk);
   const int per = ((kc1 - kc0 + NWV - 1) / NWV + 31) / 32 * 32;  // keys per wave, whole 32-key blocks
   const int kw0 = kc0 + wave * per, kw1 = min(kc1, kw0 + per);
-  const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
-  const uint16_t* vbase = a.cv + (long)w * a.x_wstride + (long)h * a.x_hstride;
+  constexpr int EB = F8 ? 1 : 2;  // image element bytes
+  const char* kbase = reinterpret_cast<const char*>(a.ck) + ((long)w * a.x_wstride + (long)h * a.x_hstride) * EB;
+  const char* vbase = reinterpret_cast<const char*>(a.cv) + ((long)w * a.x_wstride + (long)h * a.x_hstride) * EB;
+  // fp8 images: their scales (scalar loads, issued first; read-only in this launch)
+  float ksc = 1.f, vsc = 1.f;
+  if constexpr (F8) {
+    typedef const __attribute__((address_space(4))) float cf4;
+    ksc = *(cf4*)(a.ck_scale + w * a.H + h);
+    vsc = *(cf4*)(a.cv_scale + w * a.H + h);
+  }
 
   // ---- first batch of K / V^T loads (issued before the q reduction so their latency overlaps it) ----
   // K A-fragment of block b, pair u, dim half hh: key kb + 8*(fr>>2) + 4u + (fr&3), dims 32hh + 8g .. +8
   // V^T B-fragment of block b, dim block db: V^T[16db + fr][kb + 8g .. +8]
+  // (F8: kf[b][u][0] holds both dim halves' 16 bytes, vf[b][dp] the 16 bytes of dim blocks 2dp, 2dp + 1)
   u16x8 kf[KPW][2][2], vf[KPW][4];
   // buffer loads: one 32-bit lane offset per image, the block / half / dim-block offsets in the scalar operand;
   // keys past the image (kb + ... >= kXS) fall outside the descriptor's range and read as zeros
-  const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, (short)0, kXS * 64 * 2, 0x00020000);
-  const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, 64 * kXS * 2, 0x00020000);
+  const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, (short)0, kXS * 64 * EB, 0x00020000);
+  const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, 64 * kXS * EB, 0x00020000);
   // fragment-major images (crossk_off / crossv_off): every load below is one contiguous 1 KiB wave piece
   const int loff = lane * 16;
   // 32-key block index kb0 / 32 + b (blocks past the image read as zeros)
@@ -745,17 +761,17 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
+        for (int hh = 0; hh < (F8 ? 1 : 2); ++hh)
           kf[b][u][hh] = __builtin_bit_cast(
-              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, loff, ((((kb0 >> 5) + b) * 2 + u) * 2 + hh) * 1024, WMX_KV_AUX));
+              u16x8, __builtin_amdgcn_raw_buffer_load_b128(krs, loff, ((((kb0 >> 5) + b) * 2 + u) * (F8 ? 1 : 2) + hh) * 1024, WMX_KV_AUX));
   };
   auto load_v = [&](int kb0) {
 #pragma unroll
     for (int b = 0; b < KPW; ++b)
 #pragma unroll
-      for (int db = 0; db < 4; ++db)
+      for (int db = 0; db < (F8 ? 2 : 4); ++db)
         vf[b][db] = __builtin_bit_cast(
-            u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, loff, (((kb0 >> 5) + b) * 4 + db) * 1024, WMX_KV_AUX));
+            u16x8, __builtin_amdgcn_raw_buffer_load_b128(vrs, loff, (((kb0 >> 5) + b) * (F8 ? 2 : 4) + db) * 1024, WMX_KV_AUX));
   };
   auto load_batch = [&](int kb0) {
     load_k(kb0);
@@ -767,24 +783,31 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   //      one MFMA fragment per (k-step, 16-column block) from the packed layout (packed_w_elem / packed_a_elem);
   //      all of the wave's query-projection loads are issued BEFORE the first K / V batch, so its MFMAs wait only
   //      for them; rows past the tile repeat its last query (never stored) ----
-  constexpr int QKU = 5;
-  const int qksteps = a.d >> 5;
+  // (F8: a k-step is 64 deep, one 16-byte packed8 weight piece per column block and two A fragments)
+  constexpr int QKU = F8 ? 3 : 5;
+  const int qksteps = a.d >> (F8 ? 6 : 5);
   const int qkper = (qksteps + NWV - 1) / NWV;
   const int qk0 = wave * qkper, qk1 = min(qksteps, qk0 + qkper);
-  u16x8 qav[QKU], qbv[QKU][4];
+  u16x8 qav[QKU][F8 ? 2 : 1], qbv[QKU][4];
   constexpr bool fuse_q = XQ;  // (a.wq != null; the launcher picks the instantiation)
-  // this thread's query column h 64 + (tid & 63) (the same for both of its elements below): its bias now, not
-  // after the projection's barrier
+  // this thread's query column h 64 + (tid & 63) (the same for both of its elements below): its bias (and 8-bit
+  // row scale) now, not after the projection's barrier
   const float qb_col = (fuse_q && a.qbias) ? a.qbias[h * 64 + (tid & 63)] : 0.f;
+  const float qs_col = (fuse_q && F8) ? a.wq_scale[h * 64 + (tid & 63)] : 1.f;
   if (fuse_q) {
     const uint16_t* ap = a.qin + ((long)w * nq + i0 + min(fr, nqt - 1)) * a.qin_ld + 8 * g;
-    const uint16_t* wp = a.wq + (((long)h * 4 * qksteps) << 9) + lane * 8;
+    const uint16_t* wp = a.wq + (((long)h * 4 * qksteps) << 9) + lane * 8;  // (F8: the same 16-byte lane pieces)
 #pragma unroll
     for (int u = 0; u < QKU; ++u) {
       // clamped into the matrix (also for a wave with no k-steps): finite duplicate data that meets a zeroed A
       // fragment below, never uninitialised registers (0 x NaN garbage would poison the tile)
       const int k = min(qk0 + u, qksteps - 1);
-      qav[u] = *reinterpret_cast<const u16x8*>(ap + k * 32);
+      if constexpr (F8) {
+        qav[u][0] = *reinterpret_cast<const u16x8*>(ap + k * 64);
+        qav[u][1] = *reinterpret_cast<const u16x8*>(ap + k * 64 + 32);
+      } else {
+        qav[u][0] = *reinterpret_cast<const u16x8*>(ap + k * 32);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) qbv[u][j] = stream_load(reinterpret_cast<const u16x8*>(wp + (((long)j * qksteps + k) << 9)));
     }
@@ -807,9 +830,20 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
     for (int u = 0; u < QKU; ++u) {
       const u16x8 za = {0, 0, 0, 0, 0, 0, 0, 0};
-      const u16x8 av = qk0 + u < qk1 ? qav[u] : za;
+      const u16x8 av = qk0 + u < qk1 ? qav[u][0] : za;
+      if constexpr (F8) {
+        const u16x8 av1 = qk0 + u < qk1 ? qav[u][F8 ? 1 : 0] : za;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) qa[j] = mfma16<T>(av, qbv[u][j], qa[j]);
+        for (int j = 0; j < 4; ++j) {
+          u16x8 blo, bhi;
+          fp8x16_to16<T>(__builtin_bit_cast(u32x4, qbv[u][j]), blo, bhi);
+          qa[j] = mfma16<T>(av, blo, qa[j]);
+          qa[j] = mfma16<T>(av1, bhi, qa[j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qa[j] = mfma16<T>(av, qbv[u][j], qa[j]);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -822,7 +856,8 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   // ---- the tile's queries into LDS (bf16/f16), one element per thread: q = bias + sum of the split-K partials in
   //      slice order, or the stored q; pre-scaled by log2(e) / sqrt(64) so the scores come out of the MFMA in
   //      log2 units (softmax on exp2, no per-score scaling) ----
-  constexpr float kQScale = 0.125f * 1.4426950408889634f;
+  // (F8: times the K image's power-of-two scale, so S = K8 . q' = K . q exactly as with the dequantized image)
+  const float kQScale = 0.125f * 1.4426950408889634f * ksc;
   __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
   __shared__ float2 qln[16];
   if (a.qS > 0 && a.ln_c1) {  // LN2 folded into the cross-q weights: the tile's row statistics, one wave per row
@@ -842,7 +877,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         float p = 0.f;
 #pragma unroll
         for (int wv = 0; wv < NWV; ++wv) p += so[wv][q][e];
-        v = from_f32<T>((p + qb_col) * kQScale);
+        v = from_f32<T>((p * qs_col + qb_col) * kQScale);
       } else if (a.qS > 0) {
         const float* src = a.qpart + row * a.qpart_ld + col;
         float tv[8];
@@ -880,8 +915,15 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x4 acc = f32x4{0, 0, 0, 0};
-        acc = mfma16<T>(kf[b][u][0], qb[0], acc);
-        acc = mfma16<T>(kf[b][u][1], qb[1], acc);
+        if constexpr (F8) {
+          u16x8 k0, k1;
+          fp8x16_to16<T>(__builtin_bit_cast(u32x4, kf[b][u][0]), k0, k1);
+          acc = mfma16<T>(k0, qb[0], acc);
+          acc = mfma16<T>(k1, qb[1], acc);
+        } else {
+          acc = mfma16<T>(kf[b][u][0], qb[0], acc);
+          acc = mfma16<T>(kf[b][u][1], qb[1], acc);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb0 + 32 * b + 8 * g + 4 * u + r;
@@ -929,10 +971,22 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         phi[j] = hi;
         plo[j] = from_f32<T>(sv[b][j] - to_f32<T>(hi));
       }
+      if constexpr (F8) {
 #pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        o[db] = mfma16<T>(phi, vf[b][db], o[db]);
-        o[db] = mfma16<T>(plo, vf[b][db], o[db]);
+        for (int dp = 0; dp < 2; ++dp) {
+          u16x8 v0, v1;
+          fp8x16_to16<T>(__builtin_bit_cast(u32x4, vf[b][dp]), v0, v1);
+          o[2 * dp] = mfma16<T>(phi, v0, o[2 * dp]);
+          o[2 * dp] = mfma16<T>(plo, v0, o[2 * dp]);
+          o[2 * dp + 1] = mfma16<T>(phi, v1, o[2 * dp + 1]);
+          o[2 * dp + 1] = mfma16<T>(plo, v1, o[2 * dp + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          o[db] = mfma16<T>(phi, vf[b][db], o[db]);
+          o[db] = mfma16<T>(plo, vf[b][db], o[db]);
+        }
       }
     }
   }
@@ -962,7 +1016,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     }
     const long row = (long)w * nq + i0 + q;
     if (KS == 1) {
-      a.o[row * a.d + h * 64 + e] = from_f32<T>(O / L);
+      a.o[row * a.d + h * 64 + e] = from_f32<T>(O / L * vsc);
     } else {
       // chunk record, stored write-through (sc1) so the last arriver can read it without an L2 release
       gf32* pr = (gf32*)(part + (((long)(w * a.H + h) * KS + ks) * nq + i0 + q) * 66);
@@ -1021,7 +1075,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         o2 += rec[k][2] * sc2;
       }
     }
-    a.o[((long)w * nq + q) * a.d + h * 64 + e] = from_f32<T>(o2 / l);
+    a.o[((long)w * nq + q) * a.d + h * 64 + e] = from_f32<T>(o2 / l * vsc);
   }
   if (tid == 0) __hip_atomic_store(cnt + w * a.H + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   probe_end();
@@ -1045,7 +1099,7 @@ size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
   return (size_t)cross_records_floats(H, nwin, nq_max, kMaxSplits);
 }
 
-template <DT T>
+template <DT T, bool F8>
 static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
   DecAttnArgs a = a0;
   static const int remap = [] {  // WMX_XATTN_REMAP=0/1: A/B switch of the head-per-XCD placement
@@ -1068,35 +1122,35 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
     return v && atoi(v) == 4 ? 4 : 8;
   }();
   // the fused query projection holds a wave's whole K share (<= 5 k-steps) in one load batch
-  WMX_CHECK(!a.wq || (a.d / 32 + 7) / 8 <= 5,
+  WMX_CHECK(!a.wq || (F8 ? (a.d / 64 + 7) / 8 <= 3 : (a.d / 32 + 7) / 8 <= 5),
             "cross attn: fused query projection: model width too large for one load batch per wave");
   WMX_CHECK(!a.wq || (waves == 8 && nq <= 16), "cross attn: the fused query projection runs on the 8-wave decode kernel");
   if (a.wq) {
     const int per_wave = ((chunk + 7) / 8 + 31) / 32;
     switch (std::min(per_wave, 4)) {
-      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
     }
     return;
   }
   if (waves == 8 && nq <= 16) {
     const int per_wave = ((chunk + 7) / 8 + 31) / 32;
     switch (std::min(per_wave, 4)) {
-      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8, false, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8, false, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8, false, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8, false, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
     }
     return;
   }
   const int per_wave = ((chunk + 3) / 4 + 31) / 32;  // 32-key blocks per wave
   switch (std::min(per_wave, 4)) {
-    case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
-    case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
-    case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
-    default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 4>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 4, false, F8>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 4, false, F8>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 4, false, F8>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
+    default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 4, false, F8>), grid, dim3(256), 0, st, a, KS, chunk, ws); break;
   }
 }
 
@@ -1104,31 +1158,45 @@ void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {
   WMX_CHECK(a.Tk <= 1500 && a.d == a.H * 64, "cross attn: shape");
   WMX_CHECK(!a.wq || (a.qin && a.Tn == 1 && a.rows_per_win <= 16 && a.d % 32 == 0 && a.qin_ld >= a.d),
             "cross attn: fused query projection needs a decode step (one 16-query tile per window)");
-  if (dt == DT::BF16)
-    launch_cross_t<DT::BF16>(a, ws, st);
-  else
-    launch_cross_t<DT::F16>(a, ws, st);
+  const bool f8 = a.ck_scale != nullptr;
+  WMX_CHECK(!f8 || (a.cv_scale && (!a.wq || a.wq_scale)), "cross attn: fp8 images need their scales (and 8-bit query weights)");
+  WMX_CHECK(f8 || !a.wq_scale, "cross attn: 8-bit query weights run with the fp8 images only");
+  if (dt == DT::BF16) {
+    if (f8) launch_cross_t<DT::BF16, true>(a, ws, st);
+    else launch_cross_t<DT::BF16, false>(a, ws, st);
+  } else {
+    if (f8) launch_cross_t<DT::F16, true>(a, ws, st);
+    else launch_cross_t<DT::F16, false>(a, ws, st);
+  }
   WMX_HIP(hipGetLastError());
 }
 
 // ------------------------------------------------------------------------------------------------
 // raw cross-attention scores of the alignment heads: out[hh][m][s] = q_m . k_s / 8
 // ------------------------------------------------------------------------------------------------
-template <DT T>
+template <DT T, bool F8>
 __global__ __launch_bounds__(256) void cross_scores_kernel(DecAttnArgs a, const int* heads, float* out) {
   const int hh = blockIdx.x, m = blockIdx.y;
   const int h = heads[hh];
   const int r = m / a.Tn;
   const int w = r / a.rows_per_win;
   __shared__ float qs[64];
-  if (threadIdx.x < 64) qs[threadIdx.x] = to_f32<T>(a.q[(long)m * a.q_ld + h * 64 + threadIdx.x]) * 0.125f;
+  // (fp8 images: the K image's scale folded into the query, like the decode kernel)
+  const float ksc = F8 ? a.ck_scale[w * a.H + h] : 1.f;
+  if (threadIdx.x < 64) qs[threadIdx.x] = to_f32<T>(a.q[(long)m * a.q_ld + h * 64 + threadIdx.x]) * 0.125f * ksc;
   __syncthreads();
-  const uint16_t* kbase = a.ck + (long)w * a.x_wstride + (long)h * a.x_hstride;
+  const long ioff = (long)w * a.x_wstride + (long)h * a.x_hstride;
   for (int s = threadIdx.x; s < a.Tk; s += 256) {
     float acc = 0.f;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const u16x8 kv = *reinterpret_cast<const u16x8*>(kbase + crossk_off(s, c * 8));
+      u16x8 kv;
+      if constexpr (F8) {
+        const uint2 k8 = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(a.ck) + ioff + crossk8_off(s, c * 8));
+        kv = fp8x8_to16<T>(k8.x, k8.y);
+      } else {
+        kv = *reinterpret_cast<const u16x8*>(a.ck + ioff + crossk_off(s, c * 8));
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc += qs[c * 8 + e] * to_f32<T>(kv[e]);
     }
@@ -1138,10 +1206,14 @@ __global__ __launch_bounds__(256) void cross_scores_kernel(DecAttnArgs a, const 
 
 void launch_cross_scores(DT dt, const DecAttnArgs& a, const int* heads, int nh, float* out, hipStream_t st) {
   dim3 grid(nh, a.R * a.Tn);
-  if (dt == DT::BF16)
-    hipLaunchKernelGGL(cross_scores_kernel<DT::BF16>, grid, dim3(256), 0, st, a, heads, out);
-  else
-    hipLaunchKernelGGL(cross_scores_kernel<DT::F16>, grid, dim3(256), 0, st, a, heads, out);
+  const bool f8 = a.ck_scale != nullptr;
+  if (dt == DT::BF16) {
+    if (f8) hipLaunchKernelGGL((cross_scores_kernel<DT::BF16, true>), grid, dim3(256), 0, st, a, heads, out);
+    else hipLaunchKernelGGL((cross_scores_kernel<DT::BF16, false>), grid, dim3(256), 0, st, a, heads, out);
+  } else {
+    if (f8) hipLaunchKernelGGL((cross_scores_kernel<DT::F16, true>), grid, dim3(256), 0, st, a, heads, out);
+    else hipLaunchKernelGGL((cross_scores_kernel<DT::F16, false>), grid, dim3(256), 0, st, a, heads, out);
+  }
   WMX_HIP(hipGetLastError());
 }
 

@@ -237,6 +237,30 @@ __device__ __host__ inline int mx8_exp(float amax) {
   return e < -126 ? -126 : (e > 126 ? 126 : e);
 }
 __device__ inline float mx8_inv_scale(int e) { return __int_as_float((127 - e) << 23); }  // 2^-e, exact
+// eight e4m3 bytes (two dwords, little-endian) -> eight 16-bit MFMA operand values.  Exact: every e4m3 value is a
+// bf16 and an f16 value (v_cvt_scalef32_pk_{bf16,f16}_fp8 with scale 1; the row / image scale is applied outside)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <DT T> __device__ inline u16x8 fp8x8_to16(uint32_t a, uint32_t b);
+template <> __device__ inline u16x8 fp8x8_to16<DT::BF16>(uint32_t a, uint32_t b) {
+  const u32x4 r = {__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(a, 1.0f, false)),
+                   __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(a, 1.0f, true)),
+                   __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(b, 1.0f, false)),
+                   __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(b, 1.0f, true))};
+  return __builtin_bit_cast(u16x8, r);
+}
+template <> __device__ inline u16x8 fp8x8_to16<DT::F16>(uint32_t a, uint32_t b) {
+  const u32x4 r = {__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(a, 1.0f, false)),
+                   __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(a, 1.0f, true)),
+                   __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(b, 1.0f, false)),
+                   __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(b, 1.0f, true))};
+  return __builtin_bit_cast(u16x8, r);
+}
+// 16 e4m3 bytes of one lane -> the two 8-element operands they hold (bytes 0..7, bytes 8..15)
+template <DT T> __device__ inline void fp8x16_to16(const u32x4& w, u16x8& lo, u16x8& hi) {
+  lo = fp8x8_to16<T>(w[0], w[1]);
+  hi = fp8x8_to16<T>(w[2], w[3]);
+}
+
 // four values (already divided by the block scale) -> four e4m3 bytes, little-endian in one dword
 __device__ inline uint32_t mx8_pack4(float a, float b, float c, float d) {
   int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);

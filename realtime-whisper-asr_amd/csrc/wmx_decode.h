@@ -16,6 +16,11 @@ struct RuleOpts {
   float inv_temp = 0.f;
   const uint32_t* seed = nullptr;
   const int* slot = nullptr;
+  // non-finite guard: a row whose normaliser is not finite or that has no candidate (NaN / -inf logits) records
+  // 1 + row + 1024 * slot in *err (the first one wins, compare-and-swap from 0); the host turns it into
+  // WMX_ERR_NUMERIC.  The row's token still becomes EOT, so no id outside the vocabulary reaches the embedding
+  int* err = nullptr;
+  const int* err_slot = nullptr;
 };
 
 struct RowPtrs {  // per-row decode state (device arrays of R)
@@ -50,7 +55,8 @@ void launch_beam_step(const RowPtrs& rp, const RowPtrs& tmp, const int* ctok, co
                       int max_cand, int tb, int eot, int* slot, int* hist, int* hist_tmp, int* anc, int* anc_tmp, int ld,
                       const BeamState& bs, int* n_done, hipStream_t st);
 void launch_lang_detect(const float* logits, int ldl, int lang0, int nlang, int nwin, int K, int* hist, int hist_ld,
-                        const int* lang_slot, int* lang_out, float* prob_out, hipStream_t st);
+                        const int* lang_slot, int* lang_out, float* prob_out, hipStream_t st,
+                        int* err = nullptr);
 void launch_token_prob(const float* logits, int ldl, int V, int token, int rows, float* out, hipStream_t st);
 void launch_text_prob(const float* logits, int ldl, int eot, const int* target, int rows, float* out, hipStream_t st);
 // parity instrumentation (wmx_ctx_record)

@@ -424,6 +424,8 @@ __global__ __launch_bounds__(64) void logits_select_b(const float* __restrict__ 
     // vocabulary likewise, so a non-finite row can end a hypothesis but never reach the embedding gather
     const bool none = bi < 0 || bi >= o.V;
     out_tok[r * KP + lane] = none ? o.eot : bi;
+    if (lane == 0 && o.err && (none || !(fabsf(lse_all) < INFINITY)))
+      atomicCAS(o.err, 0, 1 + r + 1024 * (o.err_slot ? *o.err_slot : 0));
     if (SAMPLE) {  // bv is the sampling key: the log-probability comes from the raw logit of the drawn token
       const int lrow = row_map ? row_map[r] : r;
       out_lp[r * KP + lane] = none ? -INFINITY : logits[(long)lrow * ldl + bi] - lse_all;
@@ -592,9 +594,11 @@ __global__ __launch_bounds__(kBeamUpdThreads) void beam_update_kernel(RowState r
 
 // language detection: argmax over language tokens of the logits at <|startoftranscript|>; writes the token into
 // the prompt of every row of the window
+// (no finite language logit -- a NaN upstream: language 0 is written, so no id outside the vocabulary reaches the
+// prefill's embedding gather, and the non-finite guard word gets -(1 + window), WMX_ERR_NUMERIC on the host)
 __global__ void lang_detect_kernel(const float* __restrict__ logits, int ldl, int lang0, int nlang, int K,
                                    int* __restrict__ hist, int hist_ld, const int* __restrict__ lang_slot,
-                                   int* __restrict__ lang_out, float* __restrict__ prob_out) {
+                                   int* __restrict__ lang_out, float* __restrict__ prob_out, int* __restrict__ err) {
   const int w = blockIdx.x;
   const float* x = logits + (long)w * ldl + lang0;
   const int lane = threadIdx.x;
@@ -613,6 +617,10 @@ __global__ void lang_detect_kernel(const float* __restrict__ logits, int ldl, in
       bv = v2;
       bi = i2;
     }
+  }
+  if (bi < 0 || bi >= nlang) {  // (wave-uniform: every lane holds the reduced pair)
+    bi = 0;
+    if (lane == 0 && err) atomicCAS(err, 0, -(1 + w));
   }
   float s = 0.f;
   for (int i = lane; i < nlang; i += 64) s += __expf(x[i] - bv);
@@ -918,9 +926,9 @@ void launch_beam_step(const RowPtrs& rp, const RowPtrs& tmp, const int* ctok, co
 }
 
 void launch_lang_detect(const float* logits, int ldl, int lang0, int nlang, int nwin, int K, int* hist, int hist_ld,
-                        const int* lang_slot, int* lang_out, float* prob_out, hipStream_t st) {
+                        const int* lang_slot, int* lang_out, float* prob_out, hipStream_t st, int* err) {
   hipLaunchKernelGGL(lang_detect_kernel, dim3(nwin), dim3(64), 0, st, logits, ldl, lang0, nlang, K, hist, hist_ld,
-                     lang_slot, lang_out, prob_out);
+                     lang_slot, lang_out, prob_out, err);
   WMX_HIP(hipGetLastError());
 }
 

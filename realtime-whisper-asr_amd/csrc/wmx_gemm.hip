@@ -1774,6 +1774,11 @@ constexpr int packed_ku() {
   return (MT + NCT) <= 3 ? 5 : (MT + NCT) <= 8 ? 2 : 1;
 #endif
 }
+// 8-bit weights: a k-step is 64 deep (one 16-byte weight piece + two A fragments per 16-row tile)
+template <int MT, int NCT>
+constexpr int packed_ku8() {
+  return (MT + NCT) <= 3 ? 3 : (MT + NCT) <= 6 ? 2 : 1;
+}
 
 // S == 1 epilogues of the LayerNorm-folded decode step (wmx_common.h row_ln_from_stats): the residual producer
 // (x += acc + bias, its 16-bit copy and per-16-column statistics) and the folded-LN + GELU consumer (fc1).
@@ -1838,13 +1843,17 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
 // partials + the in-launch reduce / LayerNorm tail (RedTail)
 enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2, kPackedTail = 3 };
 
-template <DT T, int MT, int NCT, int NW, int EPK>
+// W8: the weights are e4m3 bytes in the packed8_index layout with per-row scales wsc (a k-step is 64 deep: the
+// same 16-byte lane load as a bf16 k-step, widened in registers into the B fragments of two MFMAs; the row scale
+// multiplies the reduced fp32 tile before any epilogue or partial store)
+template <DT T, int MT, int NCT, int NW, int EPK, bool W8 = false>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
                                                               int S, Epi e, float* __restrict__ part, RedTail rt,
                                                               unsigned long long* __restrict__ tprobe,
-                                                              const int* __restrict__ pslot) {
-  constexpr int KU = packed_ku<MT, NCT>();
+                                                              const int* __restrict__ pslot,
+                                                              const float* __restrict__ wsc) {
+  constexpr int KU = W8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>();
   constexpr int LDR = 16 * NCT + 1;
   constexpr bool TAIL = EPK == kPackedTail;
   constexpr int NT = 64 * NW;
@@ -1857,14 +1866,17 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   const int t0 = blockIdx.x * NCT;
   const int sp = blockIdx.y;
   const int m0 = blockIdx.z * MT * 16;
-  const int ksteps = K >> 5;
+  const int ksteps = W8 ? K >> 6 : K >> 5;
   int ks0, ks1;
-  packed_wave_ksteps(K, S, NW, sp, wave, ks0, ks1);
+  packed_wave_ksteps(W8 ? K >> 1 : K, S, NW, sp, wave, ks0, ks1);
   // kPackedGelu: a thread's column quad is the same in every row it stores (NT is a multiple of 4 NCT), so its
-  // bias is loaded now, beside the first k-step batch, not as a round trip after the reduction barrier
+  // bias is loaded now, beside the first k-step batch, not as a round trip after the reduction barrier (the 8-bit
+  // row scales likewise; the scale array is padded to whole 16-row tiles)
   float4 pbias = make_float4(0.f, 0.f, 0.f, 0.f);
   if constexpr (EPK == kPackedGelu)
     pbias = *reinterpret_cast<const float4*>(e.bias + min(t0 * 16 + (tid % (4 * NCT)) * 4, N - 4));
+  float4 wsc4 = make_float4(1.f, 1.f, 1.f, 1.f);
+  if constexpr (W8) wsc4 = *reinterpret_cast<const float4*>(wsc + min(t0 * 16 + (tid % (4 * NCT)) * 4, ntiles * 16 - 4));
   f32x4 acc[MT][NCT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -1877,7 +1889,38 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   const uint16_t* ar[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) ar[i] = A + packed_a_elem(m0 + i * 16 + fr, M, lda, 0, lane);
-  for (int kk = ks0; kk < ks1; kk += KU) {
+  if constexpr (W8) {
+    for (int kk = ks0; kk < ks1; kk += KU) {
+      u32x4 b[KU][NCT];
+      u16x8 av[KU][MT][2];
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int k = min(kk + u, ks1 - 1);  // clamped: a duplicate load of the wave's last k-step, MFMA skipped
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) b[u][j] = stream_load(reinterpret_cast<const u32x4*>(wt[j] + ((long)k << 9)));
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          av[u][i][0] = *reinterpret_cast<const u16x8*>(ar[i] + k * 64);
+          av[u][i][1] = *reinterpret_cast<const u16x8*>(ar[i] + k * 64 + 32);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < KU; ++u)
+        if (kk + u < ks1)
+#pragma unroll
+          for (int j = 0; j < NCT; ++j) {
+            u16x8 blo, bhi;
+            fp8x16_to16<T>(b[u][j], blo, bhi);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+              acc[i][j] = mfma16<T>(av[u][i][0], blo, acc[i][j]);
+              acc[i][j] = mfma16<T>(av[u][i][1], bhi, acc[i][j]);
+            }
+          }
+    }
+  }
+  for (int kk = ks0; !W8 && kk < ks1; kk += KU) {
     u16x8 b[KU][NCT], av[KU][MT];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
@@ -1927,7 +1970,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   // 4 consecutive columns per thread
   constexpr int C4 = 4 * NCT;  // column quads per row
   bool fold_epi = false;
-  if constexpr (EPK == kPackedGeneric) {
+  if constexpr (EPK == kPackedGeneric && !W8) {  // (the folded step has no 8-bit form: host-checked)
     fold_epi = S == 1 && (e.kind == EPI_RESID_STATS || e.kind == EPI_LNFOLD_GELU16);
     if (fold_epi) packed_fold_epilogue<T, MT, NCT, NW>(red, e, M, N, K, m0, t0);
   }
@@ -1942,6 +1985,12 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
 #pragma unroll
       for (int w = 1; w < NW; ++w) v += red[w][row][c + q];
       v4[q] = v;
+    }
+    if constexpr (W8) {
+      v4[0] *= wsc4.x;
+      v4[1] *= wsc4.y;
+      v4[2] *= wsc4.z;
+      v4[3] *= wsc4.w;
     }
     if constexpr (TAIL) {  // write-through (sc1) so the last arriver on another XCD reads them without an L2 release
       tail_st4(tail_rsrc(part), ((long)sp * M + m) * N + n, make_float4(v4[0], v4[1], v4[2], v4[3]));
@@ -2025,19 +2074,20 @@ static int packed_nw(int K, int S) {
   return 16;
 }
 
-template <DT T, int MT, int NCT>
+template <DT T, int MT, int NCT, bool W8>
 static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ntiles = (g.N + 15) / 16;
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
-  const int nw = packed_nw<MT, NCT>(g.K, g.S);
+  // (8-bit weights: waves per workgroup from the 64-deep k-steps of the slice)
+  const int nw = packed_nw<MT, NCT>(W8 ? g.K / 2 : g.K, g.S);
   const bool tail = g.tail.cnt != nullptr;
   const int epk = tail ? kPackedTail
                  : g.S > 1 ? kPackedPart
                  : (g.epi.kind == EPI_GELU16 && g.epi.bias && g.N % 4 == 0 && g.epi.ldc % 4 == 0) ? kPackedGelu
                                                                                                  : kPackedGeneric;
 #define WMX_PACKED_EPK(NWV, EPKV)                                                                                  \
-  hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, EPKV>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W, g.M, \
-                     g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot)
+  hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, EPKV, W8>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W,  \
+                     g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot, g.wscale)
 #define WMX_PACKED_LAUNCH(NWV)                                                                                     \
   do {                                                                                                             \
     switch (epk) {                                                                                                 \
@@ -2061,40 +2111,41 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
 }
 
 template <int MT, int NCT>
-static PackedPlan plan_cfg(int M, int N, int K, int S) {
-  return PackedPlan{MT, NCT, packed_nw<MT, NCT>(K, S), packed_ku<MT, NCT>(), ((N + 15) / 16 + NCT - 1) / NCT,
-                    (M + MT * 16 - 1) / (MT * 16)};
+static PackedPlan plan_cfg(int M, int N, int K, int S, bool w8) {
+  return PackedPlan{MT, NCT, packed_nw<MT, NCT>(w8 ? K / 2 : K, S), w8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>(),
+                    ((N + 15) / 16 + NCT - 1) / NCT, (M + MT * 16 - 1) / (MT * 16)};
 }
 
 template <int NCT>
-static PackedPlan plan_mt(int M, int N, int K, int S) {
+static PackedPlan plan_mt(int M, int N, int K, int S, bool w8) {
   switch ((std::min(M, 128) + 15) / 16) {  // launch_packed_mt's dispatch
-    case 1: return plan_cfg<1, NCT>(M, N, K, S);
-    case 2: return plan_cfg<2, NCT>(M, N, K, S);
-    case 3: return plan_cfg<3, NCT>(M, N, K, S);
-    case 4: return plan_cfg<4, NCT>(M, N, K, S);
+    case 1: return plan_cfg<1, NCT>(M, N, K, S, w8);
+    case 2: return plan_cfg<2, NCT>(M, N, K, S, w8);
+    case 3: return plan_cfg<3, NCT>(M, N, K, S, w8);
+    case 4: return plan_cfg<4, NCT>(M, N, K, S, w8);
     case 5:
-    case 6: return plan_cfg<6, 2>(M, N, K, S);
-    default: return plan_cfg<4, 2>(M, N, K, S);
+    case 6: return plan_cfg<6, 2>(M, N, K, S, w8);
+    default: return plan_cfg<4, 2>(M, N, K, S, w8);
   }
 }
 
-PackedPlan packed_plan(int M, int N, int K, int S, int nct) {
+PackedPlan packed_plan(int M, int N, int K, int S, int nct, bool w8) {
   const int c = nct ? nct : packed_nct(M, N, K);
-  return c == 4 ? plan_mt<4>(M, N, K, S) : c == 1 ? plan_mt<1>(M, N, K, S) : plan_mt<2>(M, N, K, S);
+  return c == 4 ? plan_mt<4>(M, N, K, S, w8) : c == 1 ? plan_mt<1>(M, N, K, S, w8) : plan_mt<2>(M, N, K, S, w8);
 }
 
 // walks every lane of every wave of every workgroup of the launch through the kernel's own index helpers
-PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct) {
-  const PackedPlan p = packed_plan(M, N, K, S, nct);
-  const int ntiles = (N + 15) / 16, ksteps = K / 32;
+// (w8: w_end in BYTES of the packed8 weights, k-steps 64 deep reading A fragments 2k and 2k + 1)
+PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct, bool w8) {
+  const PackedPlan p = packed_plan(M, N, K, S, nct, w8);
+  const int ntiles = (N + 15) / 16, ksteps = w8 ? K / 64 : K / 32;
   PackedExtent e{0, 0, 0, 0};
   for (int bx = 0; bx < p.gx; ++bx)
     for (int sp = 0; sp < S; ++sp)
       for (int bz = 0; bz < p.gz; ++bz)
         for (int wave = 0; wave < p.NW; ++wave) {
           int ks0, ks1;
-          packed_wave_ksteps(K, S, p.NW, sp, wave, ks0, ks1);
+          packed_wave_ksteps(w8 ? K / 2 : K, S, p.NW, sp, wave, ks0, ks1);
           for (int kk = ks0; kk < ks1; kk += p.KU)
             for (int u = 0; u < p.KU; ++u) {
               const int k = std::min(kk + u, ks1 - 1);  // the kernel's clamped load index
@@ -2103,9 +2154,11 @@ PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct) {
               // lane 63 bounds the wave
               for (int lane = 63; lane < 64; lane += 1) {
                 for (int j = 0; j < p.NCT; ++j)
-                  e.w_end = std::max(e.w_end, packed_w_elem(bx * p.NCT + j, ntiles, ksteps, k, lane) + 8);
+                  e.w_end = std::max(e.w_end, w8 ? 2 * packed_w_elem(bx * p.NCT + j, ntiles, ksteps, k, lane) + 16
+                                                 : packed_w_elem(bx * p.NCT + j, ntiles, ksteps, k, lane) + 8);
                 for (int i = 0; i < p.MT; ++i)
-                  e.a_end = std::max(e.a_end, packed_a_elem(bz * p.MT * 16 + i * 16 + (lane & 15), M, lda, k, lane) + 8);
+                  e.a_end = std::max(e.a_end, packed_a_elem(bz * p.MT * 16 + i * 16 + (lane & 15), M, lda,
+                                                            w8 ? 2 * k + 1 : k, lane) + 8);
               }
             }
           if (S > 1)  // partial stores: rows < M, column quads < N
@@ -2118,18 +2171,24 @@ PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct) {
   return e;
 }
 
-template <DT T, int NCT>
+template <DT T, int NCT, bool W8>
 static void launch_packed_mt(const PackedCall& g, hipStream_t st) {
   const int mt = (std::min(g.M, 128) + 15) / 16;
   switch (mt) {
-    case 1: launch_packed_cfg<T, 1, NCT>(g, st); break;
-    case 2: launch_packed_cfg<T, 2, NCT>(g, st); break;
-    case 3: launch_packed_cfg<T, 3, NCT>(g, st); break;
-    case 4: launch_packed_cfg<T, 4, NCT>(g, st); break;
+    case 1: launch_packed_cfg<T, 1, NCT, W8>(g, st); break;
+    case 2: launch_packed_cfg<T, 2, NCT, W8>(g, st); break;
+    case 3: launch_packed_cfg<T, 3, NCT, W8>(g, st); break;
+    case 4: launch_packed_cfg<T, 4, NCT, W8>(g, st); break;
     case 5:
-    case 6: launch_packed_cfg<T, 6, 2>(g, st); break;
-    default: launch_packed_cfg<T, 4, 2>(g, st); break;  // 7..8 row tiles: 64-row chunks (LDS budget)
+    case 6: launch_packed_cfg<T, 6, 2, W8>(g, st); break;
+    default: launch_packed_cfg<T, 4, 2, W8>(g, st); break;  // 7..8 row tiles: 64-row chunks (LDS budget)
   }
+}
+template <DT T, bool W8>
+static void launch_packed_nct(int nct, const PackedCall& g, hipStream_t st) {
+  if (nct == 4) launch_packed_mt<T, 4, W8>(g, st);
+  else if (nct == 1) launch_packed_mt<T, 1, W8>(g, st);
+  else launch_packed_mt<T, 2, W8>(g, st);
 }
 
 // the tail's reducers and its single normalising workgroup: S <= 8 slices, rows of <= 5 quads per lane, one
@@ -2158,15 +2217,17 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
                  (g.epi.kind == EPI_LNFOLD_GELU16 ? (g.epi.c1 && g.epi.c2 && g.K % 16 == 0 && g.K <= 2048)
                                                   : (g.epi.out16 != nullptr && g.N <= 2048))),
             "packed gemm: folded-LayerNorm epilogue arguments");
+  const bool w8 = g.wscale != nullptr;
+  WMX_CHECK(!w8 || (g.K % 64 == 0 && g.tail.cnt == nullptr && g.epi.kind != EPI_RESID_STATS &&
+                    g.epi.kind != EPI_LNFOLD_GELU16),
+            "packed gemm: 8-bit weights need K % 64 == 0 and no folded-LayerNorm / in-launch tail epilogue");
   const int nct = g.nct ? g.nct : packed_nct(g.M, g.N, g.K);
   if (dt == DT::BF16) {
-    if (nct == 4) launch_packed_mt<DT::BF16, 4>(g, st);
-    else if (nct == 1) launch_packed_mt<DT::BF16, 1>(g, st);
-    else launch_packed_mt<DT::BF16, 2>(g, st);
+    if (w8) launch_packed_nct<DT::BF16, true>(nct, g, st);
+    else launch_packed_nct<DT::BF16, false>(nct, g, st);
   } else {
-    if (nct == 4) launch_packed_mt<DT::F16, 4>(g, st);
-    else if (nct == 1) launch_packed_mt<DT::F16, 1>(g, st);
-    else launch_packed_mt<DT::F16, 2>(g, st);
+    if (w8) launch_packed_nct<DT::F16, true>(nct, g, st);
+    else launch_packed_nct<DT::F16, false>(nct, g, st);
   }
   WMX_HIP(hipGetLastError());
 }
@@ -2455,10 +2516,13 @@ static void launch_t(const GemmCall& g, hipStream_t st) {
     WMX_CHECK(g.epi.kind != EPI_CROSSKV || (g.epi.d % 256 == 0 && g.epi.xt % 4 == 0), "gemm256: cross K/V shape");
     const bool lns = g.epi.kind == EPI_RESID32_LNS || g.epi.kind == EPI_GELU_POS32_LNS;
     const bool lnf = g.epi.kind == EPI_LNF_STORE16 || g.epi.kind == EPI_LNF_GELU16;
-    WMX_CHECK(!lns || (g.N % 256 == 0 && g.epi.ldc % 4 == 0 && g.epi.out16 && g.epi.stats && g.epi.stats_ld >= g.M),
+    WMX_CHECK(!lns || (g.N % 256 == 0 && g.epi.ldc % 256 == 0 && g.epi.out16 && g.epi.stats && g.epi.stats_ld >= g.M),
               "gemm256: LayerNorm-statistics epilogue shape");
+    // the consumer's statistics DMA reads 16-byte (mean, M2) pairs at rows min(m0 + 2 lane, M - 2): M and the
+    // statistics stride even; the fold is LayerNorm over exactly the GEMM's K (lng groups of 256 columns)
     WMX_CHECK(!lnf || (g.N % 4 == 0 && g.epi.ldc % 4 == 0 && g.epi.c1 && g.epi.bias && g.epi.stats &&
-                       g.epi.lng >= 1 && g.epi.lng <= 8 && g.epi.stats_ld >= g.M),
+                       g.epi.lng >= 1 && g.epi.lng <= 8 && g.epi.stats_ld >= g.M && g.M % 2 == 0 &&
+                       g.epi.stats_ld % 2 == 0 && g.K == 256 * g.epi.lng),
               "gemm256: LayerNorm-folded epilogue shape");
     launch_g256<T>(g, st);
     return;

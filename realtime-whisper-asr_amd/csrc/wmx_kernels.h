@@ -72,6 +72,19 @@ __host__ __device__ inline long crossv_off(int t, int c) {
   const int db = c >> 4, fr = c & 15;
   return (((long)kb * 4 + db) * 64 + fr + 16 * g) * 8 + (t & 7);
 }
+// byte offsets of the same elements in the fp8 images (launch_crosskv_quant): 16-bit piece P = (2 blk + hh) 64 + l
+// (8 elements) sits at bytes (blk 64 + l) 16 + 8 hh
+__host__ __device__ inline long crossk8_off(int t, int c) {
+  const int kb = t >> 5, tt = t & 31;
+  const int u = (tt >> 2) & 1, fr = ((tt >> 3) << 2) | (tt & 3);
+  const int hh = c >> 5, g = (c >> 3) & 3;
+  return (((long)kb * 2 + u) * 64 + fr + 16 * g) * 16 + hh * 8 + (c & 7);
+}
+__host__ __device__ inline long crossv8_off(int t, int c) {
+  const int kb = t >> 5, g = (t >> 3) & 3;
+  const int db = c >> 4, fr = c & 15;
+  return (((long)kb * 2 + (db >> 1)) * 64 + fr + 16 * g) * 16 + (db & 1) * 8 + (t & 7);
+}
 
 enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3, TILE_256 = 4 };
 
@@ -120,6 +133,28 @@ void launch_layernorm_mx8(const float* x, const float* g, const float* b, uint8_
 __host__ __device__ inline long packed_index(long n, long k, long K) {
   return (((n >> 4) * (K >> 5) + (k >> 5)) << 9) + (((n & 15) + 16 * ((k & 31) >> 3)) << 3) + (k & 7);
 }
+// ---- 8-bit decoder weights (model dtype WMX_DTYPE_MX8, the fp8 decode of BASELINE config 5) ----
+// e4m3 bytes, one power-of-two scale per weight ROW (the OCP MX rule of mx8_exp with the block = the whole K row),
+// stored as tiles of 16 rows x 64 k (1 KiB): tile (n/16, k/64) at byte ((n/16)*(K/64) + k/64)*1024; inside it lane
+// l = (n%16) + 16*((k%32)/8) holds 16 bytes: k%64 in [0, 32) at bytes 0..7 and k%64 in [32, 64) at bytes 8..15
+// (k%8 = 0..7 each).  One wave's 16-byte load is then the B fragments of two consecutive 32-deep MFMA k-steps,
+// exactly the bf16 packed layout's lanes: the bytes are widened to the 16-bit operand in registers
+// (fp8x16_to16) and the row scale multiplies the fp32 result in the epilogue.
+__host__ __device__ inline long packed8_index(long n, long k, long K) {
+  return (((n >> 4) * (K >> 6) + (k >> 6)) << 10) + (((n & 15) + 16 * ((k & 31) >> 3)) << 4) + (((k >> 5) & 1) << 3) +
+         (k & 7);
+}
+// src: a packed 16-bit [N][K] matrix (packed_index) -> q8 (packed8_index, N padded to 16 rows), scale[n] = 2^e_n
+// (N padded entries 0), and optionally rm = the dequantized row-major [N][K] 16-bit copy (many-row passes)
+void launch_w8_quantize(DT dt, const uint16_t* src, int N, int K, uint8_t* q8, float* scale, uint16_t* rm,
+                        hipStream_t st);
+// fp8 cross K / V^T images: per (layer, kv, window, head) image one power-of-two scale (mx8_exp of the image's
+// amax); the 16-byte lane piece p = blk*64 + l of an fp8 image holds the bf16 image's pieces (2 blk + 0)*64 + l and
+// (2 blk + 1)*64 + l, i.e. for K both dim halves of one key pair (u) and for V^T two dim blocks of one key block:
+// one 1 KiB wave load per (32-key block, pair u) of K and per (32-key block, dim-block pair) of V^T.
+// src / dst images [L*2][xw][H] of kXS*64 elements; windows [0, B) converted; scale [L*2][xw][H]
+void launch_crosskv_quant(const uint16_t* src, uint8_t* dst, float* scale, int L2, int xw, int B, int H,
+                          hipStream_t st);
 
 // C[M][N] = A[M][K] . Wp^T.  S == 1: epilogue applied in-kernel.  S > 1: K is split over S workgroup slices and
 // each writes raw fp32 partials part[s][M][N] (no bias); the consumer sums them in slice order (deterministic).
@@ -137,10 +172,11 @@ struct RedTail {
 struct PackedCall {
   const uint16_t* A;
   long lda;
-  const uint16_t* W;  // packed
+  const uint16_t* W;  // packed (packed_index), or with wscale the e4m3 bytes (packed8_index)
   int M, N, K;
   int S = 1;
   Epi epi;
+  const float* wscale = nullptr;  // 8-bit weights: per-row scales (result = scale[n] * acc, before the epilogue)
   float* part = nullptr;
   RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
   // in-situ probe: [slot][workgroup][start, end] wall-clock ticks (probe_record) at slot *pslot, or null
@@ -154,7 +190,7 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st);
 struct PackedPlan {
   int MT, NCT, NW, KU, gx, gz;
 };
-PackedPlan packed_plan(int M, int N, int K, int S, int nct = 0);
+PackedPlan packed_plan(int M, int N, int K, int S, int nct = 0, bool w8 = false);
 // decode MLP in one launch (fc1 + bias + GELU -> fc2 split-K partials, the edge handed off in-launch):
 // part[8][M][d] raw fc2 partials (no bias) for reduce_ln, h [M][4d] the GELU(fc1) rows (write-through),
 // cnt: kMlpCounters zeroed ints per context (8 monotonic slice counters + an error word set on a poll timeout)
@@ -196,7 +232,7 @@ __host__ __device__ inline long packed_a_elem(int row, int M, long lda, int kste
 struct PackedExtent {
   long w_end, a_end, part_end, stray_ksteps;
 };
-PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct = 0);
+PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct = 0, bool w8 = false);
 // whether a partial-output launch of this shape can carry the RedTail; counters the tail needs
 bool packed_tail_ok(int M, int N, int K, int S);
 constexpr int packed_tail_counters() { return 4096; }
@@ -233,13 +269,13 @@ void launch_cvt16_to_f32(DT dt, const uint16_t* in, float* out, long n, hipStrea
 // x[r*Tn+i] = tok_emb[hist[r*hist_ld + slot]] + pos_emb[slot - pad[r]],  slot = *slot0 + i
 // tok_emb is packed (packed_index), pos_emb row-major
 void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R, int Tn,
-                  const int* pad, const int* slot0, int d, float* x, hipStream_t st);
+                  const int* pad, const int* slot0, int d, float* x, hipStream_t st, int V);
 // row-major [N][K] copy of a packed matrix
 void launch_unpack_packed(const uint16_t* packed, uint16_t* rowmajor, int N, int K, hipStream_t st);
 // decode step (Tn == 1): x = embed, out16 = LN(x) * g + b, in one launch
 void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
                      const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,
-                     hipStream_t st, float2* stats = nullptr, long stats_ld = 0);
+                     hipStream_t st, int V, float2* stats = nullptr, long stats_ld = 0);
 // one wave idles on the stream for `ticks` device wall-clock ticks (a phase offset between context groups)
 void launch_spin(unsigned long long ticks, hipStream_t st);
 // LayerNorm (g, b) folded into the projection W (+ bias): packed Wp = W diag(g), c1 = Wp 1, c2 = bias + W b
@@ -316,6 +352,11 @@ struct DecAttnArgs {
   const uint16_t* wq = nullptr;
   const uint16_t* qin = nullptr;
   long qin_ld = 0;
+  const float* wq_scale = nullptr;  // wq is 8-bit (packed8_index) with these per-row scales
+  // fp8 cross K / V^T images (launch_crosskv_quant layout): ck / cv point at e4m3 bytes, x_wstride / x_hstride
+  // stay in elements, and the (window w, head h) image's scales are ck_scale / cv_scale[w * H + h]
+  const float* ck_scale = nullptr;
+  const float* cv_scale = nullptr;
   int win_of_row_div;  // row -> window = row / rows_per_win
 };
 void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);

@@ -271,6 +271,119 @@ void launch_mx8_quantize_rows(DT dt, const uint16_t* src, long rows, int K, uint
   WMX_HIP(hipGetLastError());
 }
 
+// ---------------- 8-bit decoder weights (fp8 decode, model dtype MX8): one wave per weight row ----------------
+// e = mx8_exp(max |row|) (the OCP MX rule with the block = the whole K row), q = RNE e4m3(w / 2^e) in the
+// packed8_index layout, scale[n] = 2^e; rm (optional) = the dequantized row-major 16-bit copy (exact: an e4m3 value
+// times a power of two is a bf16 / f16 value), which the many-row passes (prefill, alignment) run on so that every
+// pass of the fp8 model sees the same weights.  oracle/whisper_np.py w8_rows restates the rule.
+template <DT T>
+__global__ __launch_bounds__(256) void w8_quantize_kernel(const uint16_t* __restrict__ src, int N, int Np, int K,
+                                                          uint8_t* __restrict__ q8, float* __restrict__ scale,
+                                                          uint16_t* __restrict__ rm) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= Np) return;  // (wave-uniform)
+  float am = 0.f;
+  for (int k = 8 * lane; k < K; k += 512) {
+    const u16x8 h = *reinterpret_cast<const u16x8*>(src + packed_index(n, k, K));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(to_f32<T>(h[e])));
+  }
+  am = wave_max(am);
+  const int ex = mx8_exp(am);
+  const float is = mx8_inv_scale(ex), sc = __int_as_float((127 + ex) << 23);
+  for (int k = 8 * lane; k < K; k += 512) {
+    const u16x8 h = *reinterpret_cast<const u16x8*>(src + packed_index(n, k, K));
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = to_f32<T>(h[e]) * is;
+    const uint2 b = make_uint2(mx8_pack4(v[0], v[1], v[2], v[3]), mx8_pack4(v[4], v[5], v[6], v[7]));
+    *reinterpret_cast<uint2*>(q8 + packed8_index(n, k, K)) = b;
+    if (rm && n < N) {
+      const u16x8 d = fp8x8_to16<T>(b.x, b.y);
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = from_f32<T>(to_f32<T>(d[e]) * sc);
+      *reinterpret_cast<u16x8*>(rm + (long)n * K + k) = o;
+    }
+  }
+  if (lane == 0) scale[n] = n < N ? sc : 0.f;
+}
+
+void launch_w8_quantize(DT dt, const uint16_t* src, int N, int K, uint8_t* q8, float* scale, uint16_t* rm,
+                        hipStream_t st) {
+  WMX_CHECK(K % 64 == 0 && N >= 1, "w8 quantize: K must be a multiple of 64");
+  const int Np = (N + 15) / 16 * 16;
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(w8_quantize_kernel<DT::BF16>, dim3(cdiv(Np, 4)), dim3(256), 0, st, src, N, Np, K, q8, scale, rm);
+  else
+    hipLaunchKernelGGL(w8_quantize_kernel<DT::F16>, dim3(cdiv(Np, 4)), dim3(256), 0, st, src, N, Np, K, q8, scale, rm);
+  WMX_HIP(hipGetLastError());
+}
+
+// ---------------- fp8 cross K / V^T images (fp8 decode): one 1024-thread workgroup per (layer-kv, window, head) image ---
+// The image (192 KB of 16-bit values) is read ONCE into registers: wave w owns the fp8 piece blocks blk = w + 16 i
+// (94 blocks of 64 pieces), and lane l loads the two 16-bit pieces (2 blk + hh) 64 + l, hh = 0, 1, that fp8 piece
+// blk 64 + l is packed from (12 pieces of 16 B per thread).  The image amax is reduced over the workgroup -> e =
+// mx8_exp (one power-of-two scale per image), then each lane packs and stores its pieces.  The zero pad keys stay zero.
+// oracle/whisper_np.py kv8_images restates the rule.
+template <DT T>
+__global__ __launch_bounds__(1024) void crosskv_quant_kernel(const uint16_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                             float* __restrict__ scale, int xw, int H) {
+  constexpr int kPieces = kXS * 64 / 16;  // fp8 pieces of one image (6016 = 94 blocks of 64)
+  constexpr int kIt = (kPieces / 64 + 15) / 16;  // blocks per wave (16 waves): 6
+  const int h = blockIdx.x, w = blockIdx.y, z = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long img = ((long)z * xw + w) * H + h;
+  const u16x8* s = reinterpret_cast<const u16x8*>(src + img * kXS * 64);
+  u16x8 a[kIt], b[kIt];
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int blk = wave + 16 * i;
+    const bool ok = blk < kPieces / 64;
+    const long p0 = 2L * min(blk, kPieces / 64 - 1) * 64 + lane;
+    a[i] = s[p0];
+    b[i] = s[p0 + 64];
+    if (ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) am = fmaxf(am, fmaxf(fabsf(to_f32<T>(a[i][e])), fabsf(to_f32<T>(b[i][e]))));
+    }
+  }
+  __shared__ float red[16];
+  am = wave_max(am);
+  if (lane == 0) red[wave] = am;
+  __syncthreads();
+  am = red[0];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) am = fmaxf(am, red[k]);
+  const int ex = mx8_exp(am);
+  const float is = mx8_inv_scale(ex);
+  uint8_t* d = dst + img * kXS * 64;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int blk = wave + 16 * i;
+    if (blk >= kPieces / 64) break;  // (wave-uniform)
+    u32x4 o;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      o[q] = mx8_pack4(to_f32<T>(a[i][4 * q]) * is, to_f32<T>(a[i][4 * q + 1]) * is, to_f32<T>(a[i][4 * q + 2]) * is,
+                       to_f32<T>(a[i][4 * q + 3]) * is);
+      o[2 + q] = mx8_pack4(to_f32<T>(b[i][4 * q]) * is, to_f32<T>(b[i][4 * q + 1]) * is,
+                           to_f32<T>(b[i][4 * q + 2]) * is, to_f32<T>(b[i][4 * q + 3]) * is);
+    }
+    *reinterpret_cast<u32x4*>(d + ((long)blk * 64 + lane) * 16) = o;
+  }
+  if (tid == 0) scale[img] = __int_as_float((127 + ex) << 23);
+}
+
+void launch_crosskv_quant(const uint16_t* src, uint8_t* dst, float* scale, int L2, int xw, int B, int H,
+                          hipStream_t st) {
+  WMX_CHECK(B >= 1 && B <= xw && L2 >= 1 && H >= 1, "cross K/V quantize: shape");
+  static_assert(kXS * 64 / 16 % 64 == 0, "whole 64-piece blocks per image");
+  hipLaunchKernelGGL(crosskv_quant_kernel<DT::BF16>, dim3(H, B, L2), dim3(1024), 0, st, src, dst, scale, xw, H);
+  WMX_HIP(hipGetLastError());
+}
+
 // ---------------- conv1 im2col: out[b*3000+t][kk*M + c] = mel[b][c][t+kk-1] (0 outside / in the K pad) ----------------
 template <DT T>
 __global__ __launch_bounds__(256) void im2col1_kernel(const float* __restrict__ mel, int B, int M, int Kp,
@@ -350,11 +463,12 @@ template <DT T>
 __global__ __launch_bounds__(256) void embed_kernel(const uint16_t* __restrict__ tok_emb, const uint16_t* __restrict__ pos_emb,
                                                     const int* __restrict__ hist, long hist_ld, int Tn,
                                                     const int* __restrict__ pad, const int* __restrict__ slot0, int d,
-                                                    float* __restrict__ x) {
+                                                    float* __restrict__ x, int V) {
   const int m = blockIdx.x;
   const int r = m / Tn, i = m - r * Tn;
   const int slot = *slot0 + i;
-  const int tok = hist[(long)r * hist_ld + slot];
+  // (clamped into the table: a token id is never an address outside it, whatever reached the history)
+  const int tok = min(max(hist[(long)r * hist_ld + slot], 0), V - 1);
   int pos = slot - (pad ? pad[r] : 0);
   pos = max(pos, 0);
   for (int c = threadIdx.x; c < d; c += 256)
@@ -362,13 +476,13 @@ __global__ __launch_bounds__(256) void embed_kernel(const uint16_t* __restrict__
 }
 
 void launch_embed(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R, int Tn,
-                  const int* pad, const int* slot0, int d, float* x, hipStream_t st) {
+                  const int* pad, const int* slot0, int d, float* x, hipStream_t st, int V) {
   if (dt == DT::BF16)
     hipLaunchKernelGGL(embed_kernel<DT::BF16>, dim3(R * Tn), dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, Tn, pad,
-                       slot0, d, x);
+                       slot0, d, x, V);
   else
     hipLaunchKernelGGL(embed_kernel<DT::F16>, dim3(R * Tn), dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, Tn, pad,
-                       slot0, d, x);
+                       slot0, d, x, V);
   WMX_HIP(hipGetLastError());
 }
 
@@ -400,12 +514,12 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const uint16_t* __restric
                                                        const int* __restrict__ slot0, const float* __restrict__ g,
                                                        const float* __restrict__ bb, int rows, int d,
                                                        float* __restrict__ x, uint16_t* __restrict__ out,
-                                                       float2* __restrict__ stats, long stats_ld) {
+                                                       float2* __restrict__ stats, long stats_ld, int V) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wave;
   if (r >= rows) return;
   const int slot = *slot0;
-  const int tok = hist[(long)r * hist_ld + slot];
+  const int tok = min(max(hist[(long)r * hist_ld + slot], 0), V - 1);  // (clamped into the table, as embed_kernel)
   const int pos = max(slot - (pad ? pad[r] : 0), 0);
   const int n4 = d >> 2;
   float4 v[8];  // d <= 2048
@@ -473,15 +587,15 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const uint16_t* __restric
 
 void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
                      const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,
-                     hipStream_t st, float2* stats, long stats_ld) {
-  WMX_CHECK(d % 32 == 0 && d <= 2048 && (!stats || d % 64 == 0), "embed_ln: d");
+                     hipStream_t st, int V, float2* stats, long stats_ld) {
+  WMX_CHECK(d % 32 == 0 && d <= 2048 && (!stats || d % 64 == 0) && V >= 1, "embed_ln: d");
   dim3 grid(cdiv(R, 4));
   if (dt == DT::BF16)
     hipLaunchKernelGGL(embed_ln_kernel<DT::BF16>, grid, dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, pad, slot0,
-                       g, b, R, d, x, out, stats, stats_ld);
+                       g, b, R, d, x, out, stats, stats_ld, V);
   else
     hipLaunchKernelGGL(embed_ln_kernel<DT::F16>, grid, dim3(256), 0, st, tok_emb, pos_emb, hist, hist_ld, pad, slot0,
-                       g, b, R, d, x, out, stats, stats_ld);
+                       g, b, R, d, x, out, stats, stats_ld, V);
   WMX_HIP(hipGetLastError());
 }
 

@@ -134,6 +134,10 @@ struct DecLayer {
   // load): packed W diag(g) of qkv (LN1), cross-q (LN2), fc1 (LN3) and their c1 = W' 1, c2 = bias + W b
   uint16_t *fqkv, *fcq, *ffc1;
   float *c1qkv, *c2qkv, *c1cq, *c2cq, *c1fc1, *c2fc1;
+  // fp8 decode (Model::w8): e4m3 copies of the six packed projections (packed8_index) + per-row scales, derived
+  // after every weight load (launch_w8_quantize); the row-major copies above then hold their dequantized values
+  uint8_t *q8qkv = nullptr, *q8o = nullptr, *q8cq = nullptr, *q8co = nullptr, *q8fc1 = nullptr, *q8fc2 = nullptr;
+  float *s8qkv = nullptr, *s8o = nullptr, *s8cq = nullptr, *s8co = nullptr, *s8fc1 = nullptr, *s8fc2 = nullptr;
 };
 
 struct Model {
@@ -141,6 +145,13 @@ struct Model {
   int device = 0;
   DT dt = DT::BF16;
   bool mx8 = false;  // encoder projections on MX-fp8 MFMA (BASELINE config 5); everything else in `dt`
+  // fp8 decode (model dtype MX8 unless WMX_DEC_FP8=0): the decoder projections and the logits projection on 8-bit
+  // weights (DecLayer::q8*, tok8), the cross K / V images in fp8 (Ctx::ckv8); the embedding lookup, LayerNorms,
+  // biases, the self-attention KV cache and all activations stay 16-bit / fp32
+  bool w8 = false;
+  uint8_t* tok8 = nullptr;  // the token embedding as the logits projection's 8-bit weights (packed8_index)
+  float* tok8s = nullptr;
+  size_t param_bytes = 0;  // the arena's parameter region [0, param_bytes): what a weight broadcast must carry
   char* arena = nullptr;
   size_t arena_bytes = 0;
   int K1p = 0;
@@ -184,12 +195,14 @@ static void build_model(Model& m) {
             "model: head_dim must be 64 and width a multiple of 64");
   WMX_CHECK(d.n_audio_ctx == 1500 && d.n_text_ctx <= 448 && M <= 128, "model: unsupported context sizes");
   m.K1p = (3 * M + 63) / 64 * 64;
+  // the parameter region first (every TensorEntry destination: what a checkpoint or a weight broadcast fills),
+  // then everything derived from it on each rank (positions, MX-fp8 / folded / row-major / 8-bit copies, log-mel
+  // constants), so a broadcast of [0, param_bytes) is all a rank needs before wmx_model_arena_loaded
   Planner P;
   P.add(&m.conv1w, (size_t)da * m.K1p);
   P.add(&m.conv1b, da);
   P.add(&m.conv2w, (size_t)da * 3 * da);
   P.add(&m.conv2b, da);
-  P.add(&m.enc_pos, (size_t)1500 * da);
   m.enc.resize(d.n_audio_layer);
   for (auto& L : m.enc) {
     P.add(&L.ln1g, da);
@@ -205,31 +218,10 @@ static void build_model(Model& m) {
     P.add(&L.wfc2, (size_t)4 * da * da);
     P.add(&L.bfc2, da);
   }
-  if (m.mx8) {
-    WMX_CHECK(da % 128 == 0, "model: MX-fp8 encoder needs a width multiple of 128");
-    for (auto& L : m.enc) {
-      P.add(&L.qkv8, (size_t)3 * da * da);
-      P.add(&L.qkv8s, (size_t)3 * da * da / 32);
-      P.add(&L.o8, (size_t)da * da);
-      P.add(&L.o8s, (size_t)da * da / 32);
-      P.add(&L.fc18, (size_t)4 * da * da);
-      P.add(&L.fc18s, (size_t)4 * da * da / 32);
-      P.add(&L.fc28, (size_t)4 * da * da);
-      P.add(&L.fc28s, (size_t)4 * da * da / 32);
-    }
-  }
-  for (auto& L : m.enc) {
-    if (!m.enc_fold) break;
-    P.add(&L.fqkv, (size_t)3 * da * da);
-    P.add(&L.ffc1, (size_t)4 * da * da);
-    P.add(&L.c1qkv, 3 * da);
-    P.add(&L.c2qkv, 3 * da);
-    P.add(&L.c1fc1, 4 * da);
-    P.add(&L.c2fc1, 4 * da);
-  }
   P.add(&m.lnpg, da);
   P.add(&m.lnpb, da);
-  P.add(&m.tok_emb, (size_t)(V + 15) / 16 * 16 * dt);  // packed: rows padded to a 16-row tile
+  const int Vp = (V + 15) / 16 * 16;
+  P.add(&m.tok_emb, (size_t)Vp * dt);  // packed: rows padded to a 16-row tile
   P.add(&m.dec_pos, (size_t)d.n_text_ctx * dt);
   m.dec.resize(d.n_text_layer);
   for (auto& L : m.dec) {
@@ -252,6 +244,35 @@ static void build_model(Model& m) {
     P.add(&L.wfc2, (size_t)4 * dt * dt);
     P.add(&L.bfc2, dt);
   }
+  P.add(&m.wckv, (size_t)d.n_text_layer * 2 * dt * dt);
+  P.add(&m.bckv, (size_t)d.n_text_layer * 2 * dt);
+  P.add(&m.lng, dt);
+  P.add(&m.lnb, dt);
+  P.add(&m.enc_pos, (size_t)1500 * da);  // (settable: encoder.embed_positions.weight)
+  m.param_bytes = P.off;
+  // ---- derived on every rank ----
+  if (m.mx8) {
+    WMX_CHECK(da % 128 == 0, "model: MX-fp8 encoder needs a width multiple of 128");
+    for (auto& L : m.enc) {
+      P.add(&L.qkv8, (size_t)3 * da * da);
+      P.add(&L.qkv8s, (size_t)3 * da * da / 32);
+      P.add(&L.o8, (size_t)da * da);
+      P.add(&L.o8s, (size_t)da * da / 32);
+      P.add(&L.fc18, (size_t)4 * da * da);
+      P.add(&L.fc18s, (size_t)4 * da * da / 32);
+      P.add(&L.fc28, (size_t)4 * da * da);
+      P.add(&L.fc28s, (size_t)4 * da * da / 32);
+    }
+  }
+  for (auto& L : m.enc) {
+    if (!m.enc_fold) break;
+    P.add(&L.fqkv, (size_t)3 * da * da);
+    P.add(&L.ffc1, (size_t)4 * da * da);
+    P.add(&L.c1qkv, 3 * da);
+    P.add(&L.c2qkv, 3 * da);
+    P.add(&L.c1fc1, 4 * da);
+    P.add(&L.c2fc1, 4 * da);
+  }
   for (auto& L : m.dec) {
     if (!m.fold) break;  // the folded copies exist only for the opt-in folded step (WMX_FOLD=1)
     P.add(&L.fqkv, (size_t)3 * dt * dt);
@@ -272,10 +293,25 @@ static void build_model(Model& m) {
     P.add(&L.rfc1, (size_t)4 * dt * dt);
     P.add(&L.rfc2, (size_t)4 * dt * dt);
   }
-  P.add(&m.wckv, (size_t)d.n_text_layer * 2 * dt * dt);
-  P.add(&m.bckv, (size_t)d.n_text_layer * 2 * dt);
-  P.add(&m.lng, dt);
-  P.add(&m.lnb, dt);
+  if (m.w8) {
+    WMX_CHECK(dt % 64 == 0, "model: the fp8 decode needs a text width multiple of 64");
+    for (auto& L : m.dec) {
+      P.add(&L.q8qkv, (size_t)3 * dt * dt);
+      P.add(&L.s8qkv, (size_t)3 * dt);
+      P.add(&L.q8o, (size_t)dt * dt);
+      P.add(&L.s8o, (size_t)dt);
+      P.add(&L.q8cq, (size_t)dt * dt);
+      P.add(&L.s8cq, (size_t)dt);
+      P.add(&L.q8co, (size_t)dt * dt);
+      P.add(&L.s8co, (size_t)dt);
+      P.add(&L.q8fc1, (size_t)4 * dt * dt);
+      P.add(&L.s8fc1, (size_t)4 * dt);
+      P.add(&L.q8fc2, (size_t)4 * dt * dt);
+      P.add(&L.s8fc2, (size_t)dt);
+    }
+    P.add(&m.tok8, (size_t)Vp * dt);
+    P.add(&m.tok8s, (size_t)Vp);
+  }
   // log-mel constants
   P.add(&m.mel_basis, (size_t)400 * 416);
   P.add(&m.mel_first, M);
@@ -454,6 +490,24 @@ static void prepare_mx8(Model& m) {
   WMX_HIP(hipStreamSynchronize(m.st));
 }
 
+// fp8 decode: the 8-bit copies of the decoder projections and of the logits projection (the token embedding), and
+// the row-major copies overwritten with the dequantized weights, so that the many-row passes (prefill, alignment)
+// run the same model as the decode step (after prepare_rowmajor; deterministic)
+static void prepare_w8(Model& m) {
+  if (!m.w8) return;
+  const int dt = m.d.n_text_state;
+  for (auto& L : m.dec) {
+    launch_w8_quantize(m.dt, L.wqkv, 3 * dt, dt, L.q8qkv, L.s8qkv, L.rqkv, m.st);
+    launch_w8_quantize(m.dt, L.wo, dt, dt, L.q8o, L.s8o, L.ro, m.st);
+    launch_w8_quantize(m.dt, L.wcq, dt, dt, L.q8cq, L.s8cq, L.rcq, m.st);
+    launch_w8_quantize(m.dt, L.wco, dt, dt, L.q8co, L.s8co, L.rco, m.st);
+    launch_w8_quantize(m.dt, L.wfc1, 4 * dt, dt, L.q8fc1, L.s8fc1, L.rfc1, m.st);
+    launch_w8_quantize(m.dt, L.wfc2, dt, 4 * dt, L.q8fc2, L.s8fc2, L.rfc2, m.st);
+  }
+  launch_w8_quantize(m.dt, m.tok_emb, m.d.n_vocab, dt, m.tok8, m.tok8s, nullptr, m.st);
+  WMX_HIP(hipStreamSynchronize(m.st));
+}
+
 // ------------------------------------------------------------------------------------------------
 // context
 // ------------------------------------------------------------------------------------------------
@@ -498,6 +552,9 @@ struct Ctx {
   int* wmax = nullptr;
   uint16_t *im1 = nullptr, *h1 = nullptr, *im2 = nullptr, *ehb = nullptr, *eqkv = nullptr, *eao = nullptr, *ef1 = nullptr,
            *enc_out = nullptr, *ckv = nullptr;
+  // fp8 decode: the cross K / V^T images in e4m3 (launch_crosskv_quant of ckv) + one scale per image [L*2][maxB][H]
+  uint8_t* ckv8 = nullptr;
+  float* ckv8s = nullptr;
   // MX-fp8 encoder operands: e4m3 [rows][K] + e8m0 scales [rows][K/32] (LN out, attention out, fc1 out)
   uint8_t *eh8 = nullptr, *eh8s = nullptr, *ea8 = nullptr, *ea8s = nullptr, *ef8 = nullptr, *ef8s = nullptr;
   float* ex = nullptr;
@@ -527,6 +584,7 @@ struct Ctx {
   int* xa_cnt = nullptr;
   int* red_cnt = nullptr;  // RedTail arrival counters (packed GEMM with in-launch reduce + LayerNorm)
   int* mlp_cnt = nullptr;  // fused-MLP slice counters + error word (launch_mlp_fused)
+  int* nf_err = nullptr;   // non-finite decode guard (RuleOpts::err): 0, or 1 + row + 1024 * slot of the first hit
   uint32_t* mask = nullptr;
   // alignment
   float *scores = nullptr, *align_out = nullptr, *tprob = nullptr;
@@ -619,6 +677,10 @@ static void alloc_ctx(Ctx& c) {
     P.add(&c.ef8s, (size_t)B * 1500 * 4 * da / 32);
   }
   P.add(&c.ckv, (size_t)B * kXS * Lt * 2 * dt);  // K and V^T images, key stride kXS (pad stays zero)
+  if (c.m->w8) {
+    P.add(&c.ckv8, (size_t)B * kXS * Lt * 2 * dt);
+    P.add(&c.ckv8s, (size_t)Lt * 2 * B * d.n_text_head);
+  }
   const int DR = c.dec_rows_max;
   P.add(&c.dx, (size_t)DR * dt);
   P.add(&c.dhb, (size_t)DR * dt);
@@ -675,6 +737,7 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
   P.add(&c.red_cnt, (size_t)packed_tail_counters());
   P.add(&c.mlp_cnt, (size_t)kMlpCounters);
+  P.add(&c.nf_err, 4);
   P.add(&c.probe_buf, (size_t)kProbeLaunches * T * kProbeWG * 2);
   P.add(&c.mask, (V + 31) / 32);
   P.add(&c.scores, (size_t)heads_per_layer * B * T * 1500);
@@ -772,17 +835,27 @@ static Epi epi(int kind, const float* bias, void* out, long ldc) {
 
 // decoder projection: packed weights (decode, few rows), or the row-major copy on the tiled MFMA GEMM when there
 // are many rows (prompt prefill, word alignment: the packed kernel would re-read the weights per 64-row chunk)
+// An 8-bit weight (fp8 decode): q8 (packed8_index) + per-row scales s8; the packed kernel then reads q8 instead of Wp.
+struct W8 {
+  const uint8_t* q8 = nullptr;
+  const float* s8 = nullptr;
+};
+static void set_w(PackedCall& g, const uint16_t* Wp, W8 w8) {
+  g.W = w8.q8 ? reinterpret_cast<const uint16_t*>(w8.q8) : Wp;
+  g.wscale = w8.q8 ? w8.s8 : nullptr;
+}
+
 static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, const Epi& e,
-                   const uint16_t* Wrm = nullptr) {
+                   const uint16_t* Wrm = nullptr, W8 w8 = {}) {
   static const bool packed_only = getenv("WMX_PREFILL_PACKED") != nullptr;  // A/B switch for tuning runs
-  if (Wrm && M > 256 && !packed_only) {
+  if (Wrm && M > 256 && !packed_only) {  // (fp8 decode: Wrm holds the dequantized 8-bit weights)
     gemm(c, A, lda, Wrm, K, M, N, K, e);
     return;
   }
   PackedCall g;
   g.A = A;
   g.lda = lda;
-  g.W = Wp;
+  set_w(g, Wp, w8);
   g.M = M;
   g.N = N;
   g.K = K;
@@ -794,11 +867,11 @@ static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int 
 }
 
 // decoder projection on packed weights, split-K raw partials into c.part; returns the split count
-static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K) {
+static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, W8 w8 = {}) {
   PackedCall g;
   g.A = A;
   g.lda = lda;
-  g.W = Wp;
+  set_w(g, Wp, w8);
   g.M = M;
   g.N = N;
   g.K = K;
@@ -817,13 +890,14 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
 // decoder projection whose split-K partials feed x += bias + sum; out16 = LN(x) (reduce_ln): one packed launch
 // carrying the reduction and the LayerNorm when the shape allows (RedTail), else the GEMM and reduce_ln
 static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K,
-                         const float* bias, const float* g, const float* b, unsigned long long* redprobe = nullptr) {
+                         const float* bias, const float* g, const float* b, unsigned long long* redprobe = nullptr,
+                         W8 w8 = {}) {
   // opt-in (WMX_REDLN_FUSED): measured slower than the separate reduce_ln launch, 798 vs 587 ms per call on the
   // default bench -- the in-launch chain (sc1 partial loads, write-through x, a second arrival, the single
   // normalising workgroup's row loads) costs ~10 us more than the kernel boundary it removes
   static const bool fused = getenv("WMX_REDLN_FUSED") != nullptr;
   const int S = packed_splits(M, N, K, c.part_elems);
-  if (fused && packed_tail_ok(M, N, K, S)) {
+  if (fused && !w8.q8 && packed_tail_ok(M, N, K, S)) {
     PackedCall p;
     p.A = A;
     p.lda = lda;
@@ -842,7 +916,7 @@ static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp
     launch_gemm_packed(c.dt, p, c.st);
     return;
   }
-  const int S2 = gemm_p_part(c, A, lda, Wp, M, N, K);
+  const int S2 = gemm_p_part(c, A, lda, Wp, M, N, K, w8);
   c.cur_probe = nullptr;
   launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st, redprobe, c.slot);
 }
@@ -1022,6 +1096,28 @@ static const uint16_t* cross_v(const Ctx& c, int l) {
   return c.ckv + (size_t)(2 * l + 1) * c.maxB * kXS * c.m->d.n_text_state;
 }
 
+// the cross-attention images of layer l on a decoder-attention call: the 16-bit images, or (fp8 decode) the e4m3
+// images and their per-(window, head) scales
+static void set_cross_images(const Ctx& c, DecAttnArgs& a, int l) {
+  const Model& m = *c.m;
+  a.x_wstride = (long)kXS * m.d.n_text_state;
+  a.x_hstride = (long)kXS * 64;
+  if (m.w8) {
+    const size_t img = (size_t)c.maxB * kXS * m.d.n_text_state;  // bytes per (layer, kv) block of images
+    const size_t nsc = (size_t)c.maxB * m.d.n_text_head;
+    a.ck = reinterpret_cast<const uint16_t*>(c.ckv8 + (2 * l) * img);
+    a.cv = reinterpret_cast<const uint16_t*>(c.ckv8 + (2 * l + 1) * img);
+    a.ck_scale = c.ckv8s + (2 * l) * nsc;
+    a.cv_scale = c.ckv8s + (2 * l + 1) * nsc;
+  } else {
+    a.ck = cross_k(c, l);
+    a.cv = cross_v(c, l);
+  }
+}
+
+// the 8-bit copy of a decoder projection (fp8 decode), or none
+static W8 w8_of(const Model& m, const uint8_t* q, const float* s) { return m.w8 ? W8{q, s} : W8{}; }
+
 static void cross_kv(Ctx& c, int B) {
   Model& m = *c.m;
   const int dt = m.d.n_text_state, Lt = m.d.n_text_layer;
@@ -1031,6 +1127,9 @@ static void cross_kv(Ctx& c, int B) {
   e.xw = c.maxB;
   e.xt = 1500;
   gemm(c, c.enc_out, dt, m.wckv, dt, B * 1500, Lt * 2 * dt, dt, e);
+  // fp8 decode: every (layer-kv, window, head) image to e4m3 with its own power-of-two scale (once per call; the
+  // decode steps then stream half the bytes)
+  if (m.w8) launch_crosskv_quant(c.ckv, c.ckv8, c.ckv8s, 2 * Lt, c.maxB, B, m.d.n_text_head, c.st);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1060,7 +1159,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
   const int R = f.rows;
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
   launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, m.dec[0].ln1g, m.dec[0].ln1b, dt,
-                  c.dx, c.dhb, c.st);
+                  c.dx, c.dhb, c.st, m.d.n_vocab);
   const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
@@ -1071,7 +1170,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     auto pbuf = [&](int id) { return probed ? c.probe_buf + id * probe_stride : nullptr; };
     // self attention: QKV partials -> (reduce, cache write, attention) -> out-proj partials -> +x, LN2
     probe(kProbeQKV);
-    int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt);
+    int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt, w8_of(m, L.q8qkv, L.s8qkv));
     c.cur_probe = nullptr;
     DecAttnArgs a{};
     a.o = c.dao;
@@ -1094,12 +1193,12 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     a.tprobe = pbuf(kProbeSelf);
     launch_self_attn(c.dt, a, c.st);
     probe(kProbeOut);
-    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut));
+    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut), w8_of(m, L.q8o, L.s8o));
     // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3; with c.xq_fused the
     // cross attention projects its own queries from LN2(x) (no cross-q launch)
     if (!c.xq_fused) {
       probe(kProbeCrossQ);
-      S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt);
+      S = gemm_p_part(c, c.dhb, dt, L.wcq, R, dt, dt, w8_of(m, L.q8cq, L.s8cq));
       c.cur_probe = nullptr;
     }
     DecAttnArgs x{};
@@ -1108,10 +1207,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.Tn = 1;
     x.H = H;
     x.d = dt;
-    x.ck = cross_k(c, l);
-    x.cv = cross_v(c, l);
-    x.x_wstride = (long)kXS * dt;
-    x.x_hstride = (long)kXS * 64;
+    set_cross_images(c, x, l);
     x.Tk = 1500;
     x.rows_per_win = f.win_rows > 0 ? f.win_rows : c.K;
     x.qpart = c.part;
@@ -1121,7 +1217,8 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.qbias = L.bcq;
     if (c.xq_fused) {
       x.qS = 0;
-      x.wq = L.wcq;
+      x.wq = m.w8 ? reinterpret_cast<const uint16_t*>(L.q8cq) : L.wcq;
+      x.wq_scale = m.w8 ? L.s8cq : nullptr;
       x.qin = c.dhb;
       x.qin_ld = dt;
     }
@@ -1130,7 +1227,8 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
     launch_cross_attn(c.dt, x, c.xa_ws, c.st);
     probe(kProbeCrossOut);
-    gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b, pbuf(kProbeRedCrossOut));
+    gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b, pbuf(kProbeRedCrossOut),
+                 w8_of(m, L.q8co, L.s8co));
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
     if (c.mlp_fused && mlp_fused_ok(R, dt)) {  // one launch for fc1 -> fc2 (its span is recorded as the fc1 probe), then reduce_ln
       MlpCall mc;
@@ -1153,11 +1251,13 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
       continue;
     }
     probe(kProbeFc1);
-    gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt));
+    gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), nullptr,
+           w8_of(m, L.q8fc1, L.s8fc1));
     probe(kProbeFc2);
     gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
                  last ? m.lnb : m.dec[l + 1].ln1b,
-                 probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr);
+                 probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr,
+                 w8_of(m, L.q8fc2, L.s8fc2));
     c.cur_probe = nullptr;
   }
 }
@@ -1209,7 +1309,7 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
   const int R = f.rows;
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
   launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, nullptr, nullptr, dt, c.dx, c.dhb,
-                  c.st, c.rstat, R);
+                  c.st, m.d.n_vocab, c.rstat, R);
   debug_sync(c, "embed", -1);
   const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
   for (int l = 0; l < Lt; ++l) {
@@ -1314,7 +1414,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
   const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
   const int rowsT = f.rows * f.Tn;
   WMX_CHECK(rowsT <= c.dec_rows_max, "decoder: too many rows");
-  launch_embed(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, f.rows, f.Tn, f.pad_seq, c.slot, dt, c.dx, c.st);
+  launch_embed(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, f.rows, f.Tn, f.pad_seq, c.slot, dt, c.dx, c.st, m.d.n_vocab);
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
   for (int l = 0; l < Lt; ++l) {
     DecLayer& L = m.dec[l];
@@ -1329,7 +1429,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
     eq.slot0 = c.slot;
     eq.kc = kcl;
     eq.vc = vcl;
-    gemm_p(c, c.dhb, dt, L.wqkv, rowsT, 3 * dt, dt, eq, L.rqkv);
+    gemm_p(c, c.dhb, dt, L.wqkv, rowsT, 3 * dt, dt, eq, L.rqkv, w8_of(m, L.q8qkv, L.s8qkv));
     if (f.prefill) {
       AttnArgs a{};
       a.q = c.dq;
@@ -1366,11 +1466,9 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.slot0 = c.slot;
       launch_self_attn(c.dt, a, c.st);
     }
-    gemm_p(c, c.dao, dt, L.wo, rowsT, dt, dt, epi(EPI_RESID32, L.bo, c.dx, dt), L.ro);
+    gemm_p(c, c.dao, dt, L.wo, rowsT, dt, dt, epi(EPI_RESID32, L.bo, c.dx, dt), L.ro, w8_of(m, L.q8o, L.s8o));
     launch_layernorm(c.dt, c.dx, L.ln2g, L.ln2b, c.dhb, rowsT, dt, c.st);
-    gemm_p(c, c.dhb, dt, L.wcq, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt), L.rcq);
-    const uint16_t* ckl = cross_k(c, l);
-    const uint16_t* cvl = cross_v(c, l);
+    gemm_p(c, c.dhb, dt, L.wcq, rowsT, dt, dt, epi(EPI_STORE16, L.bcq, c.dcq, dt), L.rcq, w8_of(m, L.q8cq, L.s8cq));
     {
       DecAttnArgs a{};
       a.q = c.dcq;
@@ -1380,10 +1478,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.Tn = f.Tn;
       a.H = H;
       a.d = dt;
-      a.ck = ckl;
-      a.cv = cvl;
-      a.x_wstride = (long)kXS * dt;
-      a.x_hstride = (long)kXS * 64;
+      set_cross_images(c, a, l);
       a.Tk = 1500;
       // prefill: one sequence per window; decode through this path: the beams of a window share it
       a.rows_per_win = f.prefill ? 1 : c.K;
@@ -1404,10 +1499,7 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         a.Tn = f.Tn;
         a.H = H;
         a.d = dt;
-        a.ck = ckl;
-        a.cv = cvl;
-        a.x_wstride = (long)kXS * dt;
-        a.x_hstride = (long)kXS * 64;
+        set_cross_images(c, a, l);
         a.Tk = 1500;
         a.rows_per_win = 1;
         launch_cross_scores(c.dt, a, c.a_heads, (int)hs.size(), c.scores, c.st);
@@ -1417,10 +1509,12 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         sync(c);
       }
     }
-    gemm_p(c, c.dao, dt, L.wco, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt), L.rco);
+    gemm_p(c, c.dao, dt, L.wco, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt), L.rco, w8_of(m, L.q8co, L.s8co));
     launch_layernorm(c.dt, c.dx, L.ln3g, L.ln3b, c.dhb, rowsT, dt, c.st);
-    gemm_p(c, c.dhb, dt, L.wfc1, rowsT, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), L.rfc1);
-    gemm_p(c, c.df1, 4 * dt, L.wfc2, rowsT, dt, 4 * dt, epi(EPI_RESID32, L.bfc2, c.dx, dt), L.rfc2);
+    gemm_p(c, c.dhb, dt, L.wfc1, rowsT, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), L.rfc1,
+           w8_of(m, L.q8fc1, L.s8fc1));
+    gemm_p(c, c.df1, 4 * dt, L.wfc2, rowsT, dt, 4 * dt, epi(EPI_RESID32, L.bfc2, c.dx, dt), L.rfc2,
+           w8_of(m, L.q8fc2, L.s8fc2));
   }
 }
 
@@ -1431,7 +1525,8 @@ static void dec_logits(Ctx& c, const int* rows_idx, int n, bool ln_done = false)
   const int dt = m.d.n_text_state, V = m.d.n_vocab;
   WMX_CHECK(n <= c.logits_rows, "logits: too many rows");
   if (!ln_done) launch_layernorm_rows(c.dt, c.dx, rows_idx, m.lng, m.lnb, c.dhb, n, dt, c.st);
-  gemm_p(c, c.dhb, dt, m.tok_emb, n, V, dt, epi(EPI_STORE32, nullptr, c.logits, c.ldl));
+  gemm_p(c, c.dhb, dt, m.tok_emb, n, V, dt, epi(EPI_STORE32, nullptr, c.logits, c.ldl), nullptr,
+         w8_of(m, m.tok8, m.tok8s));
 }
 
 static void set_slot(Ctx& c, int v) {
@@ -1531,6 +1626,8 @@ static void select_and_update(Ctx& c, int B, const int* row_map) {
     launch_record_logits(c.logits, c.ldl, m.d.n_vocab, R, row_map, c.slot, c.rec_base, c.rec_cap, c.rec_logits, c.st);
   RuleOpts ro{m.d.n_vocab, c.sp.eot, c.sp.timestamp_begin, c.sp.no_timestamps, c.sp.blank, c.o.suppress_blank,
               c.o.max_initial_timestamp_index, c.o.without_timestamps, c.mask};
+  ro.err = c.nf_err;
+  ro.err_slot = c.slot;
   if (c.sampling) {
     ro.inv_temp = 1.0f / c.o.temperature;
     ro.seed = reinterpret_cast<const uint32_t*>(c.slot + 2);  // written per call (transcribe prologue)
@@ -1610,6 +1707,7 @@ static void ensure_prepared(Model& m) {
   if (!m.dirty || !m.initialized) return;
   prepare_mx8(m);
   prepare_rowmajor(m);
+  prepare_w8(m);
   prepare_fold(m);
   m.dirty = false;
 }
@@ -1622,6 +1720,10 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   WMX_CHECK(B >= 1 && B <= c.maxB, "transcribe: batch exceeds max_batch");
   const int K = c.K, R = K * B, V = m.d.n_vocab, T = c.Tctx;
   const Special& sp = c.sp;
+  // per-call device words: the non-finite guard, and the fused MLP's slice counters + timeout word (zeroed every
+  // call, so the monotonic counters never approach 2^32 and a timeout fails only the call it happened in)
+  WMX_HIP(hipMemsetAsync(c.nf_err, 0, 4, c.st));
+  WMX_HIP(hipMemsetAsync(c.mlp_cnt, 0, (size_t)kMlpCounters * 4, c.st));
   rec(c, 0);
   logmel_dev(c, pcm_dev, stride, lens, seek, B, c.mel);
   rec(c, 1);
@@ -1714,7 +1816,8 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
       dec_forward(c, f);
       dec_logits(c, nullptr, B);
     }
-    launch_lang_detect(c.logits, c.ldl, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st);
+    launch_lang_detect(c.logits, c.ldl, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st,
+                       c.nf_err);
     debug_sync(c, "lang_detect", -1);
   }
   rec(c, 4);
@@ -1771,13 +1874,14 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   if (c.probe_kernel >= 0)  // per-workgroup records of this call only (read after the timed region)
     WMX_HIP(hipMemsetAsync(c.probe_buf, 0, (size_t)kProbeLaunches * T * kProbeWG * 2 * 8, c.st));
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
-    const double d = m.d.n_text_state, w2 = 2.0, r = R;
-    auto proj = [&](double n, double k) { return n * k * w2 + r * k * w2 + r * n * w2; };
+     // (fp8 decode: weights and cross K/V images at 1 byte per element; activations stay 16-bit)
+    const double d = m.d.n_text_state, w2 = 2.0, r = R, ww = m.w8 ? 1.0 : 2.0;
+    auto proj = [&](double n, double k) { return n * k * ww + r * k * w2 + r * n * w2; };
     // (fused cross-q: the cross attention also streams the d x d query weights and reads the LN2 rows)
     const bool xqf = c.xq_fused && !m.fold;  // (the folded step keeps its cross-q launch)
-    const double xq = xqf ? d * d * w2 + r * d * w2 : 0.0;
+    const double xq = xqf ? d * d * ww + r * d * w2 : 0.0;
     const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), xqf ? 0.0 : proj(d, d), proj(d, d),
-                                      proj(4 * d, d), proj(d, 4 * d), (double)B * 1500 * 2 * d * w2 + 2.0 * r * d * w2 + xq};
+                                      proj(4 * d, d), proj(d, 4 * d), (double)B * 1500 * 2 * d * ww + 2.0 * r * d * w2 + xq};
     for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
   if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
@@ -1804,6 +1908,8 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   // ---- read back and finalise (openai BeamSearchDecoder.finalize + MaximumLikelihoodRanker) ----
   std::vector<int> h((size_t)R * T), ns(R), done(R);
   std::vector<float> slp(R), nosp(B);
+  int nf_err = 0;
+  WMX_HIP(hipMemcpyAsync(&nf_err, c.nf_err, 4, hipMemcpyDeviceToHost, c.st));
   WMX_HIP(hipMemcpyAsync(h.data(), c.hist, h.size() * 4, hipMemcpyDeviceToHost, c.st));
   WMX_HIP(hipMemcpyAsync(ns.data(), c.rp.ns, R * 4, hipMemcpyDeviceToHost, c.st));
   WMX_HIP(hipMemcpyAsync(done.data(), c.rp.done, R * 4, hipMemcpyDeviceToHost, c.st));
@@ -1824,6 +1930,14 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     WMX_HIP(hipMemcpyAsync(fh.data(), c.bs.fin_hist, fh.size() * 4, hipMemcpyDeviceToHost, c.st));
   }
   sync(c);
+  if (nf_err < 0)
+    throw Error(WMX_ERR_NUMERIC, "non-finite decoder logits in language detection, window " + std::to_string(-nf_err - 1));
+  if (nf_err != 0) {  // a NaN / inf anywhere upstream of the logits: an error, not a silently shortened transcript
+    const int code = nf_err - 1, row = code % 1024, slot = code / 1024;
+    throw Error(WMX_ERR_NUMERIC, "non-finite decoder logits at decode step " + std::to_string(slot - (Pmax - 1)) +
+                                     " (slot " + std::to_string(slot) + "), row " + std::to_string(row) +
+                                     " (window " + std::to_string(row / K) + ")");
+  }
   auto* res = new ResultHolder();
   res->data.resize(B);
   res->win.resize(B);
@@ -2077,9 +2191,14 @@ wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_mod
       w->m.device = device;
       w->m.dt = dtype == WMX_DTYPE_F16 ? DT::F16 : DT::BF16;
       w->m.mx8 = dtype == WMX_DTYPE_MX8;
+      {  // the fp8 decode of the MX8 model (WMX_DEC_FP8=0: encoder-only MX-fp8, the round-3 model, for A/B runs)
+        const char* df = getenv("WMX_DEC_FP8");
+        w->m.w8 = w->m.mx8 && !(df && df[0] == '0');
+      }
       // opt-in (WMX_FOLD=1): the LayerNorm-folded decode step passes every parity test but measured slower than
-      // the split-K + reduce_ln step (356-390 vs 389-393x real time, interleaved on one box)
-      w->m.fold = getenv("WMX_FOLD") != nullptr;
+      // the split-K + reduce_ln step (356-390 vs 389-393x real time, interleaved on one box); it has
+      // no 8-bit form (the fp8 decode ignores the switch)
+      w->m.fold = getenv("WMX_FOLD") != nullptr && !w->m.w8;
       {
         const char* ef = getenv("WMX_ENC_FOLD");
         w->m.enc_fold = !w->m.mx8 && w->m.d.n_audio_state % 256 == 0 && !(ef && ef[0] == '0');
@@ -2127,6 +2246,8 @@ wmx_status wmx_model_init_synthetic(wmx_model* w, uint64_t seed) {
     prepare_mx8(m);
     prepare_rowmajor(m);
     debug_device("prepare_rowmajor");
+    prepare_w8(m);
+    debug_device("prepare_w8");
     prepare_fold(m);
     debug_device("prepare_fold");
     m.initialized = true;
@@ -2222,7 +2343,7 @@ int64_t wmx_model_n_params(const wmx_model* w) {
 wmx_status wmx_model_arena(wmx_model* w, void** ptr, size_t* bytes) {
   return guard([&] {
     *ptr = w->m.arena;
-    *bytes = w->m.arena_bytes;
+    *bytes = w->m.param_bytes;  // the parameter region (build_model: the derived copies follow it)
   });
 }
 
@@ -2231,6 +2352,7 @@ wmx_status wmx_model_arena_loaded(wmx_model* w) {
     WMX_HIP(hipSetDevice(w->m.device));
     prepare_mx8(w->m);
     prepare_rowmajor(w->m);
+    prepare_w8(w->m);
     prepare_fold(w->m);
     w->m.initialized = true;
     w->m.dirty = false;
@@ -2305,7 +2427,7 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       // fused cross-q is the default (397-398 vs 383-384x real time, gpurun_out/r02za); WMX_XQ_FUSED=0 restores the
       // separate split-K launch (A/B runs)
       c.xq_fused = !(getenv("WMX_XQ_FUSED") && atoi(getenv("WMX_XQ_FUSED")) == 0);
-      c.mlp_fused = getenv("WMX_MLP_FUSED") && atoi(getenv("WMX_MLP_FUSED")) == 1;
+      c.mlp_fused = getenv("WMX_MLP_FUSED") && atoi(getenv("WMX_MLP_FUSED")) == 1 && !w->m.w8;
       gemm_init_attributes();
       alloc_ctx(c);
     } catch (...) {
@@ -2471,6 +2593,7 @@ wmx_status wmx_ctx_forced_decode(wmx_ctx* x, const int32_t* prefix, const int32_
     WMX_HIP(hipMemcpyAsync(c.hist, hist.data(), hist.size() * 4, hipMemcpyHostToDevice, c.st));
     WMX_HIP(hipMemcpyAsync(c.pad_row, pad_row.data(), R * 4, hipMemcpyHostToDevice, c.st));
     WMX_HIP(hipMemcpyAsync(c.pad_win, pad_win.data(), B * 4, hipMemcpyHostToDevice, c.st));
+    WMX_HIP(hipMemsetAsync(c.mlp_cnt, 0, (size_t)kMlpCounters * 4, c.st));  // per-call fused-MLP counters
     set_slot(c, 0);
     std::vector<float> lg((size_t)R * V);
     auto collect = [&](int step, int nrows, int rep) {  // logits rows [0, nrows) -> top1 / logits of R rows
@@ -2861,20 +2984,19 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       a.Tn = 1;
       a.H = H;
       a.d = dt;
-      a.ck = cross_k(c, 0);
-      a.cv = cross_v(c, 0);
-      a.x_wstride = (long)kXS * dt;
-      a.x_hstride = (long)kXS * 64;
+      set_cross_images(c, a, 0);
       a.Tk = 1500;
       a.rows_per_win = c.K;
-      by = (double)B * 1500 * 2 * dt * 2 + 2.0 * R * dt * 2;
+      const double eb = m.w8 ? 1.0 : 2.0;  // image / weight bytes per element (fp8 decode: 1)
+      by = (double)B * 1500 * 2 * dt * eb + 2.0 * R * dt * 2;
       fl = 4.0 * R * 1500 * dt;
       if (c.xq_fused && !m.fold) {  // the decode step's form: the query projection inside (reads LN2 rows + wcq)
-        a.wq = m.dec[0].wcq;
+        a.wq = m.w8 ? reinterpret_cast<const uint16_t*>(m.dec[0].q8cq) : m.dec[0].wcq;
+        a.wq_scale = m.w8 ? m.dec[0].s8cq : nullptr;
         a.qin = c.dhb;
         a.qin_ld = dt;
         a.qbias = m.dec[0].bcq;
-        by += (double)dt * dt * 2;
+        by += (double)dt * dt * eb;
         fl += 2.0 * R * dt * dt;
       }
       a.xcnt = c.xa_cnt;
@@ -2914,10 +3036,11 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
                       m.mel_count, m.mel_off, m.mel_w, m.d.n_mels, c.mel_raw, c.fcap, c.wmax, c.mel, c.st);
       };
     } else if (kernel == 4) {
-      by = 4.0 * dt * dt * 2 + (double)R * dt * 2 + (double)R * 4 * dt * 2;
+      by = 4.0 * dt * dt * (m.w8 ? 1 : 2) + (double)R * dt * 2 + (double)R * 4 * dt * 2;
       fl = 2.0 * R * 4 * dt * dt;
       fn = [&c, &m, R, dt] {
-        gemm_p(c, c.dhb, dt, m.dec[0].wfc1, R, 4 * dt, dt, epi(EPI_GELU16, m.dec[0].bfc1, c.df1, 4 * dt));
+        gemm_p(c, c.dhb, dt, m.dec[0].wfc1, R, 4 * dt, dt, epi(EPI_GELU16, m.dec[0].bfc1, c.df1, 4 * dt), nullptr,
+               w8_of(m, m.dec[0].q8fc1, m.dec[0].s8fc1));
       };
     } else if (kernel == 5) {
       DecAttnArgs a{};
@@ -2951,10 +3074,13 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       // decode-step projections on packed weights, split-K partial launches: 7 qkv, 8 a d x d projection, 9 fc2
       const int N = kernel == 7 ? 3 * dt : dt, K = kernel == 9 ? 4 * dt : dt;
       const uint16_t* W = kernel == 7 ? m.dec[0].wqkv : kernel == 8 ? m.dec[0].wo : m.dec[0].wfc2;
+      const DecLayer& L0 = m.dec[0];
+      const W8 w8 = kernel == 7 ? w8_of(m, L0.q8qkv, L0.s8qkv) : kernel == 8 ? w8_of(m, L0.q8o, L0.s8o)
+                                                                             : w8_of(m, L0.q8fc2, L0.s8fc2);
       const uint16_t* A = kernel == 9 ? c.df1 : c.dhb;
-      by = (double)N * K * 2 + (double)R * K * 2 + (double)R * N * 2;
+      by = (double)N * K * (m.w8 ? 1 : 2) + (double)R * K * 2 + (double)R * N * 2;
       fl = 2.0 * R * N * K;
-      fn = [&c, A, W, R, N, K] { gemm_p_part(c, A, K, W, R, N, K); };
+      fn = [&c, A, W, R, N, K, w8] { gemm_p_part(c, A, K, W, R, N, K, w8); };
     } else if (kernel == 10) {
       // reduce_ln after a d x d projection: x += bias + sum of its split-K partials; LN(x) -> 16-bit
       const int S = packed_splits(R, dt, dt, c.part_elems);

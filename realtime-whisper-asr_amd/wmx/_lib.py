@@ -132,13 +132,18 @@ def _load():
 lib = _load()
 
 
+WMX_ERR_NUMERIC = 5  # include/wmx.h: the decode produced non-finite logits
+
+
 class WmxError(RuntimeError):
-    pass
+    def __init__(self, msg: str, status: int = 0):
+        super().__init__(msg)
+        self.status = status
 
 
 def check(status: int):
     if status != 0:
-        raise WmxError(f"libwmx error {status}: {lib.wmx_last_error().decode(errors='replace')}")
+        raise WmxError(f"libwmx error {status}: {lib.wmx_last_error().decode(errors='replace')}", status)
 
 
 def fptr(a: np.ndarray):

@@ -56,7 +56,8 @@ class _ArenaView:
 
 
 def arena_tensor(model, device):
-    """A torch uint8 tensor aliasing the model's weight arena on `device` (no copy)."""
+    """A torch uint8 tensor aliasing the parameter region of the model's weight arena on `device` (no copy;
+    wmx_model_arena: the derived copies that follow it are rebuilt per rank by mark_loaded)."""
     import torch
     ptr, nbytes = model.arena()
     return torch.as_tensor(_ArenaView(ptr, nbytes), device=device)
@@ -64,8 +65,9 @@ def arena_tensor(model, device):
 
 def share_weights(model, rank: int, device, seed: int | None = None, src: int = 0):
     """Make every rank's weights identical: rank `src` initialises (PRNG `seed`, or keeps what is loaded), then ONE RCCL
-    broadcast of the whole arena (parameters plus the derived MX-fp8 / row-major copies) over xGMI, then every rank
-    marks its arena loaded.  The only data-path collective of the job."""
+    broadcast of the arena's parameter region (3.1 GB for large-v3 bf16: the parameters only, not the derived
+    row-major / MX-fp8 / 8-bit / folded copies) over xGMI, then every rank derives its copies (mark_loaded).  The only
+    data-path collective of the job."""
     import torch
     if rank == src and seed is not None:
         model.init_synthetic(seed)

@@ -6,6 +6,7 @@ library.  Model dimensions follow openai-whisper ModelDimensions (what faster-wh
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 from dataclasses import dataclass
 
 import numpy as np
@@ -61,16 +62,26 @@ class Model:
         self.dims = MODEL_DIMS[name_or_dims] if isinstance(name_or_dims, str) else name_or_dims
         self.name = name_or_dims if isinstance(name_or_dims, str) else "custom"
         ct = compute_type.lower()
-        if ct in ("bfloat16", "bf16", "int8_bfloat16"):
+        self.compute_type = ct
+        if ct in ("bfloat16", "bf16"):
             self.dtype = L.WMX_DTYPE_BF16
-        elif ct in ("float16", "f16", "fp16", "int8_float16", "default", "auto"):
+        elif ct in ("float16", "f16", "fp16", "default", "auto"):
             self.dtype = L.WMX_DTYPE_F16
         elif ct in ("float8", "fp8", "mxfp8", "mx8", "float8_bfloat16"):
-            # BASELINE config 5: encoder projections on the CDNA4 MX-fp8 MFMA, the rest in bf16
+            # BASELINE config 5: encoder projections on the CDNA4 MX-fp8 MFMA, the decode on 8-bit weights and fp8
+            # cross-K/V images (include/wmx.h WMX_DTYPE_MX8), activations bf16
+            self.dtype = L.WMX_DTYPE_MX8
+        elif ct in ("int8_float16", "int8_bfloat16", "int8", "int8_float32"):
+            # CTranslate2's 8-bit modes (the reference's int8_float16, 一键实时识别麦克风.py:304): 8-bit weights with
+            # one scale per row.  Served by this build's 8-bit path, whose weight format is e4m3 with a power-of-two
+            # row scale (not int8): the same bytes per weight, a different rounding grid -- said out loud, not
+            # substituted silently
+            warnings.warn(f"compute_type {compute_type!r}: MI355X runs 8-bit weights as e4m3 with per-row scales "
+                          "(WMX_DTYPE_MX8, the float8 model), not CTranslate2's int8 grid", stacklevel=2)
             self.dtype = L.WMX_DTYPE_MX8
         else:
             raise ValueError(f"compute_type {compute_type!r} is not supported on MI355X "
-                             "(use float16 / bfloat16 / float8)")
+                             "(use float16 / bfloat16 / float8 / int8_float16)")
         self.device = device
         h = C.c_void_p()
         ds = _dims_struct(self.dims)

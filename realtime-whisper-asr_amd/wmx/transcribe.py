@@ -278,6 +278,9 @@ class WhisperModel:
         self.sample_seed = seed
         self._sample_calls = 0
         self._ctx = {}
+        # what the calls cost on the device (bench.py's latency lines decompose a call with it): decoded windows
+        # (engine transcribe rows, fallback retries included), engine calls, decode steps those calls ran
+        self.counters = {"windows": 0, "engine_calls": 0, "decode_steps": 0}
 
     def context(self, beam_size, language_token, task, word_timestamps, without_timestamps=False, patience=1.0,
                 length_penalty=1.0, suppress_blank=True, suppress_tokens=None, max_initial_timestamp=1.0,
@@ -376,6 +379,14 @@ class WhisperModel:
                                         max_streams=1, max_windows=64)
         return self._vad
 
+    def _count(self, ctx, windows):
+        # (host tests build the model without __init__ and drive it with engine stand-ins)
+        c = self.__dict__.setdefault("counters", {"windows": 0, "engine_calls": 0, "decode_steps": 0})
+        c["windows"] += windows
+        c["engine_calls"] += 1
+        steps = getattr(ctx, "last_steps", None)
+        c["decode_steps"] += steps() if steps else 0
+
     def _decode_with_fallback(self, audio, seek, prompt, temps, beam_size, best_of, lang_tok, task, word_timestamps,
                               ctx_kw, compression_ratio_threshold, log_prob_threshold, no_speech_threshold):
         """faster-whisper generate_with_fallback: decode at each temperature of the schedule until the result passes
@@ -390,6 +401,7 @@ class WhisperModel:
                 self._sample_calls += 1
             # the window's features come from the whole buffer (global max normalisation) -> pass the full audio
             r = ctx.transcribe([audio], prompts=[prompt], seek=[seek])[0]
+            self._count(ctx, 1)
             cr = compression_ratio(self.tokenizer.decode([x for x in r.tokens if x < self.tokenizer.sp.eot]).strip())
             results.append((r, cr))
             needs = False
@@ -483,6 +495,7 @@ class WhisperModel:
                     pr.append(list(p or []))
             try:
                 res = ctx.transcribe(chunk, prompts=pr)
+                self._count(ctx, len(idx))
             except Exception as e:
                 for i in idx:
                     out[i] = e

@@ -59,9 +59,12 @@ def _same(a, b, tag):
     np.testing.assert_array_equal(a.text_token_probs, b.text_token_probs, err_msg=tag)
 
 
-def test_two_groups_concurrent_equal_sequential_and_replay():
+@pytest.mark.parametrize("ct", ["bfloat16", "float8"])
+def test_two_groups_concurrent_equal_sequential_and_replay(ct):
+    """bfloat16 (the default bench line) and float8 (config 5's line: MX-fp8 encoder, 8-bit decoder weights and fp8
+    cross-K/V images)."""
     from wmx import engine as E
-    m = E.Model(_edims(WIDE2), 0, "bfloat16").init_synthetic(5)
+    m = E.Model(_edims(WIDE2), 0, ct).init_synthetic(5)
     sp = O.special_tokens(WIDE2.n_vocab)
     K, n_new = 5, 40
     ctxs = [E.Context(m, max_batch=4, beam_size=K, max_new_tokens=n_new, language=None, word_timestamps=True,

@@ -126,3 +126,37 @@ def test_config2_base_fp16_streaming_vac_1s_chunks():
     lat = sorted(t for _, t in calls)
     print(f"config 2: {len(calls)} ASR calls, p50 latency {1000 * lat[len(lat) // 2]:.1f} ms, "
           f"{len(committed)} commits")
+
+
+def test_nonfinite_decode_is_an_error_not_a_short_transcript():
+    """A NaN anywhere upstream of the logits (here one LayerNorm gain of decoder layer 0) must surface as an error, not
+    as an EOT that silently shortens the transcript (csrc/wmx_decode.hip logits_select_b sets the per-call guard word,
+    wmx_runtime.hip transcribe turns it into WMX_ERR_NUMERIC naming the step and row).  Through the drop-in adapter it
+    raises WmxError; through EnhancedOnlineASRProcessor.process_iter it takes the reference's recovery path
+    (enhanced_asr_processor.py:369-381: log, re-init the buffers at the same offset, return (None, None, "")).  With
+    the gain restored the next call succeeds (the guard word is per call)."""
+    import io
+    from wmx.asr import MI355XWhisperASR
+    from wmx._lib import WMX_ERR_NUMERIC, WmxError
+    from wmx.online import EnhancedOnlineASRProcessor
+    asr = MI355XWhisperASR(lan="auto", modelsize="micro", device="cuda", compute_type="bfloat16",
+                           transcribe_kwargs={"beam_size": 5}, max_new_tokens=16)
+    eng = asr.model.model
+    audio = synth.speech_like(5, 16000 * 4)
+    assert isinstance(asr.transcribe(audio), list)
+    name = "decoder.layers.0.encoder_attn_layer_norm.weight"
+    g = eng.get_tensor(name, (eng.dims.n_text_state,))
+    bad = g.copy()
+    bad[3] = np.nan
+    eng.set_tensor(name, bad)
+    with pytest.raises(WmxError) as ei:
+        asr.transcribe(audio)
+    assert ei.value.status == WMX_ERR_NUMERIC and "non-finite" in str(ei.value), str(ei.value)
+    print(ei.value)
+    log = io.StringIO()
+    p = EnhancedOnlineASRProcessor(asr, buffer_trimming=("segment", 15), agreement_n=2, logfile=log)
+    p.insert_audio_chunk(audio[:32000])
+    assert p.process_iter() == (None, None, "")
+    assert len(p.audio_buffer) == 0 and "non-finite" in log.getvalue(), log.getvalue()
+    eng.set_tensor(name, g)
+    assert isinstance(asr.transcribe(audio), list)

@@ -51,7 +51,7 @@ def test_mx8_translate_greedy_matches_oracle():
     d = O.DIMS["micro"]
     m = E.Model("micro", 0, "float8").init_synthetic(9)
     ctx = E.Context(m, max_batch=2, beam_size=1, max_new_tokens=24, task="translate", word_timestamps=False)
-    W = O.make_weights(d, 9, "bf16")
+    W = O.fp8_decoder_weights(O.make_weights(d, 9, "bf16"), d)  # (the MX-fp8 encoder + the fp8 decode)
     audios = [synth.speech_like(91, 480000), synth.speech_like(92, 96000)]
     res = ctx.transcribe(audios)
     from test_gpu_parity import greedy_forced_compare
@@ -98,3 +98,132 @@ def test_mx8_full_depth_large_v3_translate():
     res = ctx.transcribe([audio])
     opt = O.DecodeOptions(beam_size=1, max_new_tokens=8, task="translate")
     S._replay_and_compare("large-v3 full depth MX-fp8 translate greedy", ctx, res, 1, opt, sp, 1)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# the fp8 decode (round 4): every decoder projection and the logits projection on 8-bit weights (e4m3, one
+# power-of-two scale per weight row, widened to bf16 in registers, the row scale on the fp32 result) and the cross
+# K / V images in e4m3 (one power-of-two scale per (layer, window, head) image).  Oracle: oracle.fp8_decoder_weights
+# (the same rules in numpy: w8_rows, kv8_images) on the DEVICE's own encoder output, so the comparison isolates the
+# decoder.  Tolerance: the bf16 step bound, relative L2 <= 3e-2 per row and step, and argmax equality wherever the
+# oracle's top-2 margin exceeds twice the row's max abs error (tests/test_gpu_step.py _check_forced); both sides use
+# bit-identical dequantized weights, so what is left is bf16 activation rounding and the image element rounding of
+# the device's 16-bit K / V (the oracle rounds its fp32 K / V to bf16 first, as the device stores them).
+# ---------------------------------------------------------------------------------------------------------------
+WIDE2 = O.Dims(128, 51866, 1280, 20, 1, 1280, 20, 2)  # large-v3 width, 1 encoder layer, 2 decoder layers
+
+
+@pytest.fixture(scope="module")
+def wide_fp8():
+    from wmx import engine as E
+    m = E.Model(_dims(E, WIDE2), 0, "float8").init_synthetic(5)
+    W = O.fp8_decoder_weights(O.make_weights(WIDE2, 5, "bf16"), WIDE2)
+    lens = [480000, 150000, 320000, 16000, 240000, 480000, 90000, 400000]
+    mels = np.stack([O.logmel_segment(synth.speech_like(300 + i, n), 128) for i, n in enumerate(lens)])
+    return m, W, mels
+
+
+@pytest.mark.parametrize("B,K", [(4, 5), (8, 5), (20, 1)])
+def test_fp8_decode_forced_steps_wide(wide_fp8, B, K):
+    """Teacher-forced decode steps of the fp8 decode at large-v3 width: 4 and 8 windows x beam 5 (R = 20 and 40, the
+    bench's per-group rows at 8 and 16 windows per GPU) and 20 windows greedy, 24 steps, parents re-drawn every
+    step."""
+    from wmx import engine as E
+    import test_gpu_step as S
+    m, W, mels = wide_fp8
+    sp = O.special_tokens(WIDE2.n_vocab)
+    ctx = E.Context(m, max_batch=B, beam_size=K, max_new_tokens=64, word_timestamps=False)
+    mel = np.concatenate([mels] * 3)[:B]
+    encs = list(ctx.encode(mel))
+    n = 24
+    tok, par = S._forced_stream(np.random.default_rng(7 + B), n, B * K, K)
+    prefix = [[sp.sot, sp.lang0, sp.transcribe]] * B
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, WIDE2, encs, prefix, tok, par, K)
+    S._check_forced(f"fp8 decode B={B} K={K}", "bf16", top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
+    # the fp8 model sits measurably away from the bf16 one (the quantization is live, not a no-op)
+    W16 = O.make_weights(WIDE2, 5, "bf16")
+    _, _, lg16 = O.forced_rows(W16, WIDE2, encs[:1], prefix[:1], tok[:2, :K], par[:2, :K], K)
+    d16 = rel_l2(lg[1, 0], lg16[1][0])
+    print("fp8 decode vs bf16 decode weights, row 0 step 1 rel_l2", d16)
+    assert d16 > 5e-3, d16
+
+
+def test_fp8_decode_search_replay_wide(wide_fp8):
+    """Free-running beam-5 transcribe of 8 windows (config 5's per-group shape at 16 windows per GPU), translate,
+    recorded: the oracle replays the rules / beam bookkeeping on the device's logits and must choose exactly the
+    device's selection at every step, and rank the device's final sequence."""
+    from wmx import engine as E
+    import test_gpu_step as S
+    m, W, mels = wide_fp8
+    sp = O.special_tokens(WIDE2.n_vocab)
+    audios = [synth.speech_like(300 + i, n) for i, n in
+              enumerate([480000, 150000, 320000, 16000, 240000, 480000, 90000, 400000])]
+    ctx = E.Context(m, max_batch=8, beam_size=5, max_new_tokens=32, task="translate", word_timestamps=True,
+                    language=sp.lang0)
+    ctx.record(33)
+    res = ctx.transcribe(audios)
+    opt = O.DecodeOptions(language=sp.lang0, beam_size=5, max_new_tokens=32, task="translate")
+    S._replay_and_compare("fp8 decode beam5 B=8 translate", ctx, res, 5, opt, sp, 16)
+    assert all(r.jump_times is not None for r in res)
+
+
+def test_fp8_decode_full_depth_large_v3():
+    """Config 5's model at full depth (32 + 32 layers, vocab 51866): 8 teacher-forced steps of one window x beam 5
+    against the fp8 oracle on the device's encoder output."""
+    from wmx import engine as E
+    import test_gpu_step as S
+    d = O.DIMS["large-v3"]
+    sp = O.special_tokens(d.n_vocab)
+    m = E.Model("large-v3", 0, "float8").init_synthetic(1)
+    W = {name: m.get_tensor(name, shape) for name, shape, _, _ in O.tensor_specs(d)}
+    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
+    W = O.fp8_decoder_weights(W, d)
+    ctx = E.Context(m, max_batch=1, beam_size=5, max_new_tokens=16, word_timestamps=False)
+    encs = list(ctx.encode(O.logmel_segment(synth.speech_like(611, 480000), d.n_mels)[None]))
+    n = 8
+    tok, par = S._forced_stream(np.random.default_rng(11), n, 5, 5)
+    prefix = [[sp.sot, sp.lang0, sp.transcribe]]
+    top1, lg = ctx.forced_decode(prefix, tok, par, logits_every=1)
+    ref_top1, ref_margin, ref_lg = O.forced_rows(W, d, encs, prefix, tok, par, 5)
+    S._check_forced("fp8 decode large-v3 full depth", "bf16", top1, lg, 1, ref_top1, ref_margin, ref_lg, 4)
+
+
+def test_fp8_decode_word_alignment_large_v3_heads():
+    """The word-alignment pass of the fp8 model (the alignment forward over sot + text + eot runs its > 256-row
+    projections on the dequantized row-major copies, its cross attention on the fp8 images, its logits on the 8-bit
+    embedding): the device matrix against oracle.find_alignment on the fp8 weights and the device's encoder output,
+    at large-v3 width with the large-v3 alignment heads.  Bounds: tests/test_gpu_align.py's jump-time (>= 95 % within
+    one frame) and token-probability (2e-2) criteria; the matrix rel-L2 <= 5e-2 (the MX-fp8 bound of the full-depth
+    encoder above) instead of bf16's 3e-2: the K images are e4m3-rounded from the device's 16-bit GEMM output, and an
+    element whose 16-bit value differs by one ulp from the oracle's can land on the neighbouring e4m3 code (a 6 % step)
+    -- measured 3.2e-2 against bf16's 2.2e-2 (gpurun_out r04a), with 98 % of the jump times within one frame."""
+    from wmx import engine as E
+    import test_gpu_align as A
+    d = A.ALN
+    m = E.Model(_dims(E, d), 0, "float8").init_synthetic(11)
+    W = {name: m.get_tensor(name, shape) for name, shape, _, _ in O.tensor_specs(d)}
+    W["encoder.embed_positions.weight"] = O.sinusoids(1500, d.n_audio_state)
+    W = O.fp8_decoder_weights(W, d)
+    heads = E.ALIGNMENT_HEADS["large-v3"]
+    sp = O.special_tokens(d.n_vocab)
+    ctx = E.Context(m, max_batch=2, beam_size=5, max_new_tokens=120, word_timestamps=True, alignment_heads=heads,
+                    language=sp.lang0)
+    audios = [synth.speech_like(821, 480000), synth.speech_like(822, 400000)]
+    encs = ctx.encode(np.stack([O.logmel_segment(a, d.n_mels) for a in audios]))
+    res = ctx.transcribe(audios)
+    for b, r in enumerate(res):
+        text = [t for t in r.tokens if t < sp.eot]
+        assert len(text) >= 100, len(text)
+        dev = ctx.alignment_matrix(b)
+        ti, tj = A._lib_dtw(dev)
+        np.testing.assert_array_equal(r.jump_times, A._jumps(ti, tj).astype(np.float32))
+        oti, otj, probs, jt, ref = O.find_alignment(W, d, encs[b], sp.lang0, "transcribe", text, r.seek_frames,
+                                                     align_heads=heads, return_matrix=True)
+        e = rel_l2(dev, ref)
+        within = float(np.mean(np.abs(r.jump_times - jt) <= 0.02 + 1e-6))
+        print(f"fp8 window {b}: {len(text)} text tokens, matrix rel_l2 {e:.2e}, jump times within 1 frame {within:.3f}, "
+              f"token probs max err {float(np.max(np.abs(r.text_token_probs - probs))):.2e}")
+        assert e <= 5e-2, e
+        assert within >= 0.95, within
+        np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)

@@ -6,8 +6,10 @@ torch.distributed group over `nccl` (RCCL), builds a source model from the PRNG 
 model, copies the source arena into the destination's through the zero-copy arena views (a device copy standing in
 for the xGMI transfer a second rank receives), runs the RCCL broadcast on the destination's arena exactly as
 share_weights does, marks it loaded (which re-derives the row-major and MX-fp8 copies) and transcribes with both:
-the tokens, scores and jump times must be identical.  bf16 and float8 (config 5: the MX-fp8 copies are derived
-after the load).
+the tokens, scores and jump times must be identical.  bf16 and float8 (config 5: the MX-fp8 and 8-bit copies are
+derived after the load).  The broadcast carries the arena's PARAMETER region only: its byte count is the parameters'
+16-bit bytes plus the fp32 biases / LayerNorms and the encoder positions (<= 2 B x n_params x 1.02 + 1500 x d x 4),
+whatever the dtype -- the derived row-major / MX-fp8 / 8-bit copies (+50 % or more) are rebuilt on the receiving rank.
 """
 import json
 import os
@@ -48,7 +50,7 @@ for ct in ("bfloat16", "float8"):
     same = all(a.tokens == b.tokens and a.sum_logprob == b.sum_logprob and
                np.array_equal(a.jump_times, b.jump_times) for a, b in zip(*res))
     out[ct] = {"same": bool(same), "tokens": [len(r.tokens) for r in res[1]], "arena_bytes": int(vd.numel()),
-               "arena_equal": bool(torch.equal(vs, vd))}
+               "arena_equal": bool(torch.equal(vs, vd)), "n_params": int(src.n_params())}
     dst.close(); src.close()
 D.destroy()
 print("RESULT " + json.dumps(out))
@@ -67,3 +69,5 @@ def test_rccl_arena_broadcast_world1():
     for ct, v in out.items():
         assert v["same"] and v["arena_equal"], (ct, v)
         assert min(v["tokens"]) == 24, (ct, v)
+        assert 2 * v["n_params"] <= v["arena_bytes"] <= 2.04 * v["n_params"] + 1500 * 1280 * 4, (ct, v)
+    assert out["bfloat16"]["arena_bytes"] == out["float8"]["arena_bytes"], out

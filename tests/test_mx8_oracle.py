@@ -58,3 +58,37 @@ def test_mx8_quantize_round_trip_properties():
     rel = np.abs(q.reshape(16, 8, 32) - b) / np.abs(b).max(-1, keepdims=True)
     assert rel.max() <= 2.0 ** -4  # half an e4m3 ulp at the top binade, relative to the block max
     assert np.linalg.norm(q - x) / np.linalg.norm(x) < 0.05
+
+
+def test_fp8_decode_rules():
+    """The fp8 decode's oracle rules (oracle/whisper_np.py w8_rows / kv8_images / fp8_decoder_weights): one MX
+    power-of-two scale per weight row (per (window, head) image for K / V), every value an e4m3 code times its scale,
+    no saturation (row max <= 448 x scale), idempotent; the embedding lookup keeps the 16-bit table while the logits
+    projection is quantized; the cross k / v projection weights themselves stay 16-bit (their OUTPUT is quantized)."""
+    rng = np.random.default_rng(0)
+    w = (rng.standard_normal((64, 1280)) * 0.03).astype(np.float32)
+    q = O.w8_rows(w)
+    np.testing.assert_array_equal(O.w8_rows(q), q)
+    sc = np.ldexp(1.0, O.mx8_exp(np.abs(w).max(-1)))[:, None]
+    np.testing.assert_array_equal(O.e4m3_round((q / sc).astype(np.float32)), (q / sc).astype(np.float32))
+    assert np.all(np.abs(q / sc) <= 448)
+    rel = np.linalg.norm(q - w) / np.linalg.norm(w)
+    assert 0.01 < rel < 0.04, rel  # e4m3: 3 mantissa bits
+    k = (rng.standard_normal((1500, 256)) * 2.0).astype(np.float32)
+    k8 = O.kv8_images(k, 4)
+    for h in range(4):
+        blk = k8[:, 64 * h: 64 * h + 64]
+        s = np.ldexp(1.0, O.mx8_exp(np.abs(O.round_bf16(k[:, 64 * h: 64 * h + 64])).max()))
+        np.testing.assert_array_equal(O.e4m3_round((blk / s).astype(np.float32)), (blk / s).astype(np.float32))
+    d = O.DIMS["micro"]
+    W = O.make_weights(d, 3, "bf16")
+    V = O.fp8_decoder_weights(W, d)
+    assert V["decoder.kv8"] is True
+    np.testing.assert_array_equal(V["decoder.embed_tokens.weight"], W["decoder.embed_tokens.weight"])
+    np.testing.assert_array_equal(V["decoder.proj_out.weight"], O.w8_rows(W["decoder.embed_tokens.weight"]))
+    for n in ("encoder_attn.k_proj", "encoder_attn.v_proj"):
+        np.testing.assert_array_equal(V[f"decoder.layers.0.{n}.weight"], W[f"decoder.layers.0.{n}.weight"])
+    for n in O.FP8_DEC_LINEARS:
+        key = f"decoder.layers.1.{n}.weight"
+        assert not np.array_equal(V[key], W[key]), key
+    np.testing.assert_array_equal(V["encoder.layers.0.fc1.weight"], W["encoder.layers.0.fc1.weight"])
