@@ -1774,10 +1774,12 @@ constexpr int packed_ku() {
   return (MT + NCT) <= 3 ? 5 : (MT + NCT) <= 8 ? 2 : 1;
 #endif
 }
-// 8-bit weights: a k-step is 64 deep (one 16-byte weight piece + two A fragments per 16-row tile)
+// 8-bit weights: a k-step is 64 deep (one 16-byte weight piece + two A fragments per 16-row tile); the waves per
+// workgroup come from the 32-deep step count as for 16-bit weights (packed_nw), so a wave holds 1-2 of these wider
+// k-steps and issues them as one batch
 template <int MT, int NCT>
 constexpr int packed_ku8() {
-  return (MT + NCT) <= 3 ? 3 : (MT + NCT) <= 6 ? 2 : 1;
+  return (MT + NCT) <= 3 ? 3 : (MT + NCT) <= 8 ? 2 : 1;
 }
 
 // S == 1 epilogues of the LayerNorm-folded decode step (wmx_common.h row_ln_from_stats): the residual producer
@@ -2061,14 +2063,22 @@ int packed_splits(int M, int N, int K, long cap_elems) {
 
 // waves per workgroup: enough that each wave's share of its K slice is at most ~4 k-steps (two dependent load
 // batches), so long unsplit slices (fc1, whose GELU epilogue needs S = 1) are not a chain of five round trips
+// the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] of a workgroup: within 80 KiB (two workgroups per
+// CU) always; up to the CU's 160 KiB when the launch has no more workgroups than the chip has CUs (one each anyway:
+// R = 40's fc1 / fc2, MT 3 x NCT 4, whose 4 waves otherwise walk 5 / 3 dependent load batches)
 template <int MT, int NCT>
-static int packed_nw(int K, int S) {
+constexpr int packed_red_bytes(int nw) { return nw * MT * 16 * (16 * NCT + 1) * 4; }
+constexpr int kPackedOneWgPerCu = 256;
+
+template <int MT, int NCT>
+static int packed_nw(int K, int S, long wgs = 1L << 30) {
   const int ksteps = K / 32, kps = (ksteps + S - 1) / S;
   const int per4 = (kps + 3) / 4;
   static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
-  // the cross-wave reduction image red[NW][MT * 16][16 NCT + 1] stays within 80 KiB of LDS (two workgroups per CU)
-  constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
-  constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
+  static const bool lds80 = getenv("WMX_PACKED_LDS80") != nullptr;  // A/B switch: the 80 KiB budget everywhere
+  const int budget = (!lds80 && wgs <= kPackedOneWgPerCu) ? 163840 : 81920;
+  const bool fit8 = packed_red_bytes<MT, NCT>(8) <= budget;
+  const bool fit16 = packed_red_bytes<MT, NCT>(16) <= budget;
   if (only4 || per4 <= 4 || !fit8) return 4;
   if (per4 <= 8 || !fit16) return 8;
   return 16;
@@ -2078,8 +2088,7 @@ template <DT T, int MT, int NCT, bool W8>
 static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ntiles = (g.N + 15) / 16;
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
-  // (8-bit weights: waves per workgroup from the 64-deep k-steps of the slice)
-  const int nw = packed_nw<MT, NCT>(W8 ? g.K / 2 : g.K, g.S);
+  const int nw = packed_nw<MT, NCT>(g.K, g.S, (long)grid.x * grid.y * grid.z);
   const bool tail = g.tail.cnt != nullptr;
   const int epk = tail ? kPackedTail
                  : g.S > 1 ? kPackedPart
@@ -2097,8 +2106,8 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
       default: WMX_PACKED_EPK(NWV, kPackedGeneric); break;                                                         \
     }                                                                                                              \
   } while (0)
-  constexpr bool fit8 = 8 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
-  constexpr bool fit16 = 16 * MT * 16 * (16 * NCT + 1) * 4 <= 81920;
+  constexpr bool fit8 = packed_red_bytes<MT, NCT>(8) <= 163840;
+  constexpr bool fit16 = packed_red_bytes<MT, NCT>(16) <= 163840;
   if (nw == 4) {
     WMX_PACKED_LAUNCH(4);
   } else if (nw == 8) {
@@ -2112,8 +2121,9 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
 
 template <int MT, int NCT>
 static PackedPlan plan_cfg(int M, int N, int K, int S, bool w8) {
-  return PackedPlan{MT, NCT, packed_nw<MT, NCT>(w8 ? K / 2 : K, S), w8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>(),
-                    ((N + 15) / 16 + NCT - 1) / NCT, (M + MT * 16 - 1) / (MT * 16)};
+  const int gx = ((N + 15) / 16 + NCT - 1) / NCT, gz = (M + MT * 16 - 1) / (MT * 16);
+  return PackedPlan{MT, NCT, packed_nw<MT, NCT>(K, S, (long)gx * S * gz), w8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>(),
+                    gx, gz};
 }
 
 template <int NCT>
