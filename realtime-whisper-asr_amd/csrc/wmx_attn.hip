@@ -1082,7 +1082,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 }
 
 // key chunk per workgroup; WMX_CROSS_CHUNK overrides the default for tuning runs
-static int cross_chunk(int Tk, int nq) {
+static int cross_chunk(int Tk, int nq, bool f8) {
   static const int env = [] {
     const char* v = getenv("WMX_CROSS_CHUNK");
     return v ? atoi(v) : 0;
@@ -1091,8 +1091,10 @@ static int cross_chunk(int Tk, int nq) {
   if (env) return env;
   // large-v3, 2 groups x 4 windows, 8 waves per workgroup: 1024-key chunks (2 per window-head) 600-602 ms per call,
   // 768: 603-605, 512 with 4 waves: 610-625 (interleaved bench.py sweep, r01); 512 beat 256 with 4 waves;
-  // unsplit (1504): 611-612 vs 591 (r01f)
-  return 1024;
+  // unsplit (1504): 611-612 vs 591 (r01f).  fp8 images (half the bytes per key): 512-key chunks, 463 / 709x real
+  // time at 8 / 16 windows against 1024's 457 / 645-659x, 768's 466 / 665x and unsplit's 442 / 704-707x
+  // (profiles/r04_fp8_decode/, gpurun_out r04g / r04h)
+  return f8 ? 512 : 1024;
 }
 
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
@@ -1109,7 +1111,7 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
   a.xcd_remap = remap && a.wq != nullptr;
   const int nq = a.rows_per_win * a.Tn;
   const int nwin = a.R / a.rows_per_win;
-  const int chunk = std::min(cross_chunk(a.Tk, nq), a.Tk);
+  const int chunk = std::min(cross_chunk(a.Tk, nq, F8), a.Tk);
   const int KS = (a.Tk + chunk - 1) / chunk;
   const int QT = (nq + 15) / 16;
   WMX_CHECK(KS <= kMaxSplits, "cross attn: too many key chunks");

@@ -2073,7 +2073,12 @@ constexpr int kPackedOneWgPerCu = 256;
 template <int MT, int NCT>
 static int packed_nw(int K, int S, long wgs = 1L << 30) {
   const int ksteps = K / 32, kps = (ksteps + S - 1) / S;
-  const int per4 = (kps + 3) / 4;
+  // k-steps per wave the wave count aims for (WMX_PACKED_PER overrides 4 for tuning runs: 2 = one load batch)
+  static const int per_t = [] {
+    const char* v = getenv("WMX_PACKED_PER");
+    return v ? std::max(1, atoi(v)) : 4;
+  }();
+  const int per4 = (kps + per_t - 1) / per_t;
   static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
   static const bool lds80 = getenv("WMX_PACKED_LDS80") != nullptr;  // A/B switch: the 80 KiB budget everywhere
   const int budget = (!lds80 && wgs <= kPackedOneWgPerCu) ? 163840 : 81920;
