@@ -21,8 +21,9 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--beam", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dtype", default="bfloat16", help="bfloat16 / float16 / float8 (the fp8 decode's 8-bit launches)")
     args = ap.parse_args()
-    m = Model(args.model)
+    m = Model(args.model, 0, args.dtype)
     ctx = Context(m, max_batch=args.batch, beam_size=args.beam)
     ms, by, fl = ctx.bench_kernel(args.kernel, args.batch, iters=args.iters)
     print(f"{args.kernel}: {ms * 1e3:.2f} us/launch, {by / ms / 1e6:.1f} GB/s, {fl / ms / 1e9:.2f} TFLOP/s")

@@ -31,10 +31,11 @@ MATCH = {
 }
 
 
-def run_pass(kernel, counter, out_dir, batch):
-    d = os.path.join(out_dir, f"{kernel}_{batch}_{counter}")
+def run_pass(kernel, counter, out_dir, batch, dtype="bfloat16"):
+    d = os.path.join(out_dir, f"{kernel}_{batch}_{dtype}_{counter}")
     cmd = ["rocprofv3", "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
-           sys.executable, os.path.join(ROOT, "tools", "kbench.py"), kernel, "--iters", "10", "--batch", str(batch)]
+           sys.executable, os.path.join(ROOT, "tools", "kbench.py"), kernel, "--iters", "10", "--batch", str(batch),
+           "--dtype", dtype]
     subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300)
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -51,19 +52,28 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kernels", nargs="+")
     ap.add_argument("--batch", type=int, nargs="+", default=[4, 8], help="windows per launch")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01f_pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"))
+    ap.add_argument("--dtype", nargs="+", default=["bfloat16"],
+                    help="model dtypes; float8 entries are keyed kernel@batch/fp8 (the 8-bit weights / fp8 images)")
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     res = {}
-    for k in args.kernels:
-        for b in args.batch:
-            fetch_kb, n1 = run_pass(k, "FETCH_SIZE", args.work, b)
-            write_kb, n2 = run_pass(k, "WRITE_SIZE", args.work, b)
-            res[f"{k}@{b}"] = {"batch": b, "fetch_bytes": 2.0 * fetch_kb * 1024, "write_bytes": write_kb * 1024,
-                               "traffic_bytes": 2.0 * fetch_kb * 1024 + write_kb * 1024,
-                               "launches": min(n1, n2),
-                               "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B"}
-            print(k, b, json.dumps(res[f"{k}@{b}"]), flush=True)
+    if os.path.exists(args.out):  # passes are added to an existing summary (one GPU call per dtype / batch set)
+        res = json.load(open(args.out))
+    for dt in args.dtype:
+        sfx = "/fp8" if dt == "float8" else ""
+        for k in args.kernels:
+            for b in args.batch:
+                fetch_kb, n1 = run_pass(k, "FETCH_SIZE", args.work, b, dt)
+                write_kb, n2 = run_pass(k, "WRITE_SIZE", args.work, b, dt)
+                res[f"{k}@{b}{sfx}"] = {"batch": b, "dtype": dt, "fetch_bytes": 2.0 * fetch_kb * 1024,
+                                        "write_bytes": write_kb * 1024,
+                                        "traffic_bytes": 2.0 * fetch_kb * 1024 + write_kb * 1024,
+                                        "launches": min(n1, n2),
+                                        "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KB = 1024 B"}
+                print(k, b, dt, json.dumps(res[f"{k}@{b}{sfx}"]), flush=True)
+                with open(args.out, "w") as f:  # written as it goes: a later pass that fails keeps the earlier ones
+                    json.dump(res, f, indent=1)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1)
