@@ -794,6 +794,12 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   // row scale) now, not after the projection's barrier
   const float qb_col = (fuse_q && a.qbias) ? a.qbias[h * 64 + (tid & 63)] : 0.f;
   const float qs_col = (fuse_q && F8) ? a.wq_scale[h * 64 + (tid & 63)] : 1.f;
+  // LN2 folded into the query weights (the mixed step, dec_step_mixed): qin is the 16-bit residual x and
+  // q = rstd_row (p - mean_row c1[col]) + c2[col]; the constants now, the row statistics right after the K batch
+  const bool fold_q = fuse_q && a.ln_c1 != nullptr;
+  const float qc1_col = fold_q ? a.ln_c1[h * 64 + (tid & 63)] : 0.f;
+  const float qc2_col = fold_q ? a.ln_c2[h * 64 + (tid & 63)] : 0.f;
+  float2 lnA[2], lnB[2];
   if (fuse_q) {
     const uint16_t* ap = a.qin + ((long)w * nq + i0 + min(fr, nqt - 1)) * a.qin_ld + 8 * g;
     const uint16_t* wp = a.wq + (((long)h * 4 * qksteps) << 9) + lane * 8;  // (F8: the same 16-byte lane pieces)
@@ -820,6 +826,11 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     load_k(kw0);
   else if (kw0 < kw1)
     load_batch(kw0);
+  if (fold_q) {  // rows wave and wave + 8 of the tile (clamped: rows past nqt are never used), merged after the MFMAs
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      row_ln_stats_load(a.ln_stats + (long)w * nq + i0 + min(wave + 8 * j, nqt - 1), a.ln_ld, a.d >> 4, lnA[j], lnB[j]);
+  }
   __builtin_amdgcn_sched_barrier(0);  // keep the K batch in flight under the projection (the scheduler sinks it)
   if (fuse_q) {
     f32x4 qa[4];
@@ -860,7 +871,14 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const float kQScale = 0.125f * 1.4426950408889634f * ksc;
   __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
   __shared__ float2 qln[16];
-  if (a.qS > 0 && a.ln_c1) {  // LN2 folded into the cross-q weights: the tile's row statistics, one wave per row
+  if (fold_q) {  // the statistics loaded beside the K batch, merged now (wave-uniform rows)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float2 st = row_ln_stats_merge(lnA[j], lnB[j], a.d >> 4);
+      if (lane == 0 && wave + 8 * j < nqt) qln[wave + 8 * j] = st;
+    }
+    __syncthreads();
+  } else if (a.qS > 0 && a.ln_c1) {  // LN2 folded into the cross-q weights: the tile's row statistics, one wave per row
     for (int q = wave; q < nqt; q += NWV) {
       const float2 st = row_ln_from_stats(a.ln_stats + (long)w * nq + i0 + q, a.ln_ld, a.d >> 4);
       if (lane == 0) qln[q] = st;
@@ -877,7 +895,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
         float p = 0.f;
 #pragma unroll
         for (int wv = 0; wv < NWV; ++wv) p += so[wv][q][e];
-        v = from_f32<T>((p * qs_col + qb_col) * kQScale);
+        v = from_f32<T>((fold_q ? qln[q].y * (p - qln[q].x * qc1_col) + qc2_col : p * qs_col + qb_col) * kQScale);
       } else if (a.qS > 0) {
         const float* src = a.qpart + row * a.qpart_ld + col;
         float tv[8];
@@ -1163,6 +1181,8 @@ void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {
   const bool f8 = a.ck_scale != nullptr;
   WMX_CHECK(!f8 || (a.cv_scale && (!a.wq || a.wq_scale)), "cross attn: fp8 images need their scales (and 8-bit query weights)");
   WMX_CHECK(f8 || !a.wq_scale, "cross attn: 8-bit query weights run with the fp8 images only");
+  WMX_CHECK(!(a.wq && a.ln_c1) || (!a.wq_scale && a.ln_c2 && a.ln_stats && a.d / 16 <= 128 && a.qS == 0),
+            "cross attn: the LayerNorm-folded fused query projection is 16-bit only");
   if (dt == DT::BF16) {
     if (f8) launch_cross_t<DT::BF16, true>(a, ws, st);
     else launch_cross_t<DT::BF16, false>(a, ws, st);

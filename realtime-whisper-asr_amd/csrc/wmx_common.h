@@ -214,14 +214,23 @@ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 // i.e. sum (x - mean)^2 exactly) and applies LN through the folded weights:
 //   LN(x) W^T + bias = rstd (x W'^T - mean c1) + c2,  W' = W diag(g),  c1 = W' 1,  c2 = bias + W b.
 // One wave per row, every lane active; G = d / 16 <= 128.  Returns (mean, rstd).
-__device__ inline float2 row_ln_from_stats(const float2* __restrict__ st, long ld, int G) {
+// (split in two so a kernel can issue the statistics loads early and merge them where it needs the result)
+__device__ inline void row_ln_stats_load(const float2* __restrict__ st, long ld, int G, float2& a, float2& b) {
   const int lane = threadIdx.x & 63;
-  const float2 a = lane < G ? st[lane * ld] : make_float2(0.f, 0.f);
-  const float2 b = lane + 64 < G ? st[(lane + 64) * ld] : make_float2(0.f, 0.f);
+  a = lane < G ? st[lane * ld] : make_float2(0.f, 0.f);
+  b = lane + 64 < G ? st[(lane + 64) * ld] : make_float2(0.f, 0.f);
+}
+__device__ inline float2 row_ln_stats_merge(float2 a, float2 b, int G) {
+  const int lane = threadIdx.x & 63;
   const float mean = wave_sum(a.x + b.x) / G;
   const float da = lane < G ? a.x - mean : 0.f, db = lane + 64 < G ? b.x - mean : 0.f;
   const float m2 = wave_sum((a.y + b.y) + 16.f * (da * da + db * db));
   return make_float2(mean, 1.0f / sqrtf(m2 / (16.f * G) + 1e-5f));
+}
+__device__ inline float2 row_ln_from_stats(const float2* __restrict__ st, long ld, int G) {
+  float2 a, b;
+  row_ln_stats_load(st, ld, G, a, b);
+  return row_ln_stats_merge(a, b, G);
 }
 
 // ---- OCP MX-fp8: e4m3 elements (OCP "fn", max 448), one e8m0 scale 2^e per 32 consecutive K elements ----

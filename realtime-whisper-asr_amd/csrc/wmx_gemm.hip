@@ -1785,17 +1785,48 @@ constexpr int packed_ku8() {
 // S == 1 epilogues of the LayerNorm-folded decode step (wmx_common.h row_ln_from_stats): the residual producer
 // (x += acc + bias, its 16-bit copy and per-16-column statistics) and the folded-LN + GELU consumer (fc1).
 // Trip counts are whole waves (MT * 16 * 4 NCT is a multiple of 64), so the 4-lane DPP sums see every lane.
+// The consumer's row statistics and the producer's residual quad are loaded before the main loop (FoldPre, beside
+// the first weight batch), so neither is a round trip after the reduction barrier.
+template <int MT, int NW>
+struct FoldPre {
+  static constexpr int RPW = (MT * 16 + NW - 1) / NW;  // statistics rows per wave (rows wave + NW j)
+  float2 sa[RPW], sb[RPW];
+  float4 x0;  // EPI_RESID_STATS: the residual quad of this thread's first epilogue item (idx = tid)
+  float4 c1, c2;  // EPI_LNFOLD_GELU16: the folded constants of the thread's column quad (the same in every row)
+};
+template <DT T, int MT, int NCT, int NW>
+__device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const Epi& e, int M, int N, int K, int m0,
+                                                     int t0) {
+  constexpr int C4 = 4 * NCT;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if (e.kind == EPI_LNFOLD_GELU16) {
+#pragma unroll
+    for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j)
+      row_ln_stats_load(e.stats + min(m0 + min(wave + NW * j, MT * 16 - 1), M - 1), e.stats_ld, K >> 4, P.sa[j], P.sb[j]);
+    const int n = min(t0 * 16 + (tid % C4) * 4, N - 4);
+    P.c1 = *reinterpret_cast<const float4*>(e.c1 + n);
+    P.c2 = *reinterpret_cast<const float4*>(e.c2 + n);
+  } else {
+    const int row = tid / C4, c = (tid - row * C4) * 4;
+    const int m = min(m0 + min(row, MT * 16 - 1), M - 1), n = min(t0 * 16 + c, N - 4);
+    P.x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
+  }
+}
 template <DT T, int MT, int NCT, int NW>
 __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT * 16][16 * NCT + 1], const Epi& e,
-                                                     int M, int N, int K, int m0, int t0) {
+                                                     int M, int N, int K, int m0, int t0, const FoldPre<MT, NW>& P) {
   constexpr int NT = 64 * NW, C4 = 4 * NCT;
   const int tid = threadIdx.x, wave = tid >> 6;
   __shared__ float2 rln[MT * 16];
   const bool fold = e.kind == EPI_LNFOLD_GELU16;
   if (fold) {
-    for (int r = wave; r < MT * 16; r += NW) {
-      const float2 st = row_ln_from_stats(e.stats + min(m0 + r, M - 1), e.stats_ld, K >> 4);
-      if ((tid & 63) == 0) rln[r] = st;
+#pragma unroll
+    for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j) {
+      const int r = wave + NW * j;
+      if (r < MT * 16) {  // (wave-uniform)
+        const float2 st = row_ln_stats_merge(P.sa[j], P.sb[j], K >> 4);
+        if ((tid & 63) == 0) rln[r] = st;
+      }
     }
     __syncthreads();
   }
@@ -1813,7 +1844,7 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
     }
     if (!fold) {
       float* xp = reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n;
-      const float4 x0 = ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x0 = idx == tid ? P.x0 : ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 b = ok && e.bias ? *reinterpret_cast<const float4*>(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
       // the order of the split-K path: x + bias + sum (reduce_ln4_kernel)
       const float4 x = make_float4(x0.x + b.x + v4[0], x0.y + b.y + v4[1], x0.z + b.z + v4[2], x0.w + b.w + v4[3]);
@@ -1828,7 +1859,7 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
       }
     } else if (ok) {
       const float2 ln = rln[row];
-      const float4 a = *reinterpret_cast<const float4*>(e.c1 + n), b = *reinterpret_cast<const float4*>(e.c2 + n);
+      const float4 a = P.c1, b = P.c2;  // (prefetched: a thread's column quad is the same in every row, NT % C4 == 0)
       const u16x4 h = {from_f32<T>(gelu_erf(ln.y * (v4[0] - ln.x * a.x) + b.x)),
                        from_f32<T>(gelu_erf(ln.y * (v4[1] - ln.x * a.y) + b.y)),
                        from_f32<T>(gelu_erf(ln.y * (v4[2] - ln.x * a.z) + b.z)),
@@ -1879,6 +1910,12 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     pbias = *reinterpret_cast<const float4*>(e.bias + min(t0 * 16 + (tid % (4 * NCT)) * 4, N - 4));
   float4 wsc4 = make_float4(1.f, 1.f, 1.f, 1.f);
   if constexpr (W8) wsc4 = *reinterpret_cast<const float4*>(wsc + min(t0 * 16 + (tid % (4 * NCT)) * 4, ntiles * 16 - 4));
+  // the folded-LayerNorm epilogues (S == 1): their statistics / residual loads ride ahead of the main loop
+  FoldPre<MT, NW> fpre;
+  const bool fold_epi = EPK == kPackedGeneric && !W8 && S == 1 &&
+                        (e.kind == EPI_RESID_STATS || e.kind == EPI_LNFOLD_GELU16);
+  if constexpr (EPK == kPackedGeneric && !W8)
+    if (fold_epi) packed_fold_prefetch<T, MT, NCT, NW>(fpre, e, M, N, K, m0, t0);
   f32x4 acc[MT][NCT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -1971,10 +2008,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   __syncthreads();
   // 4 consecutive columns per thread
   constexpr int C4 = 4 * NCT;  // column quads per row
-  bool fold_epi = false;
   if constexpr (EPK == kPackedGeneric && !W8) {  // (the folded step has no 8-bit form: host-checked)
-    fold_epi = S == 1 && (e.kind == EPI_RESID_STATS || e.kind == EPI_LNFOLD_GELU16);
-    if (fold_epi) packed_fold_epilogue<T, MT, NCT, NW>(red, e, M, N, K, m0, t0);
+    if (fold_epi) packed_fold_epilogue<T, MT, NCT, NW>(red, e, M, N, K, m0, t0, fpre);
   }
   for (int idx = tid; !fold_epi && idx < MT * 16 * C4; idx += NT) {
     const int row = idx / C4, c = (idx - row * C4) * 4;

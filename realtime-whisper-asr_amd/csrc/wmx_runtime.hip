@@ -169,9 +169,13 @@ struct Model {
   bool initialized = false;
   bool dirty = false;  // a tensor was set since the derived copies (row-major, MX-fp8, folded) were made
   bool fold = false;   // decode step on the LayerNorm-folded projections (WMX_FOLD=1; default: reduce_ln form)
+  // the mixed decode step (dec_step_mixed): the d x d residual producers (out-proj, cross-out) unsplit with row
+  // statistics and LN2 / LN3 folded into their consumers (the fused cross-q projection, fc1); fc2 stays split-K +
+  // reduce_ln.  16-bit models only (the fp8 decode keeps the fast step)
   // encoder: the two LayerNorms of every layer folded into qkv / fc1 (the residual producers leave x's 16-bit copy
   // and per-256-column statistics); 16-bit models with a width multiple of 256 (WMX_ENC_FOLD=0 turns it off)
   bool enc_fold = false;
+  bool mixed = false;
   hipStream_t st = nullptr;
 };
 
@@ -274,7 +278,7 @@ static void build_model(Model& m) {
     P.add(&L.c2fc1, 4 * da);
   }
   for (auto& L : m.dec) {
-    if (!m.fold) break;  // the folded copies exist only for the opt-in folded step (WMX_FOLD=1)
+    if (!m.fold && !m.mixed) break;  // the folded copies exist only for the folded / mixed steps
     P.add(&L.fqkv, (size_t)3 * dt * dt);
     P.add(&L.fcq, (size_t)dt * dt);
     P.add(&L.ffc1, (size_t)4 * dt * dt);
@@ -468,7 +472,7 @@ static void prepare_fold(Model& m) {
     }
     WMX_HIP(hipStreamSynchronize(m.st));
   }
-  if (!m.fold) return;
+  if (!m.fold && !m.mixed) return;
   const int dt = m.d.n_text_state;
   for (auto& L : m.dec) {
     launch_fold_ln(m.dt, L.rqkv, L.ln1g, L.ln1b, L.bqkv, 3 * dt, dt, L.fqkv, L.c1qkv, L.c2qkv, m.st);
@@ -1402,9 +1406,101 @@ static void dec_step_fold(Ctx& c, const FwdArgs& f) {
   debug_sync(c, "final_ln", -1);
 }
 
+// The mixed decode step: dec_step_fast with the two d x d residual producers of every layer (out-projection,
+// cross out-projection) unsplit -- x += acc + bias, its 16-bit copy and per-16-column row statistics in the GEMM
+// epilogue (EPI_RESID_STATS) -- so their reduce_ln launches go: LN2 is applied by the fused cross-q projection
+// through W diag(g2), c1, c2 (the cross attention merges the row statistics it loads beside its K batch), LN3 by fc1's
+// folded GELU epilogue.  fc2 (K = 4d) keeps split-K partials + reduce_ln (its unsplit form is 15 vs 11 us, DESIGN.md
+// §3), which also produces the next layer's LN1 rows for the split-K QKV.  8 launches per layer instead of 10.
+// Leaves LN_final(x) of every row in c.dhb.
+static void dec_step_mixed(Ctx& c, const FwdArgs& f) {
+  Model& m = *c.m;
+  const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
+  const int R = f.rows;
+  const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
+  launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, m.dec[0].ln1g, m.dec[0].ln1b, dt,
+                  c.dx, c.dhb, c.st, m.d.n_vocab);
+  const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
+  for (int l = 0; l < Lt; ++l) {
+    DecLayer& L = m.dec[l];
+    const bool last = l + 1 == Lt;
+    const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
+    const bool prev = c.probe_kernel >= 0 && l + 1 == c.probe_layer;
+    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
+    auto pbuf = [&](int id) { return probed ? c.probe_buf + id * probe_stride : nullptr; };
+    // self attention on LN1(x) (c.dhb): QKV partials -> (reduce, cache write, attention)
+    probe(kProbeQKV);
+    const int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt);
+    c.cur_probe = nullptr;
+    DecAttnArgs a{};
+    a.o = c.dao;
+    a.R = R;
+    a.Tn = 1;
+    a.H = H;
+    a.d = dt;
+    a.kc = c.kc + l * cache_layer;
+    a.vc = c.vc + l * cache_layer;
+    a.kv_R = c.R;
+    a.anc = f.anc;
+    a.anc_ld = c.Tctx;
+    a.pad = f.pad_seq;
+    a.slot0 = c.slot;
+    a.qpart = c.part;
+    a.qS = S;
+    a.qpart_stride = (long)R * 3 * dt;
+    a.qpart_ld = 3 * dt;
+    a.qbias = L.bqkv;
+    a.tprobe = pbuf(kProbeSelf);
+    launch_self_attn(c.dt, a, c.st);
+    // out-projection, unsplit: x += o Wo^T + bo, x16 -> c.dhb, row statistics -> c.rstat
+    probe(kProbeOut);
+    gemm_p_resid(c, c.dao, dt, L.wo, R, dt, dt, epi_resid_stats(c, L.bo, R));
+    c.cur_probe = nullptr;
+    // cross attention with the fused, LN2-folded query projection of x16
+    DecAttnArgs x{};
+    x.o = c.dao;
+    x.R = R;
+    x.Tn = 1;
+    x.H = H;
+    x.d = dt;
+    set_cross_images(c, x, l);
+    x.Tk = 1500;
+    x.rows_per_win = f.win_rows > 0 ? f.win_rows : c.K;
+    x.wq = L.fcq;
+    x.qin = c.dhb;
+    x.qin_ld = dt;
+    x.ln_c1 = L.c1cq;
+    x.ln_c2 = L.c2cq;
+    x.ln_stats = c.rstat;
+    x.ln_ld = R;
+    x.xcnt = c.xa_cnt;
+    x.slot0 = c.slot;
+    if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
+    launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    // cross out-projection, unsplit: x += o Wco^T + bco, x16, statistics
+    probe(kProbeCrossOut);
+    gemm_p_resid(c, c.dao, dt, L.wco, R, dt, dt, epi_resid_stats(c, L.bco, R));
+    // MLP: GELU(LN3-folded fc1 of x16) -> fc2 partials -> reduce_ln (x += ..., next layer's LN1 or the final LN)
+    probe(kProbeFc1);
+    Epi e1 = epi(EPI_LNFOLD_GELU16, nullptr, c.df1, 4 * dt);
+    e1.c1 = L.c1fc1;
+    e1.c2 = L.c2fc1;
+    e1.stats = c.rstat;
+    e1.stats_ld = R;
+    gemm_p(c, c.dhb, dt, L.ffc1, R, 4 * dt, dt, e1);
+    probe(kProbeFc2);
+    gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
+                 last ? m.lnb : m.dec[l + 1].ln1b,
+                 probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr);
+    c.cur_probe = nullptr;
+  }
+}
+
 static void dec_step(Ctx& c, const FwdArgs& f) {
   if (c.m->fold)
     dec_step_fold(c, f);
+  else if (c.m->mixed && c.xq_fused)
+    dec_step_mixed(c, f);
   else
     dec_step_fast(c, f);
 }
@@ -2199,6 +2295,10 @@ wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_mod
       // the split-K + reduce_ln step (356-390 vs 389-393x real time, interleaved on one box); it has
       // no 8-bit form (the fp8 decode ignores the switch)
       w->m.fold = getenv("WMX_FOLD") != nullptr && !w->m.w8;
+      {  // the mixed decode step (WMX_DEC_MIXED=1 while it is measured; 16-bit models)
+        const char* dm = getenv("WMX_DEC_MIXED");
+        w->m.mixed = !w->m.w8 && !w->m.fold && dm && dm[0] == '1';
+      }
       {
         const char* ef = getenv("WMX_ENC_FOLD");
         w->m.enc_fold = !w->m.mx8 && w->m.d.n_audio_state % 256 == 0 && !(ef && ef[0] == '0');

@@ -461,7 +461,8 @@ def test_folded_layernorm_step_parity():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, WMX_FOLD="1")
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
-           "-k", "not folded_layernorm and not full_depth", "tests/test_gpu_step.py"]
+           "-k", "not folded_layernorm and not full_depth and not mixed_step and not fused_mlp and not separate_cross_q",
+           "tests/test_gpu_step.py"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
@@ -483,6 +484,25 @@ def test_separate_cross_q_step_parity():
 
 
 @pytest.mark.timeout(900)
+def test_mixed_step_parity():
+    """The mixed decode step (WMX_DEC_MIXED=1, wmx_runtime.hip dec_step_mixed: the out-projection and the cross
+    out-projection unsplit with row statistics, LN2 folded into the fused cross-q projection of the cross attention,
+    LN3 into fc1's GELU epilogue; fc2 split-K + reduce_ln): this file's step, search and full-depth tests rerun in a
+    child process with the switch set (read at model creation)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WMX_DEC_MIXED="1")
+    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+           "-k", "not folded_layernorm and not mixed_step and not fused_mlp and not separate_cross_q",
+           "tests/test_gpu_step.py"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=880)
+    print(r.stdout[-1500:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
 def test_fused_mlp_step_parity():
     """The decode MLP as one launch (WMX_MLP_FUSED=1, wmx_gemm.hip mlp_fused_kernel: fc1 + GELU -> fc2 partials with
     the fc1 -> fc2 edge handed off inside the launch, write-through stores + slice counters): this file's teacher-forced
