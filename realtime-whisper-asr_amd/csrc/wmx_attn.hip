@@ -698,7 +698,9 @@ inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long
 // widened to the 16-bit MFMA operands in registers; the image scales enter exactly -- the K scale (a power of two)
 // multiplies the queries before their 16-bit rounding, the V scale the merged output -- and with XQ the fused
 // query projection's weights are 8-bit too (packed8_index, per-row scales a.wq_scale)
-template <DT T, int KPW, int NWV, bool XQ = false, bool F8 = false>
+// FQ (with XQ): LN2 folded into the fused query projection (the mixed step); its own instantiation, so the default
+// fused kernel does not carry the statistics registers (at the 128-VGPR cap of 4 waves per SIMD they spilled)
+template <DT T, int KPW, int NWV, bool XQ = false, bool F8 = false, bool FQ = false>
 __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   constexpr int NT = 64 * NWV;
   int h = blockIdx.x, w = blockIdx.y, zz = blockIdx.z;
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const float qs_col = (fuse_q && F8) ? a.wq_scale[h * 64 + (tid & 63)] : 1.f;
   // LN2 folded into the query weights (the mixed step, dec_step_mixed): qin is the 16-bit residual x and
   // q = rstd_row (p - mean_row c1[col]) + c2[col]; the constants now, the row statistics right after the K batch
-  const bool fold_q = fuse_q && a.ln_c1 != nullptr;
+  constexpr bool fold_q = fuse_q && FQ;  // (launcher: FQ iff a.ln_c1 with a.wq)
   const float qc1_col = fold_q ? a.ln_c1[h * 64 + (tid & 63)] : 0.f;
   const float qc2_col = fold_q ? a.ln_c2[h * 64 + (tid & 63)] : 0.f;
   float2 lnA[2], lnB[2];
@@ -1147,12 +1149,22 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
   WMX_CHECK(!a.wq || (waves == 8 && nq <= 16), "cross attn: the fused query projection runs on the 8-wave decode kernel");
   if (a.wq) {
     const int per_wave = ((chunk + 7) / 8 + 31) / 32;
+    const bool fq = a.ln_c1 != nullptr;  // (16-bit only: launch_cross_attn's check)
+#define WMX_XQ_LAUNCH(KPW)                                                                                           \
+  if constexpr (!F8) {                                                                                             \
+    if (fq) {                                                                                                      \
+      hipLaunchKernelGGL((dec_cross_attn_kernel<T, KPW, 8, true, false, true>), grid, dim3(512), 0, st, a, KS, chunk, ws); \
+      break;                                                                                                       \
+    }                                                                                                              \
+  }                                                                                                                \
+  hipLaunchKernelGGL((dec_cross_attn_kernel<T, KPW, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws);
     switch (std::min(per_wave, 4)) {
-      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
-      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8, true, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;
+      case 1: WMX_XQ_LAUNCH(1) break;
+      case 2: WMX_XQ_LAUNCH(2) break;
+      case 3: WMX_XQ_LAUNCH(3) break;
+      default: WMX_XQ_LAUNCH(4) break;
     }
+#undef WMX_XQ_LAUNCH
     return;
   }
   if (waves == 8 && nq <= 16) {

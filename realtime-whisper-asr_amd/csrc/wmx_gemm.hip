@@ -1791,8 +1791,11 @@ template <int MT, int NW>
 struct FoldPre {
   static constexpr int RPW = (MT * 16 + NW - 1) / NW;  // statistics rows per wave (rows wave + NW j)
   float2 sa[RPW], sb[RPW];
-  float4 x0;  // EPI_RESID_STATS: the residual quad of this thread's first epilogue item (idx = tid)
-  float4 c1, c2;  // EPI_LNFOLD_GELU16: the folded constants of the thread's column quad (the same in every row)
+  // EPI_RESID_STATS: q0 = the residual quad of this thread's first epilogue item (idx = tid); EPI_LNFOLD_GELU16:
+  // q0 / q1 = the folded constants c1 / c2 of the thread's column quad (the same in every row).  One slot for both
+  // kinds, each assigned whole: two members loaded on either side of a branch were merged into one load stored
+  // through a selected pointer, which demoted the whole struct to scratch in every generic instantiation
+  float4 q0, q1;
 };
 template <DT T, int MT, int NCT, int NW>
 __device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const Epi& e, int M, int N, int K, int m0,
@@ -1804,12 +1807,13 @@ __device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const E
     for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j)
       row_ln_stats_load(e.stats + min(m0 + min(wave + NW * j, MT * 16 - 1), M - 1), e.stats_ld, K >> 4, P.sa[j], P.sb[j]);
     const int n = min(t0 * 16 + (tid % C4) * 4, N - 4);
-    P.c1 = *reinterpret_cast<const float4*>(e.c1 + n);
-    P.c2 = *reinterpret_cast<const float4*>(e.c2 + n);
+    P.q0 = *reinterpret_cast<const float4*>(e.c1 + n);
+    P.q1 = *reinterpret_cast<const float4*>(e.c2 + n);
   } else {
     const int row = tid / C4, c = (tid - row * C4) * 4;
     const int m = min(m0 + min(row, MT * 16 - 1), M - 1), n = min(t0 * 16 + c, N - 4);
-    P.x0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
+    P.q0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
+    P.q1 = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 template <DT T, int MT, int NCT, int NW>
@@ -1844,7 +1848,7 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
     }
     if (!fold) {
       float* xp = reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n;
-      const float4 x0 = idx == tid ? P.x0 : ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x0 = idx == tid ? P.q0 : ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 b = ok && e.bias ? *reinterpret_cast<const float4*>(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
       // the order of the split-K path: x + bias + sum (reduce_ln4_kernel)
       const float4 x = make_float4(x0.x + b.x + v4[0], x0.y + b.y + v4[1], x0.z + b.z + v4[2], x0.w + b.w + v4[3]);
@@ -1859,7 +1863,7 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
       }
     } else if (ok) {
       const float2 ln = rln[row];
-      const float4 a = P.c1, b = P.c2;  // (prefetched: a thread's column quad is the same in every row, NT % C4 == 0)
+      const float4 a = P.q0, b = P.q1;  // (prefetched: a thread's column quad is the same in every row, NT % C4 == 0)
       const u16x4 h = {from_f32<T>(gelu_erf(ln.y * (v4[0] - ln.x * a.x) + b.x)),
                        from_f32<T>(gelu_erf(ln.y * (v4[1] - ln.x * a.y) + b.y)),
                        from_f32<T>(gelu_erf(ln.y * (v4[2] - ln.x * a.z) + b.z)),

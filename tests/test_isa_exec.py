@@ -36,3 +36,35 @@ def test_no_mfma_under_possibly_empty_exec():
 def test_check_flags_the_guarded_variant():
     r = _run(GUARDED)
     assert r.returncode == 1 and "gemm_packed_kernel" in r.stdout, r.stdout
+
+
+# Kernels allowed a private segment (tools/scratch_check.py), each for a stated reason; any other kernel that grows
+# one fails here, so a register-pressure regression on the decode / encoder path is caught at build time (round 4:
+# a prefetch struct demoted to scratch in every S == 1 packed-GEMM instantiation cost the mixed step's fc1 5 us).
+SCRATCH_ALLOWED = [
+    (r"gemm256_kernelILNS_2DTE\dELin1E", "generic-epilogue fallback for N % 4 != 0 (no hot-path shape)"),
+    (r"gemm256_kernelILNS_2DTE1ELi11E", "f16 only, 12 bytes"),
+    (r"gemm_mx8_256_kernelILNS_2DTE\dELi2E", "MX-fp8 residual epilogue, 3 dwords outside the main loop"),
+    (r"enc_attn_kernelILNS_2DTE\dELi8ELi4E", "one VGPR stored before and reloaded after the key loop"),
+    (r"gemm_packed_kernelILNS_2DTE\dELi\dELi\dELi16ELi3E", "RedTail (opt-in WMX_REDLN_FUSED)"),
+    (r"dec_cross_attn_kernelILNS_2DTE\dELi[12]ELi\dELb\dELb0E",
+     "16-bit images at <= 2 key blocks per wave under the 128-VGPR cap (not the default 1024-key decode chunk)"),
+]
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libwmx.so not built")
+def test_no_unexpected_scratch():
+    import re
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from scratch_check import kernels
+
+    ks = kernels(LIB)
+    assert len(ks) > 100
+    bad = [n for n, (priv, _spill) in ks.items() if priv and not any(re.search(p, n) for p, _ in SCRATCH_ALLOWED)]
+    assert not bad, "kernels with an unexpected private segment:\n" + "\n".join(bad)
+    # the default decode kernels are in the library and scratch-free
+    for pat in (r"dec_cross_attn_kernelILNS_2DTE0ELi4ELi8ELb1ELb0ELb0E", r"dec_cross_attn_kernelILNS_2DTE0ELi2ELi8ELb1ELb1ELb0E",
+                r"gemm_packed_kernelILNS_2DTE0ELi2ELi4ELi16ELi2ELb0E", r"dec_self_attn_kernel"):
+        hits = [n for n in ks if re.search(pat, n)]
+        assert hits and all(ks[n][0] == 0 for n in hits), pat
