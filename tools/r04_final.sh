@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 4, final measurement pass: the whole -m gpu suite, smoke, the default bench line (with the CPU baseline),
+# round 4, final measurement pass (two calls: '<tag> tests' = the whole -m gpu suite + smoke; '<tag> bench' =
+# the default bench line (with the CPU baseline),
 # the f16 line, the MX-fp8 / bf16 encoder at 16 windows, and a rocprofv3 kernel-trace summary (the trace itself
 # is deleted on the box: only the stats come back)
 set -o pipefail
@@ -11,11 +12,23 @@ export PYTHONUNBUFFERED=1
 (while sleep 50; do date >> $O/heartbeat.txt; done) &
 HB=$!
 trap "kill $HB" EXIT
-if [ "${2:-tests}" = tests ]; then
-  timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread --durations=25 -m gpu tests > $O/gputest.log 2>&1
-  rc=$?; tail -3 $O/gputest.log
+# the suite in two calls (each under gpurun's 20-minute limit): 'tests1' = every file but test_gpu_step.py,
+# 'tests2' = test_gpu_step.py + smoke
+if [ "${2:-tests1}" = tests1 ]; then
+  timeout -k 10 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread --durations=25 -m gpu tests \
+    --ignore=tests/test_gpu_step.py > $O/gputest1.log 2>&1
+  rc=$?; tail -3 $O/gputest1.log
+  if [ $rc -ne 0 ]; then echo "gpu tests failed (rc $rc): stopping"; exit 1; fi
+  exit 0
+fi
+if [ "${2}" = tests2 ]; then
+  timeout -k 10 1000 python -u -m pytest -x -v --timeout 600 --timeout-method thread --durations=25 -m gpu \
+    tests/test_gpu_step.py > $O/gputest2.log 2>&1
+  rc=$?; tail -3 $O/gputest2.log
   if [ $rc -ne 0 ]; then echo "gpu tests failed (rc $rc): stopping"; exit 1; fi
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; exit 1; }
+  echo "tests + smoke ok"
+  exit 0
 fi
 timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { echo bench failed; exit 1; }
 head -c 300 $O/bench_default.json; echo
