@@ -594,6 +594,12 @@ struct Ctx {
   float *scores = nullptr, *align_out = nullptr, *tprob = nullptr;
   int *a_ntok = nullptr, *a_nframes = nullptr, *a_target = nullptr, *a_heads = nullptr;
   int a_heads_cap = 0;
+  // the alignment heads grouped by layer, uploaded once at context creation: layer l's heads are
+  // a_heads[a_head_off[l] .. + a_head_cnt[l]) (no per-layer upload and stream sync in the alignment forward)
+  std::vector<int> a_head_off, a_head_cnt, a_head_flat;
+  // pinned host images of the alignment matrix [B][T][1500] and the text-token probabilities [B][T]: their D2H is a
+  // DMA instead of a staged copy into fresh pageable vectors (round 4: 1.4 ms of idle GPU per call and group)
+  float *h_align = nullptr, *h_tp = nullptr;
   int* pinned_i = nullptr;
   // decode-step graphs, kept across calls: [0] one step, [1] kGraphChunk steps; valid while graph_key matches
   // (batch, the rule options baked into the captured launches, the probe placement)
@@ -628,7 +634,7 @@ struct Ctx {
   int rec_cap = 0, rec_R = 0;
   // word-alignment matrices of the last transcribe (wmx_ctx_alignment_matrix, tests): [B][Tn][1500] as the DTW read
   // them, and per window the text-token count and the content frames
-  std::vector<float> last_align;
+  bool last_align_ok = false;  // h_align holds the last transcribe's matrices
   std::vector<int> last_ntext, last_nframes;
   int last_align_Tn = 0;
 };
@@ -755,6 +761,20 @@ static void alloc_ctx(Ctx& c) {
   WMX_HIP(hipMemsetAsync(c.buf, 0, P.off, c.st));
   P.bind(c.buf);
   WMX_HIP(hipHostMalloc(&c.pinned_i, 64));
+  WMX_HIP(hipHostMalloc(&c.h_align, (size_t)B * T * 1500 * sizeof(float)));
+  WMX_HIP(hipHostMalloc(&c.h_tp, (size_t)B * T * sizeof(float)));
+  c.a_head_off.assign(Lt, 0);
+  c.a_head_cnt.assign(Lt, 0);
+  c.a_head_flat.clear();
+  for (int l = 0; l < Lt; ++l) {
+    c.a_head_off[l] = (int)c.a_head_flat.size();
+    for (size_t i = 0; i + 1 < c.align_heads.size(); i += 2)
+      if (c.align_heads[i] == l) c.a_head_flat.push_back(c.align_heads[i + 1]);
+    c.a_head_cnt[l] = (int)c.a_head_flat.size() - c.a_head_off[l];
+  }
+  WMX_CHECK((int)c.a_head_flat.size() <= c.a_heads_cap, "alignment heads: table overflow");
+  if (!c.a_head_flat.empty())
+    WMX_HIP(hipMemcpyAsync(c.a_heads, c.a_head_flat.data(), c.a_head_flat.size() * 4, hipMemcpyHostToDevice, c.st));
   // suppress bitmask
   std::vector<uint32_t> mask((V + 31) / 32, 0u);
   for (int t : c.suppress)
@@ -1581,13 +1601,9 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
       a.xcnt = c.xa_cnt;
       launch_cross_attn(c.dt, a, c.xa_ws, c.st);
     }
-    if (f.align) {
-      // alignment heads of this layer
-      std::vector<int> hs;
-      for (size_t i = 0; i + 1 < c.align_heads.size(); i += 2)
-        if (c.align_heads[i] == l) hs.push_back(c.align_heads[i + 1]);
-      if (!hs.empty()) {
-        WMX_HIP(hipMemcpyAsync(c.a_heads, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, c.st));
+    if (f.align && c.a_head_cnt[l] > 0) {  // this layer's alignment heads (the device table, alloc_ctx)
+      const int nh = c.a_head_cnt[l];
+      {
         DecAttnArgs a{};
         a.q = c.dcq;
         a.q_ld = dt;
@@ -1598,11 +1614,9 @@ static void dec_forward(Ctx& c, const FwdArgs& f) {
         set_cross_images(c, a, l);
         a.Tk = 1500;
         a.rows_per_win = 1;
-        launch_cross_scores(c.dt, a, c.a_heads, (int)hs.size(), c.scores, c.st);
-        launch_align_matrix_acc(c.scores, (int)hs.size(), rowsT, 1500, f.Tn, c.a_ntok, c.a_nframes,
-                                c.o.median_filter_width, f.rows, c.st, c.align_out);
-        // hipMemcpyAsync of a host vector: make sure it completed before hs goes out of scope
-        sync(c);
+        launch_cross_scores(c.dt, a, c.a_heads + c.a_head_off[l], nh, c.scores, c.st);
+        launch_align_matrix_acc(c.scores, nh, rowsT, 1500, f.Tn, c.a_ntok, c.a_nframes, c.o.median_filter_width,
+                                f.rows, c.st, c.align_out);
       }
     }
     gemm_p(c, c.dao, dt, L.wco, rowsT, dt, dt, epi(EPI_RESID32, L.bco, c.dx, dt), L.rco, w8_of(m, L.q8co, L.s8co));
@@ -2171,9 +2185,11 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
       launch_text_prob(c.logits, c.ldl, sp.eot, c.a_target + r0, n, c.tprob + r0, c.st);
       sync(c);
     }
-    std::vector<float> mat((size_t)B * Tn * 1500), tp((size_t)B * Tn);
-    WMX_HIP(hipMemcpyAsync(mat.data(), c.align_out, mat.size() * 4, hipMemcpyDeviceToHost, c.st));
-    WMX_HIP(hipMemcpyAsync(tp.data(), c.tprob, tp.size() * 4, hipMemcpyDeviceToHost, c.st));
+    c.last_align_ok = false;
+    float* const mat = c.h_align;  // [B][Tn][1500], pinned
+    float* const tp = c.h_tp;
+    WMX_HIP(hipMemcpyAsync(mat, c.align_out, (size_t)B * Tn * 1500 * 4, hipMemcpyDeviceToHost, c.st));
+    WMX_HIP(hipMemcpyAsync(tp, c.tprob, (size_t)B * Tn * 4, hipMemcpyDeviceToHost, c.st));
     sync(c);
     // DTW per window on host threads
     std::vector<std::thread> th;
@@ -2185,12 +2201,12 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
         for (int b = next++; b < B; b = next++) {
           WindowOut& wo = res->data[b];
           const int n = ntext[b] + 1, nf = nframes[b] / 2;
-          wo.probs.assign(tp.begin() + (size_t)b * Tn + 3, tp.begin() + (size_t)b * Tn + 3 + ntext[b]);
+          wo.probs.assign(tp + (size_t)b * Tn + 3, tp + (size_t)b * Tn + 3 + ntext[b]);
           if (nf <= 0) {
             wo.jump_times.assign(n, 0.f);
             continue;
           }
-          dtw(mat.data() + ((size_t)b * Tn + 3) * 1500, n, nf, 1500, ti, tj);
+          dtw(mat + ((size_t)b * Tn + 3) * 1500, n, nf, 1500, ti, tj);
           wo.jump_times.clear();
           for (size_t k = 0; k < ti.size(); ++k)
             if (k == 0 || ti[k] != ti[k - 1]) wo.jump_times.push_back(tj[k] / 50.0f);
@@ -2198,7 +2214,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
         }
       });
     for (auto& x : th) x.join();
-    c.last_align.swap(mat);  // kept for wmx_ctx_alignment_matrix (a swap: no copy on the hot path)
+    c.last_align_ok = true;  // h_align is read by wmx_ctx_alignment_matrix until the next transcribe
     c.last_ntext = ntext;
     c.last_nframes = nframes;
     c.last_align_Tn = Tn;
@@ -2532,9 +2548,12 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       alloc_ctx(c);
     } catch (...) {
       if (c.buf) (void)hipFree(c.buf);
-  if (c.dsp_scratch) (void)hipFree(c.dsp_scratch);
-  if (c.dsp_io) (void)hipFree(c.dsp_io);
-  if (c.dsp_lens) (void)hipFree(c.dsp_lens);
+      if (c.dsp_scratch) (void)hipFree(c.dsp_scratch);
+      if (c.dsp_io) (void)hipFree(c.dsp_io);
+      if (c.dsp_lens) (void)hipFree(c.dsp_lens);
+      for (void* p : {(void*)c.pinned_i, (void*)c.h_align, (void*)c.h_tp})
+        if (p) (void)hipHostFree(p);
+      if (c.st) (void)hipStreamDestroy(c.st);
       delete x;
       throw;
     }
@@ -2551,6 +2570,8 @@ void wmx_ctx_destroy(wmx_ctx* x) {
   free_recorder(c);
   if (c.buf) (void)hipFree(c.buf);
   if (c.pinned_i) (void)hipHostFree(c.pinned_i);
+  if (c.h_align) (void)hipHostFree(c.h_align);
+  if (c.h_tp) (void)hipHostFree(c.h_tp);
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
   if (c.st) (void)hipStreamDestroy(c.st);
@@ -2829,14 +2850,14 @@ wmx_status wmx_ctx_alignment_matrix(wmx_ctx* x, int b, float* out, int* n, int* 
   return guard([&] {
     Ctx& c = x->c;
     WMX_CHECK(n && nf, "alignment_matrix: null argument");
-    WMX_CHECK(!c.last_align.empty() && b >= 0 && b < (int)c.last_ntext.size(),
+    WMX_CHECK(c.last_align_ok && b >= 0 && b < (int)c.last_ntext.size(),
               "alignment_matrix: no word alignment for this window in the last transcribe");
     const int rows = c.last_ntext[b] + 1, cols = c.last_nframes[b] / 2;
     *n = rows;
     *nf = cols;
     if (!out) return;
     for (int i = 0; i < rows; ++i)
-      std::memcpy(out + (size_t)i * cols, c.last_align.data() + ((size_t)b * c.last_align_Tn + 3 + i) * 1500,
+      std::memcpy(out + (size_t)i * cols, c.h_align + ((size_t)b * c.last_align_Tn + 3 + i) * 1500,
                   (size_t)std::max(cols, 0) * 4);
   });
 }
