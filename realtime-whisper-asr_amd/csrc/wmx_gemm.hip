@@ -1873,6 +1873,9 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
   }
 }
 
+#ifndef WMX_PART_ST
+#define WMX_PART_ST 0  // split-K partial stores: 0 plain (default), 1 non-temporal, 2 write-through sc1 (A/B builds)
+#endif
 // Epilogue class, a template parameter so each launch carries only the code it runs (these launches are a few
 // microseconds long and start on a cold instruction cache: a generic epilogue switch in a split-K launch measured
 // +0.6 us per launch): kPackedPart split-K raw partials (S > 1); kPackedGelu S == 1 bias + GELU -> 16-bit
@@ -2042,7 +2045,13 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     } else if (EPK == kPackedPart || S > 1) {
       float* dst = part + ((long)sp * M + m) * N + n;
       if (n + 3 < N && (N & 3) == 0) {
+#if WMX_PART_ST == 2  // A/B build switch: write-through (sc1) partial stores, no dirty L2 lines at the boundary
+        tail_st4(tail_rsrc(part), ((long)sp * M + m) * N + n, make_float4(v4[0], v4[1], v4[2], v4[3]));
+#elif WMX_PART_ST == 1  // non-temporal partial stores
+        __builtin_nontemporal_store(f32x4{v4[0], v4[1], v4[2], v4[3]}, reinterpret_cast<f32x4*>(dst));
+#else
         *reinterpret_cast<float4*>(dst) = make_float4(v4[0], v4[1], v4[2], v4[3]);
+#endif
       } else {
         for (int q = 0; q < 4 && n + q < N; ++q) dst[q] = v4[q];
       }
