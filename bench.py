@@ -551,6 +551,17 @@ def main():
                        "rule": "cross attention / (packed GEMMs + reduce_ln) in situ >= 0.35 -> fast"}
         if args.dtype == "fp8":  # the fp8 decode halves the cross attention's bytes: the bf16 calibration does not hold
             decode_mode["mode"] = "n/a (rule calibrated on the bf16 decode)"
+        # per context group: the slow mode can hit one group alone, and the call takes the
+        # slower group's time; each group's decode stage and its own ratio
+        per_group = []
+        for c in ctxs:
+            ev_g = c.probe_launches(e2e=True)
+            ch = [k for k in chain if ev_g.get(k, (0, 0))[1]]
+            r_g = (ev_g["cross_attn"][0] / sum(ev_g[k][0] for k in ch)
+                   if ch and ev_g.get("cross_attn", (0, 0))[1] else None)
+            per_group.append({"decode_stage_ms": round(c.stage_ms()[5], 2),
+                              "cross_to_chain_ratio": round(r_g, 4) if r_g is not None else None})
+        decode_mode["groups"] = per_group
         log(f"[rank {rank}] decode mode: {decode_mode}")
     # the other named stages: the log-mel front end (north_star: HBM GB/s of the mel path) and the self attention,
     # replayed alone with HIP events on the context stream
