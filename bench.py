@@ -394,6 +394,13 @@ def main():
                            language=None, word_timestamps=True, alignment_heads=heads, use_graph=not args.no_graph)
             for _ in range(G)]
     ctx = ctxs[0]
+    # the groups' decode loops start together (wmx_ctx_set_lockstep): in step they share each layer's weight reads
+    # through the caches; started a few layers apart they do not, and the call runs ~5 % slower (the
+    # slow decode mode).  WMX_LOCKSTEP=0 turns it off (A/B runs)
+    lockstep = G > 1 and os.environ.get("WMX_LOCKSTEP", "1") != "0"
+    if lockstep:
+        for c in ctxs:
+            c.set_lockstep(1, G)
     # synthetic 30 s streams, resident in HBM before the timed region
     audio = np.stack([synth.speech_like(rank * B + i, 480000) for i in range(B)])
     pcm = torch.from_numpy(audio).to(f"cuda:{local}")
@@ -644,6 +651,7 @@ def main():
                    "use_graph": not args.no_graph, "context_groups": G},
         "stage_ms": [round(s, 2) for s in stages],
         "decode_mode": decode_mode,
+        "lockstep": lockstep,
         "roofline": roof,
         "encoder": encoder,
         "logmel": logmel,

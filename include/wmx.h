@@ -294,8 +294,19 @@ wmx_status wmx_ctx_set_probe(wmx_ctx* c, int kernel, int layer);
  * microseconds before this context's decode loop shifts its phase against the other group's, so their HBM-heavy
  * (cross attention) and latency-bound launches overlap each other instead of coinciding.  0 = none. */
 wmx_status wmx_ctx_set_phase_offset(wmx_ctx* c, double us);
+/* context groups decoding concurrently on one GPU (e.g. the bench's two groups, one host thread each): contexts set to
+ * the same key (!= 0) with n_members >= 2 meet at a host barrier right before their decode loops (5 ms timeout), so
+ * their step graphs start together and stay in step -- each layer's weights are then read once for all groups (the
+ * later reader hits the caches). Every member must call wmx_transcribe concurrently with the others; a member that does
+ * not costs the others the timeout. key 0 leaves the group. */
+wmx_status wmx_ctx_set_lockstep(wmx_ctx* c, int key, int n_members);
 wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
 wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* span_ms, double* bytes, int* span_n, float* e2e_ms, int* e2e_n);
+/* the probes' raw device wall-clock ticks of the last transcribe (diagnostics: the relative phase of two context
+ * groups, per-step durations): lo_hi[(s * 12 + k) * 2 + {0, 1}] = earliest workgroup start / latest workgroup end of
+ * launch id k at the s-th probed decode step, 0 when not recorded; *n_steps = steps written (lo_hi may be null to
+ * query; capacity 448 steps), *wall_khz = the tick rate. */
+wmx_status wmx_ctx_probe_ticks(wmx_ctx* c, uint64_t* lo_hi, int* n_steps, double* wall_khz);
 
 #ifdef __cplusplus
 }

@@ -14,10 +14,12 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unistd.h>
@@ -534,6 +536,34 @@ enum {
   kProbeRedOut, kProbeRedCrossOut, kProbeRedFc2, kProbePrev, kProbeLaunches = 12
 };
 
+// Context groups that decode concurrently on one GPU (wmx_ctx_set_lockstep): a host barrier right before the
+// decode loop so that the groups' step graphs start together. In step, the groups run the same launch of the same
+// layer at the same time and read its weights once between them (the second reader hits the caches); started a few
+// layers apart, each streams the weights from HBM on its own and the decode runs ~5 % slower, a state that persists
+// for the whole call because both groups keep the same period (the slow decode mode).
+struct Lockstep {
+  std::mutex mu;
+  std::condition_variable cv;
+  int n = 0, arrived = 0;
+  unsigned long long gen = 0;
+  // true when all n members arrived within the timeout (a member that is not decoding costs the others one timeout)
+  bool arrive(std::chrono::microseconds timeout) {
+    std::unique_lock<std::mutex> lk(mu);
+    const unsigned long long g = gen;
+    if (++arrived >= n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    const bool ok = cv.wait_for(lk, timeout, [&] { return gen != g; });
+    if (!ok) --arrived;
+    return ok;
+  }
+};
+static std::mutex g_lockstep_mu;
+static std::map<int, std::shared_ptr<Lockstep>> g_lockstep;  // by wmx_ctx_set_lockstep key
+
 struct Ctx {
   Model* m = nullptr;
   wmx_opts o{};
@@ -623,6 +653,8 @@ struct Ctx {
   double probe_bytes[kProbeLaunches] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   double start_delay_us = 0;    // wmx_ctx_set_phase_offset: idle time before the decode loop (group phase offset)
+  std::shared_ptr<struct Lockstep> lockstep;  // wmx_ctx_set_lockstep: the decode loops of the group start together
+  bool lockstep_ok = false;                   // the last call's barrier saw every member
   bool xq_fused = true;         // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED=0: off)
   bool mlp_fused = false;       // decode step: fc1 -> fc2 in one launch, in-launch hand-off (WMX_MLP_FUSED=1)
   float stage_ms[7] = {0};
@@ -1995,12 +2027,20 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
   if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
+  if (c.lockstep && steps < max_new) {  // idle stream, then the group's barrier: the step graphs start together
+    sync(c);
+    c.lockstep_ok = c.lockstep->arrive(std::chrono::microseconds(5000));
+  }
   if (c.start_delay_us > 0 && steps < max_new) launch_spin((unsigned long long)(c.start_delay_us * c.wall_khz / 1000.0), c.st);
   while (steps < max_new) {
     const int chunk = std::min(kGraphChunk, max_new - steps);
     if (!c.o.use_graph) {
       for (int i = 0; i < chunk; ++i) run_step(c, B);
     } else if (chunk == kGraphChunk) {
+      // (diagnostic A/B, WMX_LOCKSTEP_CHUNKS=1: the group's barrier before every chunk, not only the first; valid
+      // only while every member runs the same number of chunks, i.e. no early stop)
+      static const bool every_chunk = getenv("WMX_LOCKSTEP_CHUNKS") && atoi(getenv("WMX_LOCKSTEP_CHUNKS")) == 1;
+      if (c.lockstep && every_chunk && steps > 0) c.lockstep->arrive(std::chrono::microseconds(5000));
       WMX_HIP(hipGraphLaunch(c.graph[1], c.st));  // one launch per chunk: no per-step graph launch bubble
     } else {
       for (int i = 0; i < chunk; ++i) WMX_HIP(hipGraphLaunch(c.graph[0], c.st));
@@ -3083,6 +3123,53 @@ wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* span_ms, double* bytes, int
       if (e2e_ms) e2e_ms[k] = (float)e2e[k];
       if (e2e_n) e2e_n[k] = en[k];
     }
+  });
+}
+
+wmx_status wmx_ctx_set_lockstep(wmx_ctx* x, int key, int n_members) {
+  return guard([&] {
+    Ctx& c = x->c;
+    if (key == 0) {
+      c.lockstep.reset();
+      return;
+    }
+    WMX_CHECK(n_members >= 2 && n_members <= 64, "lockstep: 2..64 members");
+    std::lock_guard<std::mutex> g(g_lockstep_mu);
+    auto& p = g_lockstep[key];
+    if (!p) {
+      p = std::make_shared<Lockstep>();
+      p->n = n_members;
+    }
+    WMX_CHECK(p->n == n_members, "lockstep: this key was created with another member count");
+    c.lockstep = p;
+  });
+}
+
+wmx_status wmx_ctx_probe_ticks(wmx_ctx* x, uint64_t* lo_hi, int* n_steps, double* wall_khz) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(n_steps && wall_khz, "probe_ticks: null argument");
+    const int T = c.Tctx;
+    const int s0 = c.probe_slots[0], s1 = std::min(c.probe_slots[1], T);
+    *n_steps = std::max(0, s1 - s0);
+    *wall_khz = c.wall_khz;
+    if (!lo_hi || *n_steps == 0) return;
+    std::vector<unsigned long long> tk((size_t)kProbeLaunches * T * kProbeWG * 2);
+    WMX_HIP(hipStreamSynchronize(c.st));
+    WMX_HIP(hipMemcpy(tk.data(), c.probe_buf, tk.size() * 8, hipMemcpyDeviceToHost));
+    for (int sl = s0; sl < s1; ++sl)
+      for (int k = 0; k < kProbeLaunches; ++k) {
+        unsigned long long lo = ~0ull, hi = 0;
+        const unsigned long long* r = tk.data() + ((size_t)k * T + sl) * kProbeWG * 2;
+        for (int w = 0; w < kProbeWG; ++w)
+          if (r[2 * w + 1] > r[2 * w] && r[2 * w] != 0) {
+            lo = std::min(lo, r[2 * w]);
+            hi = std::max(hi, r[2 * w + 1]);
+          }
+        uint64_t* o = lo_hi + ((size_t)(sl - s0) * kProbeLaunches + k) * 2;
+        o[0] = hi > lo ? lo : 0;
+        o[1] = hi > lo ? hi : 0;
+      }
   });
 }
 

@@ -368,6 +368,21 @@ class Context:
             ms, n = ems, en
         return {k: (float(ms[i]), int(n[i]), float(by[i])) for i, k in enumerate(self.PROBE_LAUNCHES)}
 
+    def set_lockstep(self, key: int, n_members: int):
+        """Join (key != 0) or leave (key 0) a lockstep group of contexts that transcribe concurrently: their decode
+        loops start together (wmx_ctx_set_lockstep)."""
+        check(lib.wmx_ctx_set_lockstep(self._h, int(key), int(n_members)))
+
+    def probe_ticks(self):
+        """(ticks [steps][12][2] uint64 earliest start / latest end per probed launch, wall-clock kHz) of the last
+        transcribe (wmx_ctx_probe_ticks; 0 = not recorded)."""
+        n, khz = C.c_int(), C.c_double()
+        check(lib.wmx_ctx_probe_ticks(self._h, None, C.byref(n), C.byref(khz)))
+        t = np.zeros((max(n.value, 1), len(self.PROBE_LAUNCHES), 2), np.uint64)
+        if n.value:
+            check(lib.wmx_ctx_probe_ticks(self._h, t.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(n), C.byref(khz)))
+        return t[:n.value], float(khz.value)
+
     def bench_kernel(self, kernel: str, batch: int, iters: int = 50):
         """Average launch duration (ms) of one hot-path kernel replayed on the context stream (HIP events),
         with its algorithmic bytes and flops per launch."""
