@@ -112,3 +112,38 @@ def test_two_groups_concurrent_equal_sequential_and_replay(ct):
     print("detected languages per group", opt_langs)
     for c in ctxs:
         c.record(0)
+
+
+def test_lockstep_groups_equal_alone_and_a_lone_member_proceeds():
+    """wmx_ctx_set_lockstep (bench.py's default for its two groups): the groups' decode loops meet at a host barrier.
+    Results stay bit-identical to each context run alone, and a member transcribing without its partner proceeds
+    after the barrier's timeout instead of hanging."""
+    import time
+
+    from wmx import engine as E
+    m = E.Model(_edims(WIDE2), 0, "bfloat16").init_synthetic(6)
+    n_new = 24
+    ctxs = [E.Context(m, max_batch=2, beam_size=5, max_new_tokens=n_new, language=None, word_timestamps=True,
+                      use_graph=True) for _ in range(2)]
+    audios = [synth.speech_like(950 + i, 480000) for i in range(4)]
+    batches = [audios[:2], audios[2:]]
+    alone = [ctxs[g].transcribe(batches[g]) for g in range(2)]
+    for c in ctxs:
+        c.set_lockstep(11, 2)
+    for rep in range(2):
+        both = _run_concurrently(ctxs, batches)
+        for g in range(2):
+            for b in range(2):
+                _same(both[g][b], alone[g][b], f"lockstep rep {rep} group {g} window {b}")
+    t = time.perf_counter()
+    lone = ctxs[0].transcribe(batches[0])  # partner absent: one 5 ms barrier timeout, then the decode
+    dt = time.perf_counter() - t
+    for b in range(2):
+        _same(lone[b], alone[0][b], f"lone member window {b}")
+    both = _run_concurrently(ctxs, batches)  # the group recovers on the next concurrent call
+    for g in range(2):
+        for b in range(2):
+            _same(both[g][b], alone[g][b], f"after the lone call, group {g} window {b}")
+    for c in ctxs:
+        c.set_lockstep(0, 0)
+    print(f"lone member call {1e3 * dt:.1f} ms")
