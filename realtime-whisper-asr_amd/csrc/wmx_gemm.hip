@@ -2097,10 +2097,15 @@ int packed_splits(int M, int N, int K, long cap_elems) {
   const int chunks = (M + mt * 16 - 1) / (mt * 16);
   const int nct = packed_nct(M, N, K);
   const long wgs = (long)((N + 16 * nct - 1) / (16 * nct)) * chunks;
-  static const long target = [] {  // workgroups a split aims for; WMX_PACKED_TARGET overrides (tuning runs)
-    const char* v = getenv("WMX_PACKED_TARGET");
-    return v ? std::max(1L, atol(v)) : 480L;
+  // workgroups a split aims for: 160 up to 24 rows (the bench's two groups of 4 windows x beam 5 decode in step, so
+  // two launches of this size run at once; fewer slices = fewer partials for the consumers: 414.3-414.7x against
+  // 410.5-410.8x with 480, profiles/r04_split_target/), 480 above (16 windows: 724.6 / 568.0x against 723.1 / 562.6x
+  // with 240); WMX_PACKED_TARGET overrides (tuning runs)
+  static const long target_env = [] {
+    const char* v = getenv("WMX_PACKED_TARGET");  // (<= 0 or unset: the row rule below)
+    return v ? std::max(0L, atol(v)) : 0L;
   }();
+  const long target = target_env ? target_env : (M <= 24 ? 160L : 480L);
   long S = (target + wgs - 1) / wgs;
   S = std::min<long>(S, std::max(1, (K / 32) / 4));
   S = std::min<long>(S, K / (2L * std::max(M, 1)));
