@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--calls", type=int, default=4)
     ap.add_argument("--out", default=None)
     ap.add_argument("--lockstep", type=int, default=0, help="1: the groups' decode loops start together")
+    ap.add_argument("--phase-offset-us", type=float, default=0.0, help="group g idles g x this before its decode loop")
     args = ap.parse_args()
     torch.zeros(1, device="cuda:0")
     m = engine.Model("large-v3", 0, "bfloat16")
@@ -44,6 +45,8 @@ def main():
         c.set_probe(True, 16)
         if args.lockstep:
             c.set_lockstep(7, G)
+    for g, c in enumerate(ctxs):
+        c.set_phase_offset(g * args.phase_offset_us)
     pool = ThreadPoolExecutor(max_workers=G)
     rows = []
     for call in range(args.calls + 1):  # call 0 = warm-up
