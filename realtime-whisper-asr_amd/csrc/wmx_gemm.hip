@@ -2123,8 +2123,11 @@ template <int MT, int NCT>
 constexpr int packed_red_bytes(int nw) { return nw * MT * 16 * (16 * NCT + 1) * 4; }
 constexpr int kPackedOneWgPerCu = 256;
 
+// (w8: the 8-bit decode keeps the 80 KiB budget: with the two groups in step, 8 waves on 8-bit weights measured
+// 728.8-731.8x against 726.0-726.7x at 16 windows, while the 16-bit decode keeps its 16-wave fc2: 568.3 / 569.4x against
+// 564.4 / 564.5x, profiles/r04_lds_budget/)
 template <int MT, int NCT>
-static int packed_nw(int K, int S, long wgs = 1L << 30) {
+static int packed_nw(int K, int S, long wgs = 1L << 30, bool w8 = false) {
   const int ksteps = K / 32, kps = (ksteps + S - 1) / S;
   // k-steps per wave the wave count aims for (WMX_PACKED_PER overrides 4 for tuning runs: 2 = one load batch)
   static const int per_t = [] {
@@ -2134,7 +2137,7 @@ static int packed_nw(int K, int S, long wgs = 1L << 30) {
   const int per4 = (kps + per_t - 1) / per_t;
   static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
   static const bool lds80 = getenv("WMX_PACKED_LDS80") != nullptr;  // A/B switch: the 80 KiB budget everywhere
-  const int budget = (!lds80 && wgs <= kPackedOneWgPerCu) ? 163840 : 81920;
+  const int budget = (!lds80 && !w8 && wgs <= kPackedOneWgPerCu) ? 163840 : 81920;
   const bool fit8 = packed_red_bytes<MT, NCT>(8) <= budget;
   const bool fit16 = packed_red_bytes<MT, NCT>(16) <= budget;
   if (only4 || per4 <= 4 || !fit8) return 4;
@@ -2146,7 +2149,7 @@ template <DT T, int MT, int NCT, bool W8>
 static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ntiles = (g.N + 15) / 16;
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
-  const int nw = packed_nw<MT, NCT>(g.K, g.S, (long)grid.x * grid.y * grid.z);
+  const int nw = packed_nw<MT, NCT>(g.K, g.S, (long)grid.x * grid.y * grid.z, W8);
   const bool tail = g.tail.cnt != nullptr;
   const int epk = tail ? kPackedTail
                  : g.S > 1 ? kPackedPart
@@ -2180,7 +2183,7 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
 template <int MT, int NCT>
 static PackedPlan plan_cfg(int M, int N, int K, int S, bool w8) {
   const int gx = ((N + 15) / 16 + NCT - 1) / NCT, gz = (M + MT * 16 - 1) / (MT * 16);
-  return PackedPlan{MT, NCT, packed_nw<MT, NCT>(K, S, (long)gx * S * gz), w8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>(),
+  return PackedPlan{MT, NCT, packed_nw<MT, NCT>(K, S, (long)gx * S * gz, w8), w8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>(),
                     gx, gz};
 }
 
