@@ -17,6 +17,14 @@ run() {
     > $O/$tag.json 2> $O/$tag.err || { echo "$tag failed"; tail -5 $O/$tag.err; exit 1; }
   python -c "import json;d=json.load(open('$O/$tag.json'));m=d['decode_mode'];e=d['roofline']['layer_e2e_us'];print('$tag', d['value'], d['ms_per_step'], [g['decode_stage_ms'] for g in m['groups']], round(sum(e.values()),1))"
 }
+if [ "${2:-}" = fold ]; then
+  for i in 1 2; do
+    run base_$i WMX_X=1 --
+    run fold_$i WMX_FOLD=1 --
+    run mlpf_$i WMX_MLP_FUSED=1 --
+  done
+  exit 0
+fi
 for i in 1 2; do
   run base_$i WMX_X=1 --
   run chunk768_$i WMX_CROSS_CHUNK=768 --
