@@ -300,6 +300,9 @@ wmx_status wmx_ctx_set_phase_offset(wmx_ctx* c, double us);
  * later reader hits the caches). Every member must call wmx_transcribe concurrently with the others; a member that does
  * not costs the others the timeout. key 0 leaves the group. */
 wmx_status wmx_ctx_set_lockstep(wmx_ctx* c, int key, int n_members);
+/* the lockstep barrier alone (host tests, no GPU): arrive once at group `key` of n members; *ok = 1 when all
+ * arrived within timeout_us, else 0 (the member leaves; the group's next round starts clean) */
+wmx_status wmx_debug_lockstep_arrive(int key, int n_members, int timeout_us, int* ok);
 wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
 wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* span_ms, double* bytes, int* span_n, float* e2e_ms, int* e2e_n);
 /* the probes' raw device wall-clock ticks of the last transcribe (diagnostics: the relative phase of two context

@@ -3126,6 +3126,26 @@ wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* span_ms, double* bytes, int
   });
 }
 
+// the lockstep barrier alone, for host tests without a GPU (tests/test_lockstep.py): join group `key` of n members
+// (created on first use) and arrive once; *ok = 1 when every member arrived within timeout_us
+wmx_status wmx_debug_lockstep_arrive(int key, int n_members, int timeout_us, int* ok) {
+  return guard([&] {
+    WMX_CHECK(key != 0 && n_members >= 2 && n_members <= 64 && timeout_us >= 0 && ok, "debug_lockstep: args");
+    std::shared_ptr<Lockstep> p;
+    {
+      std::lock_guard<std::mutex> g(g_lockstep_mu);
+      auto& q = g_lockstep[key];
+      if (!q) {
+        q = std::make_shared<Lockstep>();
+        q->n = n_members;
+      }
+      WMX_CHECK(q->n == n_members, "debug_lockstep: this key was created with another member count");
+      p = q;
+    }
+    *ok = p->arrive(std::chrono::microseconds(timeout_us)) ? 1 : 0;
+  });
+}
+
 wmx_status wmx_ctx_set_lockstep(wmx_ctx* x, int key, int n_members) {
   return guard([&] {
     Ctx& c = x->c;
