@@ -247,6 +247,10 @@ def stream_load(name, dtype, n_streams, seconds, max_new_tokens):
     model = asr.model
     model.max_batch = n_streams
     model._ctx.clear()
+    # one context per batched call; WMX_STREAM_GROUPS=2 splits a tick's due windows over two contexts decoding in step
+    # (WhisperModel.groups, wmx_ctx_set_lockstep): 4 windows per call measured 515-519 against 511-513 ms p50, so
+    # the split pays only from larger batches (the 8-window bench line)
+    model.groups = int(os.environ.get("WMX_STREAM_GROUPS", "1"))
     tick, n = 8000, int(seconds * 16000)
     audios = [synth.speech_like(700 + s, n) for s in range(n_streams)]
     n_win = n // 512 + 2
@@ -280,6 +284,7 @@ def stream_load(name, dtype, n_streams, seconds, max_new_tokens):
             "tick_busy": round(float(np.mean([c[3] for c in calls])) / 0.5, 3) if calls else None,
             "feed": "VAC (1 s online chunks, scripted VAD track), 0.5 s per tick, streams staggered by one tick; one "
                     "batched transcribe per tick over the due streams (StreamBatcher)",
+            "context_groups": model.groups,
             "max_new_tokens": max_new_tokens, "beam": 5}
 
 

@@ -278,13 +278,16 @@ class WhisperModel:
         self.sample_seed = seed
         self._sample_calls = 0
         self._ctx = {}
+        # transcribe_batch: split a batch of >= `groups` windows over that many contexts decoding concurrently in step
+        # (wmx_ctx_set_lockstep, as bench.py's two groups; 1 = one context per batch)
+        self.groups = 1
         # what the calls cost on the device (bench.py's latency lines decompose a call with it): decoded windows
         # (engine transcribe rows, fallback retries included), engine calls, decode steps those calls ran
         self.counters = {"windows": 0, "engine_calls": 0, "decode_steps": 0}
 
     def context(self, beam_size, language_token, task, word_timestamps, without_timestamps=False, patience=1.0,
                 length_penalty=1.0, suppress_blank=True, suppress_tokens=None, max_initial_timestamp=1.0,
-                max_new_tokens=None, temperature=0.0, best_of=5):
+                max_new_tokens=None, temperature=0.0, best_of=5, group=None):
         sup = tuple(suppressed_tokens(self.tokenizer.sp, self.suppress_tokens if suppress_tokens is None
                                       else suppress_tokens))
         mit = None if max_initial_timestamp is None else int(round(max_initial_timestamp / TIME_PRECISION))
@@ -293,15 +296,20 @@ class WhisperModel:
         best_of = int(best_of) if temperature > 0 else 5
         key = (beam_size, language_token, task, word_timestamps, without_timestamps, float(patience),
                float(length_penalty), bool(suppress_blank), sup, mit, mnt, temperature, best_of)
+        opts = key
+        if group is not None:  # (g, n): member g of n contexts that decode one batch concurrently, in step
+            key = key + (group,)
         if key not in self._ctx:
-            self._ctx[key] = Context(self.model, max_batch=self.max_batch, beam_size=beam_size, patience=patience,
-                                     length_penalty=length_penalty, max_new_tokens=mnt, task=task,
-                                     language=language_token, without_timestamps=without_timestamps,
-                                     max_initial_timestamp_index=mit, suppress_blank=suppress_blank,
-                                     suppress_tokens=sup, word_timestamps=word_timestamps,
-                                     alignment_heads=self.alignment_heads, use_graph=self.use_graph,
-                                     max_audio_samples=2 * 480000, temperature=temperature, best_of=best_of,
-                                     sample_seed=self.sample_seed)
+            ctx = Context(self.model, max_batch=self.max_batch, beam_size=beam_size, patience=patience,
+                          length_penalty=length_penalty, max_new_tokens=mnt, task=task, language=language_token,
+                          without_timestamps=without_timestamps, max_initial_timestamp_index=mit,
+                          suppress_blank=suppress_blank, suppress_tokens=sup, word_timestamps=word_timestamps,
+                          alignment_heads=self.alignment_heads, use_graph=self.use_graph,
+                          max_audio_samples=2 * 480000, temperature=temperature, best_of=best_of,
+                          sample_seed=self.sample_seed)
+            if group is not None:  # one lockstep key per (model, options, group count)
+                ctx.set_lockstep(1 + (hash((id(self), opts, group[1])) & 0x3FFFFFFF), group[1])
+            self._ctx[key] = ctx
         return self._ctx[key]
 
     # ---- faster-whisper WhisperModel.transcribe ----
@@ -451,6 +459,25 @@ class WhisperModel:
             toks.extend(s["tokens"])
         return out, toks, seek_new, last_speech
 
+    def _transcribe_groups(self, G, chunk, pr, beam, lang_tok, task, word_timestamps, best_of):
+        """One batch split over G contexts, each on its own host thread (ctypes drops the GIL inside libwmx), their
+        decode loops started together and kept in step (wmx_ctx_set_lockstep): each layer's weights are then read once
+        for all groups, and one group's kernel boundaries overlap the others' work -- the bench's two-group form."""
+        from concurrent.futures import ThreadPoolExecutor
+        parts = [p for p in np.array_split(np.arange(len(chunk)), G) if len(p)]
+        ctxs = [self.context(beam, lang_tok, task, word_timestamps, temperature=0.0, best_of=best_of, group=(g, G))
+                for g in range(len(parts))]
+        pool = self.__dict__.get("_group_pool")
+        if pool is None:
+            pool = self._group_pool = ThreadPoolExecutor(max_workers=G)
+        futs = [pool.submit(c.transcribe, [chunk[j] for j in p], prompts=[pr[j] for j in p])
+                for c, p in zip(ctxs, parts)]
+        res = []
+        for c, p, f in zip(ctxs, parts, futs):
+            res.extend(f.result())
+            self._count(c, len(p))
+        return res
+
     def transcribe_batch(self, audios, prompts=None, language=None, task="transcribe", beam_size=None,
                          word_timestamps=True, no_speech_threshold=0.6, log_prob_threshold=-1.0, temperature=0.0,
                          best_of=5):
@@ -493,9 +520,13 @@ class WhisperModel:
                     pr.append(tok.encode(" " + p.strip()))
                 else:
                     pr.append(list(p or []))
+            G = max(1, int(getattr(self, "groups", 1)))
             try:
-                res = ctx.transcribe(chunk, prompts=pr)
-                self._count(ctx, len(idx))
+                if G > 1 and temps[0] == 0 and len(idx) >= G:
+                    res = self._transcribe_groups(G, chunk, pr, beam, lang_tok, task, word_timestamps, best_of)
+                else:
+                    res = ctx.transcribe(chunk, prompts=pr)
+                    self._count(ctx, len(idx))
             except Exception as e:
                 for i in idx:
                     out[i] = e

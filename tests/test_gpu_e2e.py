@@ -63,6 +63,30 @@ def test_stream_batcher_matches_single_stream_calls(asr):
     assert StreamBatcher(model, asr) is not None
 
 
+def test_stream_batcher_two_groups_in_step_match_single_stream_calls(asr):
+    """WhisperModel.groups = 2 (bench.py's stream_load): a batch of 4 streams split over two contexts decoding
+    concurrently in step (wmx_ctx_set_lockstep) gives the same words as 4 separate calls, twice in a row."""
+    model = asr.model
+    audios = [synth.speech_like(40 + i, 16000 * (3 + i)) for i in range(4)]
+    prompts = ["", "t5 t6", "", "t9"]
+    model.max_batch = 1
+    model._ctx.clear()
+    single = [model.transcribe_batch([a], [p])[0] for a, p in zip(audios, prompts)]
+    model.max_batch = 4
+    model._ctx.clear()
+    model.groups = 2
+    try:
+        for rep in range(2):
+            grouped = model.transcribe_batch(audios, prompts)
+            for b, s_ in zip(grouped, single):
+                assert not isinstance(b, Exception), b
+                assert [seg.tokens for seg in b] == [seg.tokens for seg in s_], rep
+        assert sum(1 for k in model._ctx if len(k) == 14) == 2  # the two group contexts (options + (g, n))
+    finally:
+        model.groups = 1
+        model._ctx.clear()
+
+
 @pytest.mark.parametrize("kind,n", [("zeros", 32000), ("noise", 16000), ("speech", 8000), ("speech", 16000 * 31),
                                     ("speech", 116800), ("empty", 0)])
 def test_asr_controls_and_lengths(asr, kind, n):
