@@ -472,6 +472,8 @@ class WhisperModel:
             pool = self._group_pool = ThreadPoolExecutor(max_workers=G)
         futs = [pool.submit(c.transcribe, [chunk[j] for j in p], prompts=[pr[j] for j in p])
                 for c, p in zip(ctxs, parts)]
+        from concurrent.futures import wait
+        wait(futs)  # every group finishes before any error propagates (a context serves one call at a time)
         res = []
         for c, p, f in zip(ctxs, parts, futs):
             res.extend(f.result())
