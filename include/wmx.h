@@ -297,12 +297,14 @@ wmx_status wmx_ctx_set_phase_offset(wmx_ctx* c, double us);
 /* context groups decoding concurrently on one GPU (e.g. the bench's two groups, one host thread each): contexts set to
  * the same key (!= 0) with n_members >= 2 meet at a host barrier right before their decode loops (5 ms timeout), so
  * their step graphs start together and stay in step -- each layer's weights are then read once for all groups (the
- * later reader hits the caches). Every member must call wmx_transcribe concurrently with the others; a member that does
- * not costs the others the timeout. key 0 leaves the group. */
+ * later reader hits the caches) -- and again before every later 8-step chunk, waiting only for the members still
+ * decoding (WMX_LOCKSTEP_CHUNKS=0: the start barrier only). Every member must call wmx_transcribe concurrently with
+ * the others; a member that does not costs the others the timeout once. key 0 leaves the group. */
 wmx_status wmx_ctx_set_lockstep(wmx_ctx* c, int key, int n_members);
-/* the lockstep barrier alone (host tests, no GPU): arrive once at group `key` of n members; *ok = 1 when all
- * arrived within timeout_us, else 0 (the member leaves; the group's next round starts clean) */
-wmx_status wmx_debug_lockstep_arrive(int key, int n_members, int timeout_us, int* ok);
+/* the lockstep barriers alone (host tests, no GPU), group `key` of n members: op 0 = the start barrier (all n),
+ * 1 = a chunk barrier (the members still decoding), 2 = leave (this member's decode loop ended); *ok = 1 when every
+ * expected member arrived within timeout_us, else 0 (the member leaves that round; the next one starts clean) */
+wmx_status wmx_debug_lockstep_arrive(int key, int n_members, int op, int timeout_us, int* ok);
 wmx_status wmx_ctx_probe_stats(wmx_ctx* c, float* avg_ms, int* n, double* bytes);
 wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* span_ms, double* bytes, int* span_n, float* e2e_ms, int* e2e_n);
 /* the probes' raw device wall-clock ticks of the last transcribe (diagnostics: the relative phase of two context

@@ -541,11 +541,17 @@ enum {
 // layer at the same time and read its weights once between them (the second reader hits the caches); started a few
 // layers apart, each streams the weights from HBM on its own and the decode runs ~5 % slower, a state that persists
 // for the whole call because both groups keep the same period (the slow decode mode).
+// The same group also meets before every later chunk of 8 decode steps (each member after its previous chunk
+// completed), so a perturbation inside a call (a host thread descheduled at a chunk boundary) cannot leave the groups
+// apart for the rest of it; that barrier waits only for the members still decoding: a member whose decode loop ends
+// (EOT everywhere, or max_new_tokens) leaves it and releases the others.
 struct Lockstep {
   std::mutex mu;
   std::condition_variable cv;
-  int n = 0, arrived = 0;
+  int n = 0, arrived = 0;  // the start barrier: all n members
   unsigned long long gen = 0;
+  int active = 0, c_arrived = 0;  // the chunk barrier: the members of the current call still decoding
+  unsigned long long c_gen = 0;
   // true when all n members arrived within the timeout (a member that is not decoding costs the others one timeout)
   bool arrive(std::chrono::microseconds timeout) {
     std::unique_lock<std::mutex> lk(mu);
@@ -553,12 +559,39 @@ struct Lockstep {
     if (++arrived >= n) {
       arrived = 0;
       ++gen;
+      active = n;  // every member is in this call's decode loop: a fresh chunk barrier
+      c_arrived = 0;
+      ++c_gen;
       cv.notify_all();
       return true;
     }
     const bool ok = cv.wait_for(lk, timeout, [&] { return gen != g; });
     if (!ok) --arrived;
     return ok;
+  }
+  // before a later chunk: true when every member still decoding arrived within the timeout
+  bool chunk(std::chrono::microseconds timeout) {
+    std::unique_lock<std::mutex> lk(mu);
+    const unsigned long long g = c_gen;
+    if (++c_arrived >= active) {
+      c_arrived = 0;
+      ++c_gen;
+      cv.notify_all();
+      return true;
+    }
+    const bool ok = cv.wait_for(lk, timeout, [&] { return c_gen != g; });
+    if (!ok) --c_arrived;
+    return ok;
+  }
+  // this member's decode loop ended: the others' chunk barriers no longer wait for it
+  void leave() {
+    std::lock_guard<std::mutex> lk(mu);
+    if (active > 0) --active;
+    if (c_arrived > 0 && c_arrived >= active) {
+      c_arrived = 0;
+      ++c_gen;
+      cv.notify_all();
+    }
   }
 };
 static std::mutex g_lockstep_mu;
@@ -2032,15 +2065,23 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     c.lockstep_ok = c.lockstep->arrive(std::chrono::microseconds(5000));
   }
   if (c.start_delay_us > 0 && steps < max_new) launch_spin((unsigned long long)(c.start_delay_us * c.wall_khz / 1000.0), c.st);
+  // the group's chunk barrier (default with lockstep; WMX_LOCKSTEP_CHUNKS=0 keeps only the start barrier), left on
+  // every exit of the loop
+  static const bool lk_every = !(getenv("WMX_LOCKSTEP_CHUNKS") && atoi(getenv("WMX_LOCKSTEP_CHUNKS")) == 0);
+  struct LockstepLeave {
+    Lockstep* p;
+    ~LockstepLeave() {
+      if (p) p->leave();
+    }
+  } lk_leave{c.lockstep && c.lockstep_ok && lk_every && steps < max_new ? c.lockstep.get() : nullptr};
+  bool first_chunk = true;
   while (steps < max_new) {
     const int chunk = std::min(kGraphChunk, max_new - steps);
+    if (lk_leave.p && !first_chunk) lk_leave.p->chunk(std::chrono::microseconds(5000));
+    first_chunk = false;
     if (!c.o.use_graph) {
       for (int i = 0; i < chunk; ++i) run_step(c, B);
     } else if (chunk == kGraphChunk) {
-      // (diagnostic A/B, WMX_LOCKSTEP_CHUNKS=1: the group's barrier before every chunk, not only the first; valid
-      // only while every member runs the same number of chunks, i.e. no early stop)
-      static const bool every_chunk = getenv("WMX_LOCKSTEP_CHUNKS") && atoi(getenv("WMX_LOCKSTEP_CHUNKS")) == 1;
-      if (c.lockstep && every_chunk && steps > 0) c.lockstep->arrive(std::chrono::microseconds(5000));
       WMX_HIP(hipGraphLaunch(c.graph[1], c.st));  // one launch per chunk: no per-step graph launch bubble
     } else {
       for (int i = 0; i < chunk; ++i) WMX_HIP(hipGraphLaunch(c.graph[0], c.st));
@@ -3126,11 +3167,13 @@ wmx_status wmx_ctx_probe_launches(wmx_ctx* x, float* span_ms, double* bytes, int
   });
 }
 
-// the lockstep barrier alone, for host tests without a GPU (tests/test_lockstep.py): join group `key` of n members
-// (created on first use) and arrive once; *ok = 1 when every member arrived within timeout_us
-wmx_status wmx_debug_lockstep_arrive(int key, int n_members, int timeout_us, int* ok) {
+// the lockstep barriers alone, for host tests without a GPU (tests/test_lockstep.py): join group `key` of n members
+// (created on first use); op 0 = the start barrier, 1 = a chunk barrier, 2 = leave; *ok = 1 when every member
+// expected arrived within timeout_us
+wmx_status wmx_debug_lockstep_arrive(int key, int n_members, int op, int timeout_us, int* ok) {
   return guard([&] {
-    WMX_CHECK(key != 0 && n_members >= 2 && n_members <= 64 && timeout_us >= 0 && ok, "debug_lockstep: args");
+    WMX_CHECK(key != 0 && n_members >= 2 && n_members <= 64 && timeout_us >= 0 && ok && op >= 0 && op <= 2,
+              "debug_lockstep: args");
     std::shared_ptr<Lockstep> p;
     {
       std::lock_guard<std::mutex> g(g_lockstep_mu);
@@ -3142,7 +3185,13 @@ wmx_status wmx_debug_lockstep_arrive(int key, int n_members, int timeout_us, int
       WMX_CHECK(q->n == n_members, "debug_lockstep: this key was created with another member count");
       p = q;
     }
-    *ok = p->arrive(std::chrono::microseconds(timeout_us)) ? 1 : 0;
+    if (op == 2) {
+      p->leave();
+      *ok = 1;
+    } else {
+      *ok = (op == 0 ? p->arrive(std::chrono::microseconds(timeout_us)) : p->chunk(std::chrono::microseconds(timeout_us)))
+                ? 1 : 0;
+    }
   });
 }
 

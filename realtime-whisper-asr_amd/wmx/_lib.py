@@ -115,7 +115,7 @@ def _load():
         "wmx_ctx_probe_launches": (C.c_int, [VP, P(F), P(C.c_double), P(C.c_int), P(F), P(C.c_int)]),
         "wmx_ctx_probe_ticks": (C.c_int, [VP, P(C.c_uint64), P(C.c_int), P(C.c_double)]),
         "wmx_ctx_set_lockstep": (C.c_int, [VP, C.c_int, C.c_int]),
-        "wmx_debug_lockstep_arrive": (C.c_int, [C.c_int, C.c_int, C.c_int, P(C.c_int)]),
+        "wmx_debug_lockstep_arrive": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_int)]),
         "wmx_ctx_bench_kernel": (C.c_int, [VP, C.c_int, C.c_int, C.c_int, P(F), P(C.c_double), P(C.c_double)]),
         "wmx_vad_create": (C.c_int, [C.c_int, C.c_int, C.c_int, P(VP)]),
         "wmx_vad_free": (None, [VP]),
