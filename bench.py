@@ -129,12 +129,19 @@ def cpu_baseline(model, args, steps_done, n_text):
     from threadpoolctl import threadpool_limits
 
     d = O.DIMS[args.model] if args.model in O.DIMS else None
-    # BASELINE.md §4 states the host core count from the affinity mask; on the GPU box that mask lists the whole
-    # machine while this process's CPU share is OMP_NUM_THREADS (16), so the all-cores leg runs at the smaller of the
-    # two and both are reported
+    # BASELINE.md §4 states the host core count from the affinity mask.  On the GPU box that mask lists the whole
+    # machine (256) while this job's CPU share is 16 (the pool's per-GPU share, exported as OMP_NUM_THREADS; a cgroup
+    # quota when one is set): 256 BLAS threads on 16 CPUs time oversubscription, not the CPU path, so the all-cores
+    # leg runs at the smallest of the three and all three are reported
     affinity = len(os.sched_getaffinity(0))
     omp = int(os.environ.get("OMP_NUM_THREADS", "0")) or None
-    cores = min(affinity, omp) if omp else affinity
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = max(1, int(int(q) / int(per))) if q != "max" else None
+    except (OSError, ValueError):
+        pass
+    cores = min(x for x in (affinity, omp, quota) if x)
     t0 = time.perf_counter()
     W = {}
     for name, shape, _, _ in O.tensor_specs(d):
@@ -152,7 +159,9 @@ def cpu_baseline(model, args, steps_done, n_text):
     totalc = out[cores][0]
     return {"value": round(30.0 / total4, 4), "unit": "x_realtime", "cores": 4, "kind": "proxy",
             "all_cores": {"value": round(30.0 / totalc, 4), "cores": cores},
-            "host": {"sched_getaffinity": affinity, "OMP_NUM_THREADS": omp},
+            "host": {"sched_getaffinity": affinity, "OMP_NUM_THREADS": omp, "cgroup_cpu_quota": quota,
+                     "cores_note": "all_cores = min(affinity, OMP_NUM_THREADS, cgroup quota): the CPUs this job "
+                                   "may use on the box (16 of the machine's 256 per GPU), not the machine's count"},
             "sample": f"1 x 30 s window of {args.model} through the numpy fp32 oracle (faster-whisper/CT2 absent: "
                       f"proxy): log-mel + encoder + language detect + prefill + 4 beam-{args.beam} decode steps "
                       f"(per-step time extrapolated to the GPU run's {steps_done} steps) + word alignment over "
@@ -231,61 +240,41 @@ def stream_latency(name, dtype, seconds, cadence_s, max_new_tokens, vac):
             "max_new_tokens": max_new_tokens, "beam": 5}
 
 
-def stream_load(name, dtype, n_streams, seconds, max_new_tokens):
-    """Per-stream chunk latency UNDER LOAD (BASELINE's second number at config 4's 8 streams per GPU): n_streams
-    synthetic mic streams on one GPU, each a DynamicVACOnlineASRProcessor (reference asr_components.py:119-179; 1 s
-    online chunks, scripted VAD track), fed in real-time order 0.5 s per tick (the reference loop calls process_iter
-    every 0.5 s, 一键实时识别麦克风.py:1510), half the streams starting one tick later (unsynchronised mics).  Every
-    tick, the process_iter() calls that are due run as ONE batched transcribe (wmx.online.StreamBatcher); a due
-    stream's latency is that call's wall time.  Reported: p50 / p90 per stream, windows and decode steps per batched
-    call, and the GPU busy fraction of the tick budget (mean call time / 0.5 s; > 1 cannot keep up in real time)."""
-    from wmx import synth
+def stream_load(name, dtype, n_per_gpu, seconds, max_new_tokens, world=1, rank=0):
+    """Per-stream chunk latency UNDER LOAD (BASELINE's second number at config 4: 64 streams over 8 GPUs = 8 per GPU),
+    on the streaming path sharded over ranks (wmx.streamload): n_per_gpu x world synthetic mic streams,
+    stream s on rank shard_streams(...), each a DynamicVACOnlineASRProcessor (reference asr_components.py:81-179; 1 s
+    online chunks, scripted VAD track) fed in real-time order 0.5 s per tick (the reference loop calls process_iter
+    every 0.5 s, 一键实时识别麦克风.py:1510-1513), odd streams one tick late (unsynchronised mics).  Every tick, a
+    rank's due process_iter calls run as ONE batched transcribe on its GPU (StreamBatcher); a due stream's latency is
+    that call's wall time.  Rank 0 gathers every rank's (stream, tick, beg, end, text) records and latencies
+    (all_gather_object, once) and reports p50 / p90 over all streams, windows and decode steps per batched call, and
+    the GPU busy fraction of the tick budget (mean call time / 0.5 s; > 1 cannot keep up in real time)."""
+    from wmx import dist as D
+    from wmx import streamload as SL
     from wmx.asr import MI355XWhisperASR
-    from wmx.online import DynamicVACOnlineASRProcessor, ScriptedVAD, StreamBatcher
     asr = MI355XWhisperASR(lan="auto", modelsize=name, device="cuda", compute_type=dtype,
                            transcribe_kwargs={"beam_size": 5}, max_new_tokens=max_new_tokens)
     model = asr.model
-    model.max_batch = n_streams
+    mine = D.shard_streams(n_per_gpu * world, world, rank)
+    model.max_batch = max(1, len(mine))
     model._ctx.clear()
     # one context per batched call; WMX_STREAM_GROUPS=2 splits a tick's due windows over two contexts decoding in step
     # (WhisperModel.groups, wmx_ctx_set_lockstep): 4 windows per call measured 515-519 against 511-513 ms p50, so
     # the split pays only from larger batches (the 8-window bench line)
     model.groups = int(os.environ.get("WMX_STREAM_GROUPS", "1"))
-    tick, n = 8000, int(seconds * 16000)
-    audios = [synth.speech_like(700 + s, n) for s in range(n_streams)]
-    n_win = n // 512 + 2
-    streams = [DynamicVACOnlineASRProcessor(1.0, asr, vad_model=ScriptedVAD([0.0] * 20 + [0.95] * n_win))
-               for _ in range(n_streams)]
-    batcher = StreamBatcher(model, asr)
-    cnt = model.counters
-    lat, calls = [], []
-    for k in range(n // tick + 1):
-        for s, (p, a) in enumerate(zip(streams, audios)):
-            i = (k - s % 2) * tick  # odd streams start one tick later
-            if 0 <= i < n:
-                p.insert_audio_chunk(a[i: i + tick])
-        due = sum(1 for p in streams if not p.is_currently_final and p.wants_iter())
-        c0 = dict(cnt)
-        t0 = time.perf_counter()
-        batcher.step(streams)
-        dt_ = time.perf_counter() - t0
-        if due:
-            calls.append((due, cnt["windows"] - c0["windows"], cnt["decode_steps"] - c0["decode_steps"], dt_))
-    calls = calls[1:] if len(calls) > 2 else calls  # the first batched call captures the decode graphs
-    for due, _, _, dt_ in calls:
-        lat.extend([dt_] * due)
-    return {"model": f"whisper-{name}", "dtype": dtype, "streams": n_streams, "audio_s_per_stream": seconds,
-            "batched_calls": len(calls), "stream_iters": len(lat),
-            "p50_ms": round(1000 * float(np.median(lat)), 2) if lat else None,
-            "p90_ms": round(1000 * float(np.percentile(lat, 90)), 2) if lat else None,
-            "due_streams_per_call": round(float(np.mean([c[0] for c in calls])), 2) if calls else None,
-            "windows_per_call": round(float(np.mean([c[1] for c in calls])), 2) if calls else None,
-            "decode_steps_per_call": round(float(np.mean([c[2] for c in calls])), 1) if calls else None,
-            "tick_busy": round(float(np.mean([c[3] for c in calls])) / 0.5, 3) if calls else None,
-            "feed": "VAC (1 s online chunks, scripted VAD track), 0.5 s per tick, streams staggered by one tick; one "
-                    "batched transcribe per tick over the due streams (StreamBatcher)",
-            "context_groups": model.groups,
-            "max_new_tokens": max_new_tokens, "beam": 5}
+    res = SL.run_shard(model, asr, mine, seconds)
+    parts = SL.gather(res, world)
+    out = SL.summarize(parts)
+    out.update({"model": f"whisper-{name}", "dtype": dtype, "audio_s_per_stream": seconds,
+                "streams_per_gpu": n_per_gpu,
+                "per_rank_p50_ms": [round(1000 * float(np.median([dt for _, _, dt in p["lat"]])), 2) if p["lat"] else None
+                                    for p in parts],
+                "feed": "VAC (1 s online chunks, scripted VAD track), 0.5 s per tick, streams staggered by one tick; "
+                        "one batched transcribe per tick per rank over its due streams (StreamBatcher); streams sharded "
+                        "over ranks (wmx.dist.shard_streams), records and latencies gathered to rank 0",
+                "context_groups": model.groups, "max_new_tokens": max_new_tokens, "beam": 5})
+    return out
 
 
 def vad_bench(streams):
@@ -452,6 +441,9 @@ def main():
         elapsed = D.max_over_ranks(elapsed, device=f"cuda:{local}")
     stages = ctx.stage_ms()
     steps_done = ctx.last_steps()
+    if os.environ.get("WMX_PHASE_PROBE") == "1" and os.environ.get("WMX_PHASE_DUMP"):  # diagnostics only
+        ph = [c.probe_phases() for c in ctxs]
+        np.savez(os.environ["WMX_PHASE_DUMP"], **{f"g{g}": p[0] for g, p in enumerate(ph)}, khz=ph[0][1])
     n_tok = [len(r.tokens) for r in res]
     log(f"[rank {rank}] stage ms (logmel, enc, xkv, lang, prefill, decode, align): "
         f"{[round(s, 2) for s in stages]}  decode steps {steps_done}  tokens/window {n_tok}")
@@ -494,26 +486,26 @@ def main():
     dom = max(fam_ms, key=fam_ms.get)
     ms_e2e = fam_ms[dom]
     by = sum(launch[k][1] for k in fams[dom])
-    # the duration basis of `frac`: the in-situ end-to-end span (dispatch + execution, what
-    # rocprofv3's kernel trace reports: profiles/r03zv kernel_stats agreed within 0.2 %) unless the context groups
-    # contend -- the end-to-end time then includes waiting behind the other group's kernels (16 windows: dec_out 12.7
-    # us end to end against 5.0 us of execution) -- in which case the launches' own execution span (first workgroup
-    # start .. last workgroup end, device clock) is the kernel number
-    # (round 4: the groups decode in step -- wmx_ctx_set_lockstep -- so with two or more groups every launch runs beside
-    # the other group's same launch and its end-to-end time includes waiting for that one's workgroups: the span
-    # basis whenever G > 1, not only past an end-to-end / span threshold, so the basis does not flip between runs)
+    # the duration basis of `frac`: the in-situ END-TO-END time of each launch (its last
+    # workgroup's end minus its predecessor's: dispatch + execution, what rocprofv3's kernel trace reports as the
+    # kernel's duration), so the headline can be recomputed from the committed rocprofv3 kernel_stats summary.  The
+    # execution span (first workgroup start .. last workgroup end, device clock) is kept as a labelled secondary
+    # figure: with two context groups in step each launch runs beside the other group's same launch, and the span of
+    # one group's launch divides the bytes by a window the GPU also spent on the other's (it overstates, r04: 0.215
+    # on the span basis against 0.164 end to end and 0.153 from rocprofv3)
     span_ms = sum(insitu[k][0] for k in fams[dom]) if all(insitu.get(k, (0, 0))[1] for k in fams[dom]) else 0.0
-    contended = use_ev and span_ms > 0 and (G > 1 or ms_e2e > 1.3 * span_ms)
-    ms = span_ms if contended else ms_e2e
+    contended = False
+    ms = ms_e2e
     ach = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-            "frac_basis": (f"execution span in situ ({G} context groups share the GPU in step: end-to-end / span = "
-                           f"{ms_e2e / span_ms:.2f}; frac_end_to_end is the rocprofv3-comparable figure)" if contended else
-                           ("end-to-end in situ (dispatch + execution, rocprofv3's kernel duration)" if use_ev
-                            else "isolated replay"))}
+            "frac_basis": ("end-to-end in situ (dispatch + execution of each launch, rocprofv3's kernel duration; "
+                           f"{G} context group(s), every launch of layer {probe_layer} in every timed decode step)"
+                           if use_ev else "isolated replay")}
     roof["frac_end_to_end"] = round(by / (ms_e2e * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if ms_e2e > 0 else None
     roof["frac_span"] = round(by / (span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if span_ms > 0 else None
+    roof["frac_span_note"] = ("secondary: execution span of one group's launches (first workgroup start .. last end); "
+                              "overstates when the groups' same launches run at once and share the weight reads")
     rep_ms = sum(replay[k][0] for k in fams[dom])
     roof["frac_isolated_replay"] = round(by / (rep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if rep_ms > 0 else None
     # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py: FETCH_SIZE x2 +
@@ -680,9 +672,11 @@ def main():
             except Exception as e:  # reported, never the target
                 log(f"[stream] {cfg[0]} failed: {e!r}")
         log(f"[rank {rank}] stream latency: {out['stream_latency']}")
-        # the same per-stream latency under load: this GPU's streams (config 4: 64 streams / 8 GPUs = 8) batched
+    if not args.no_stream:
+        # the same per-stream latency under load, config 4's streaming path: B streams per GPU (64 streams / 8 GPUs),
+        # sharded over every rank, gathered to rank 0 (every rank takes part: the gather is a collective)
         try:
-            out["stream_load"] = stream_load(args.model, dt, B, 12.0, args.max_new_tokens)
+            out["stream_load"] = stream_load(args.model, dt, B, 12.0, args.max_new_tokens, world, rank)
             log(f"[rank {rank}] stream load: {out['stream_load']}")
         except Exception as e:  # reported, never the target
             log(f"[stream load] failed: {e!r}")

@@ -312,6 +312,13 @@ wmx_status wmx_ctx_probe_launches(wmx_ctx* c, float* span_ms, double* bytes, int
  * launch id k at the s-th probed decode step, 0 when not recorded; *n_steps = steps written (lo_hi may be null to
  * query; capacity 448 steps), *wall_khz = the tick rate. */
 wmx_status wmx_ctx_probe_ticks(wmx_ctx* c, uint64_t* lo_hi, int* n_steps, double* wall_khz);
+/* diagnostics (WMX_PHASE_PROBE=1 in the environment at wmx_ctx_set_probe): the probed layer's decode cross attention
+ * phase stamps of the last transcribe, out[(s * n_wg + wg) * n_words + i] for decode step s (at most cap_steps),
+ * workgroup wg (linear id), word i = 0..7 device wall-clock ticks at the kernel's phase boundaries (wave 0: start,
+ * query projection done, query tile ready, first scores, P.V done, waves combined, ticket taken, end), 8 = XCC_ID,
+ * 9 = HW_ID; zero words for workgroups past the grid.  out may be null to query the sizes. */
+wmx_status wmx_ctx_probe_phases(wmx_ctx* c, uint64_t* out, int cap_steps, int* n_steps, int* n_wg, int* n_words,
+                                double* wall_khz);
 
 #ifdef __cplusplus
 }

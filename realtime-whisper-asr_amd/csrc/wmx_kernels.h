@@ -334,6 +334,9 @@ struct DecAttnArgs {
   int* xcnt = nullptr; // key-chunked launches: one arrival counter per (window, head), zero between launches
   int xcd_remap = 0;   // cross attention: place the workgroups of one head on one or two XCDs (launch_cross_t)
   unsigned long long* tprobe = nullptr;  // [slot][workgroup][start, end] wall-clock ticks (probe_record), or null
+  // diagnostic phase stamps of the decode cross attention (WMX_PHASE_PROBE with the in-situ probe): [slot][workgroup]
+  // [kPhaseStamps] wall-clock ticks at the kernel's phase boundaries (wave 0), the last two words its XCC_ID / HW_ID
+  unsigned long long* pphase = nullptr;
   // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
   // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
   const float* qpart = nullptr;

@@ -682,12 +682,16 @@ struct Ctx {
   int probe_kernel = -1, probe_layer = 0;
   unsigned long long* probe_buf = nullptr;
   unsigned long long* cur_probe = nullptr;
+  // diagnostic phase stamps of the probed layer's cross attention ([T][kProbeWG][kPhaseStamps]; WMX_PHASE_PROBE=1 at
+  // wmx_ctx_set_probe, read by wmx_ctx_probe_phases), or null
+  unsigned long long* phase_buf = nullptr;
 
   double probe_bytes[kProbeLaunches] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
   double start_delay_us = 0;    // wmx_ctx_set_phase_offset: idle time before the decode loop (group phase offset)
   std::shared_ptr<struct Lockstep> lockstep;  // wmx_ctx_set_lockstep: the decode loops of the group start together
   bool lockstep_ok = false;                   // the last call's barrier saw every member
+  long lockstep_timeouts = 0;                 // chunk barriers that timed out (this member then left the barrier)
   bool xq_fused = true;         // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED=0: off)
   bool mlp_fused = false;       // decode step: fc1 -> fc2 in one launch, in-launch hand-off (WMX_MLP_FUSED=1)
   float stage_ms[7] = {0};
@@ -980,7 +984,7 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
 // carrying the reduction and the LayerNorm when the shape allows (RedTail), else the GEMM and reduce_ln
 static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K,
                          const float* bias, const float* g, const float* b, unsigned long long* redprobe = nullptr,
-                         W8 w8 = {}) {
+                         W8 w8 = {}, int ablate = 0) {
   // opt-in (WMX_REDLN_FUSED): measured slower than the separate reduce_ln launch, 798 vs 587 ms per call on the
   // default bench -- the in-launch chain (sc1 partial loads, write-through x, a second arrival, the single
   // normalising workgroup's row loads) costs ~10 us more than the kernel boundary it removes
@@ -1005,9 +1009,10 @@ static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp
     launch_gemm_packed(c.dt, p, c.st);
     return;
   }
-  const int S2 = gemm_p_part(c, A, lda, Wp, M, N, K, w8);
+  // (ablate: timing-only WMX_ABLATE bits of dec_step_fast; 16 = leave out the GEMM, 4 = leave out reduce_ln)
+  const int S2 = (ablate & 16) ? S : gemm_p_part(c, A, lda, Wp, M, N, K, w8);
   c.cur_probe = nullptr;
-  launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st, redprobe, c.slot);
+  if (!(ablate & 4)) launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st, redprobe, c.slot);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1242,8 +1247,20 @@ struct FwdArgs {
 // fused into the consumers -- q/k/v into self attention (which also writes the KV cache), cross q into cross
 // attention, out-proj / fc2 into reduce_ln (residual add + the next LayerNorm).  11 launches per layer.
 // Leaves LN_final(x) of every row in c.dhb.
+// Timing-only ablation of the decode step (WMX_ABLATE, a bit mask read once; never set in a product or parity run):
+// the launches named by the set bits are left out of the step so that an A/B run measures what each kind of launch
+// costs on the critical path with the context groups running beside each other. 1 self attention, 2 cross
+// attention, 4 reduce_ln, 8 fc1 + fc2, 16 qkv / out / cross-out projections; 32 every layer's cross attention reads
+// layer 0's cross K / V images, 64 every layer streams layer 0's weights (the caches then hold them: what the HBM
+// stream of each costs). Results are wrong by construction.
+static int ablate_mask() {
+  static const int m = getenv("WMX_ABLATE") ? atoi(getenv("WMX_ABLATE")) : 0;
+  return m;
+}
+
 static void dec_step_fast(Ctx& c, const FwdArgs& f) {
   Model& m = *c.m;
+  const int ab = ablate_mask();
   const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
   const int R = f.rows;
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
@@ -1251,7 +1268,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
                   c.dx, c.dhb, c.st, m.d.n_vocab);
   const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
   for (int l = 0; l < Lt; ++l) {
-    DecLayer& L = m.dec[l];
+    DecLayer& L = m.dec[(ab & 64) ? 0 : l];
     const bool last = l + 1 == Lt;
     const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
     const bool prev = c.probe_kernel >= 0 && l + 1 == c.probe_layer;  // its last launch precedes the probed qkv
@@ -1259,7 +1276,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     auto pbuf = [&](int id) { return probed ? c.probe_buf + id * probe_stride : nullptr; };
     // self attention: QKV partials -> (reduce, cache write, attention) -> out-proj partials -> +x, LN2
     probe(kProbeQKV);
-    int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt, w8_of(m, L.q8qkv, L.s8qkv));
+    int S = (ab & 16) ? 2 : gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt, w8_of(m, L.q8qkv, L.s8qkv));
     c.cur_probe = nullptr;
     DecAttnArgs a{};
     a.o = c.dao;
@@ -1280,9 +1297,9 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     a.qpart_ld = 3 * dt;
     a.qbias = L.bqkv;
     a.tprobe = pbuf(kProbeSelf);
-    launch_self_attn(c.dt, a, c.st);
+    if (!(ab & 1)) launch_self_attn(c.dt, a, c.st);
     probe(kProbeOut);
-    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut), w8_of(m, L.q8o, L.s8o));
+    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut), w8_of(m, L.q8o, L.s8o), ab);
     // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3; with c.xq_fused the
     // cross attention projects its own queries from LN2(x) (no cross-q launch)
     if (!c.xq_fused) {
@@ -1296,7 +1313,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.Tn = 1;
     x.H = H;
     x.d = dt;
-    set_cross_images(c, x, l);
+    set_cross_images(c, x, (ab & 32) ? 0 : l);
     x.Tk = 1500;
     x.rows_per_win = f.win_rows > 0 ? f.win_rows : c.K;
     x.qpart = c.part;
@@ -1313,11 +1330,14 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     }
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
-    if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
-    launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    if (probed) {
+      x.tprobe = c.probe_buf + kProbeCross * probe_stride;
+      x.pphase = c.phase_buf;
+    }
+    if (!(ab & 2)) launch_cross_attn(c.dt, x, c.xa_ws, c.st);
     probe(kProbeCrossOut);
     gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b, pbuf(kProbeRedCrossOut),
-                 w8_of(m, L.q8co, L.s8co));
+                 w8_of(m, L.q8co, L.s8co), ab);
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
     if (c.mlp_fused && mlp_fused_ok(R, dt)) {  // one launch for fc1 -> fc2 (its span is recorded as the fc1 probe), then reduce_ln
       MlpCall mc;
@@ -1340,13 +1360,14 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
       continue;
     }
     probe(kProbeFc1);
-    gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), nullptr,
-           w8_of(m, L.q8fc1, L.s8fc1));
+    if (!(ab & 8))
+      gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), nullptr,
+             w8_of(m, L.q8fc1, L.s8fc1));
     probe(kProbeFc2);
     gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
                  last ? m.lnb : m.dec[l + 1].ln1b,
                  probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr,
-                 w8_of(m, L.q8fc2, L.s8fc2));
+                 w8_of(m, L.q8fc2, L.s8fc2), (ab & 8) ? (ab | 16) : (ab & ~16));
     c.cur_probe = nullptr;
   }
 }
@@ -2046,8 +2067,10 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   const int need_done = c.beam ? B : R;
   c.probe_slots[0] = steps > 0 ? Pmax : 0;  // slots of the graph-replayed steps of this call
 
-  if (c.probe_kernel >= 0)  // per-workgroup records of this call only (read after the timed region)
+  if (c.probe_kernel >= 0) {  // per-workgroup records of this call only (read after the timed region)
     WMX_HIP(hipMemsetAsync(c.probe_buf, 0, (size_t)kProbeLaunches * T * kProbeWG * 2 * 8, c.st));
+    if (c.phase_buf) WMX_HIP(hipMemsetAsync(c.phase_buf, 0, (size_t)T * kProbeWG * kPhaseStamps * 8, c.st));
+  }
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
      // (fp8 decode: weights and cross K/V images at 1 byte per element; activations stay 16-bit)
     const double d = m.d.n_text_state, w2 = 2.0, r = R, ww = m.w8 ? 1.0 : 2.0;
@@ -2077,7 +2100,13 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   bool first_chunk = true;
   while (steps < max_new) {
     const int chunk = std::min(kGraphChunk, max_new - steps);
-    if (lk_leave.p && !first_chunk) lk_leave.p->chunk(std::chrono::microseconds(5000));
+    if (lk_leave.p && !first_chunk && !lk_leave.p->chunk(std::chrono::microseconds(5000))) {
+      // a partner more than the timeout behind (or gone): leave the chunk barrier for the rest of this call rather
+      // than pay the timeout again at every later chunk
+      lk_leave.p->leave();
+      lk_leave.p = nullptr;
+      ++c.lockstep_timeouts;
+    }
     first_chunk = false;
     if (!c.o.use_graph) {
       for (int i = 0; i < chunk; ++i) run_step(c, B);
@@ -2091,6 +2120,12 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     sync(c);
 
     if (c.pinned_i[0] >= need_done) break;
+  }
+  // this member's decode loop is over: release the partners' chunk barriers now, not when transcribe returns
+  // (the read-back, the alignment forward and the host DTW below would otherwise hold them at the timeout)
+  if (lk_leave.p) {
+    lk_leave.p->leave();
+    lk_leave.p = nullptr;
   }
   c.last_steps = steps;
   rec(c, 6);
@@ -2121,6 +2156,7 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     WMX_HIP(hipMemcpyAsync(fh.data(), c.bs.fin_hist, fh.size() * 4, hipMemcpyDeviceToHost, c.st));
   }
   sync(c);
+  if (nf_err != 0 && ablate_mask()) nf_err = 0;  // (timing-only ablation: the skipped launches leave stale rows)
   if (nf_err < 0)
     throw Error(WMX_ERR_NUMERIC, "non-finite decoder logits in language detection, window " + std::to_string(-nf_err - 1));
   if (nf_err != 0) {  // a NaN / inf anywhere upstream of the logits: an error, not a silently shortened transcript
@@ -2653,6 +2689,7 @@ void wmx_ctx_destroy(wmx_ctx* x) {
   if (c.pinned_i) (void)hipHostFree(c.pinned_i);
   if (c.h_align) (void)hipHostFree(c.h_align);
   if (c.h_tp) (void)hipHostFree(c.h_tp);
+  if (c.phase_buf) (void)hipFree(c.phase_buf);
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
   if (c.st) (void)hipStreamDestroy(c.st);
@@ -3084,6 +3121,30 @@ wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
     Ctx& c = x->c;
     c.probe_kernel = kernel;
     c.probe_layer = layer;
+    if (kernel >= 0 && !c.phase_buf && getenv("WMX_PHASE_PROBE") && atoi(getenv("WMX_PHASE_PROBE")) == 1) {
+      WMX_HIP(hipMalloc(&c.phase_buf, (size_t)c.Tctx * kProbeWG * kPhaseStamps * 8));
+      WMX_HIP(hipMemset(c.phase_buf, 0, (size_t)c.Tctx * kProbeWG * kPhaseStamps * 8));
+    }
+  });
+}
+
+// the cross attention's phase stamps of the last transcribe's probed layer (WMX_PHASE_PROBE=1): out = [n_steps]
+// [kProbeWG][kPhaseStamps] words (zero rows: workgroups past the grid), one slot per graph-replayed decode step
+wmx_status wmx_ctx_probe_phases(wmx_ctx* x, uint64_t* out, int cap_steps, int* n_steps, int* n_wg, int* n_words,
+                                double* wall_khz) {
+  return guard([&] {
+    Ctx& c = x->c;
+    WMX_CHECK(n_steps && n_wg && n_words && wall_khz, "probe_phases: null argument");
+    const int s0 = c.probe_slots[0], s1 = std::min(c.probe_slots[1], c.Tctx);
+    *n_steps = c.phase_buf ? std::max(0, s1 - s0) : 0;
+    *n_wg = kProbeWG;
+    *n_words = kPhaseStamps;
+    *wall_khz = c.wall_khz;
+    if (!out || *n_steps == 0) return;
+    const int n = std::min(*n_steps, cap_steps);
+    WMX_HIP(hipStreamSynchronize(c.st));
+    WMX_HIP(hipMemcpy(out, c.phase_buf + (size_t)s0 * kProbeWG * kPhaseStamps, (size_t)n * kProbeWG * kPhaseStamps * 8,
+                      hipMemcpyDeviceToHost));
   });
 }
 

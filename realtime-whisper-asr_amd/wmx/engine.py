@@ -383,6 +383,17 @@ class Context:
             check(lib.wmx_ctx_probe_ticks(self._h, t.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(n), C.byref(khz)))
         return t[:n.value], float(khz.value)
 
+    def probe_phases(self):
+        """(stamps [steps][workgroups][10] uint64, wall-clock kHz): the probed layer's cross-attention phase stamps
+        of the last transcribe (wmx_ctx_probe_phases; diagnostics, WMX_PHASE_PROBE=1 at set_probe)."""
+        n, nwg, nw, khz = C.c_int(), C.c_int(), C.c_int(), C.c_double()
+        check(lib.wmx_ctx_probe_phases(self._h, None, 0, C.byref(n), C.byref(nwg), C.byref(nw), C.byref(khz)))
+        t = np.zeros((max(n.value, 1), nwg.value, nw.value), np.uint64)
+        if n.value:
+            check(lib.wmx_ctx_probe_phases(self._h, t.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n),
+                                           C.byref(nwg), C.byref(nw), C.byref(khz)))
+        return t[:n.value], float(khz.value)
+
     def bench_kernel(self, kernel: str, batch: int, iters: int = 50):
         """Average launch duration (ms) of one hot-path kernel replayed on the context stream (HIP events),
         with its algorithmic bytes and flops per launch."""

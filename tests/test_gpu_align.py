@@ -11,8 +11,12 @@ _dynamic_time_warping by tests/test_oracle_golden.py) at large-v3 width: d = 128
 heads (decoder layers 7..25, so the model carries 26 decoder layers), beam 5 as in the bench, >= 100 text tokens per
 window.  Tolerances:
   * the matrix: relative L2 <= 3e-2 (the bf16 bound of tests/test_gpu_parity.py);
-  * jump_times: EXACTLY the library DTW (wmx_debug_dtw) of the device matrix, and within one frame (20 ms) of the
-    oracle's for >= 95 % of the tokens (the DTW path on a 16-bit-noisy cost can move where two paths nearly tie);
+  * jump_times: EXACTLY the library DTW (wmx_debug_dtw) of the device matrix; and the device's path is an optimal
+    path of the ORACLE's matrix up to the matrix error (path_check below: its cost on the oracle's matrix exceeds the
+    oracle path's by at most the summed |device - oracle| over the two paths -- which must hold when both DTWs are
+    exact, whatever the near-ties).  The fraction of jump times within one frame (20 ms) of the oracle's is a coarse
+    floor (>= 90 %), not the criterion: where two paths nearly tie the oracle's own path moves with its BLAS
+    reduction order (the same device matrix, rel-L2 2.13e-2, gave 99.2 % on one box and 94.2 % on another);
   * text-token probabilities within 2e-2 absolute.
 """
 import numpy as np
@@ -37,6 +41,22 @@ def _jumps(ti, tj):
     ti, tj = np.asarray(ti), np.asarray(tj)
     jumps = np.pad(np.diff(ti), (1, 0), constant_values=1).astype(bool)
     return tj[jumps] / 50.0
+
+
+def path_check(dev, ref, ti, tj, oti, otj):
+    """The device DTW path (ti, tj) against the oracle's (oti, otj) on the oracle's matrix `ref` (DTW cost = -matrix):
+    excess = cost(device path) - cost(oracle path) >= 0, bound = sum of |dev - ref| over both paths.  Since the device
+    path is optimal for `dev` and the oracle's for `ref`, excess <= bound exactly (up to f32 sums); a wrong DTW or a
+    path that does not belong to the matrix fails.  Returns (excess, bound, relative excess)."""
+    ti, tj, oti, otj = (np.asarray(x, np.int64) for x in (ti, tj, oti, otj))
+    ref64, dif = ref.astype(np.float64), np.abs(dev.astype(np.float64) - ref.astype(np.float64))
+    cost_dev = -ref64[ti, tj].sum()
+    cost_ref = -ref64[oti, otj].sum()
+    excess = cost_dev - cost_ref
+    bound = dif[ti, tj].sum() + dif[oti, otj].sum()
+    assert excess >= -1e-3 * max(1.0, abs(cost_ref)), ("the oracle path is not optimal on its own matrix", excess)
+    assert excess <= bound + 1e-4 * max(1.0, abs(cost_ref)), ("device path not near-optimal", excess, bound)
+    return float(excess), float(bound), float(excess / max(abs(cost_ref), 1e-30))
 
 
 def _lib_dtw(matrix):
@@ -87,6 +107,8 @@ def test_word_alignment_matrix_large_v3_heads_beam5():
         print(f"window {b}: {len(text)} text tokens x {dev.shape[1]} frames, matrix rel_l2 {e:.2e}, "
               f"max abs {float(np.max(np.abs(dev - ref))):.3f}; jump times within 1 frame {within:.3f}, "
               f"max err {float(err.max()):.2f} s; token probs max err {float(np.max(np.abs(r.text_token_probs - probs))):.2e}")
+        ex, bd, rex = path_check(dev, ref, ti, tj, oti, otj)
+        print(f"    device path on the oracle matrix: excess cost {ex:.4f} <= bound {bd:.4f} (relative {rex:.2e})")
         assert e <= REL_BF16, e
-        assert within >= 0.95, (within, r.jump_times, jt)
+        assert within >= 0.90, (within, r.jump_times, jt)
         np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)

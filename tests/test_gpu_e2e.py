@@ -184,3 +184,57 @@ def test_nonfinite_decode_is_an_error_not_a_short_transcript():
     assert len(p.audio_buffer) == 0 and "non-finite" in log.getvalue(), log.getvalue()
     eng.set_tensor(name, g)
     assert isinstance(asr.transcribe(audio), list)
+
+
+@pytest.mark.parametrize("ct", ["bfloat16", "float8"])
+def test_nonfinite_in_a_graph_replayed_decode_step_is_an_error(ct):
+    """The decode loop's own guard: a fixed language (lan="en": no language detection to catch
+    the NaN first) and a NaN in the decoder's positional embedding row of slot 5 only, so the prompt prefill and the
+    first selection (slot 2) are clean and the first non-finite logits come from the third graph-replayed step
+    (wmx_runtime.hip transcribe: the per-chunk hipGraph of the step, logits_select_b's guard word).  The call must
+    fail with WMX_ERR_NUMERIC naming that decode step, its slot and a row; with the row restored the next call on
+    the same (cached) context and graphs succeeds -- for the bf16 model and the float8 model (8-bit decode)."""
+    from wmx.asr import MI355XWhisperASR
+    from wmx._lib import WMX_ERR_NUMERIC, WmxError
+    asr = MI355XWhisperASR(lan="en", modelsize="micro", device="cuda", compute_type=ct,
+                           transcribe_kwargs={"beam_size": 5}, max_new_tokens=16)
+    eng = asr.model.model
+    audio = synth.speech_like(15, 16000 * 4)
+    ok = asr.transcribe(audio)
+    assert isinstance(ok, list)
+    name = "decoder.embed_positions.weight"
+    shape = (eng.dims.n_text_ctx, eng.dims.n_text_state)
+    pos = eng.get_tensor(name, shape)
+    bad = pos.copy()
+    bad[5, 7] = np.nan
+    eng.set_tensor(name, bad)
+    with pytest.raises(WmxError) as ei:
+        asr.transcribe(audio)
+    msg = str(ei.value)
+    print(ct, msg)
+    assert ei.value.status == WMX_ERR_NUMERIC, msg
+    assert "decode step 3 (slot 5)" in msg and "row " in msg and "window 0" in msg, msg
+    eng.set_tensor(name, pos)
+    again = asr.transcribe(audio)
+    assert [s.tokens for s in again] == [s.tokens for s in ok]
+
+
+def test_streamload_rank_local_path_matches_per_stream_runs(asr):
+    """Config 4's rank-local streaming path (wmx.streamload.run_shard: a DynamicVACOnlineASRProcessor per mic stream at
+    the reference cadence, one batched transcribe per tick through StreamBatcher) on the GPU at world 1: three streams
+    batched give the same committed words as each stream run alone, and every stream commits time-ordered words."""
+    from wmx import streamload as SL
+    model = asr.model
+    model.max_batch = 3
+    model._ctx.clear()
+    together = SL.run_shard(model, asr, [0, 1, 2], 5.0)
+    model.max_batch = 1
+    model._ctx.clear()
+    alone = [SL.run_shard(model, asr, [s], 5.0) for s in (0, 1, 2)]
+    by = lambda recs: sorted((s, k, round(b, 4), round(e, 4), t) for s, k, b, e, t in recs)  # noqa: E731
+    assert together["records"], "the streams must commit words"
+    assert by(together["records"]) == by([r for a in alone for r in a["records"]])
+    assert max(c[0] for c in together["calls"]) >= 2  # due streams shared a batched call
+    summ = SL.summarize([together])
+    print("rank-local streams:", summ)
+    assert summ["p50_ms"] > 0 and 0 < summ["stream_iters"] <= len(together["lat"])

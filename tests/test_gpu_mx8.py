@@ -189,18 +189,11 @@ def test_fp8_decode_full_depth_large_v3():
     S._check_forced("fp8 decode large-v3 full depth", "bf16", top1, lg, 1, ref_top1, ref_margin, ref_lg, 4)
 
 
-@pytest.mark.parametrize("ct", ["float8", "bfloat16"])
-def test_fp8_decode_word_alignment_large_v3_heads(ct):
-    """The word-alignment pass of the fp8 model (the alignment forward over sot + text + eot runs its > 256-row
-    projections on the dequantized row-major copies, its cross attention on the fp8 images, its logits on the 8-bit
-    embedding): the device matrix against oracle.find_alignment on the fp8 weights and the device's encoder output,
-    at large-v3 width with the large-v3 alignment heads.  Bounds: tests/test_gpu_align.py's jump-time (>= 95 % within
-    one frame) and token-probability (2e-2) criteria; the matrix rel-L2 <= 5e-2 (the MX-fp8 bound of the full-depth
-    encoder above) instead of bf16's 3e-2: the K images are e4m3-rounded from the device's 16-bit GEMM output, and an
-    element whose 16-bit value differs by one ulp from the oracle's can land on the neighbouring e4m3 code (a 6 % step)
-    -- measured 3.2e-2 against bf16's 2.2e-2 (gpurun_out r04a), with 98 % of the jump times within one frame.
-    The same protocol on the bf16 model (ct = bfloat16: the oracle on the device's encoder output, no fp8 rule) is the
-    yardstick the fp8 numbers are printed against."""
+def _alignment_legs(ct):
+    """The word-alignment pass of one model (compute type ct) on two windows at large-v3 width with the large-v3
+    alignment heads, against oracle.find_alignment on the same weights (fp8: the fp8 decoder rule) and the device's own
+    encoder output.  Returns per window (matrix rel-L2, fraction of jump times within one frame, tokens off by more
+    than one frame, text tokens)."""
     from wmx import engine as E
     import test_gpu_align as A
     d = A.ALN
@@ -216,6 +209,7 @@ def test_fp8_decode_word_alignment_large_v3_heads(ct):
     audios = [synth.speech_like(821, 480000), synth.speech_like(822, 400000)]
     encs = ctx.encode(np.stack([O.logmel_segment(a, d.n_mels) for a in audios]))
     res = ctx.transcribe(audios)
+    out = []
     for b, r in enumerate(res):
         text = [t for t in r.tokens if t < sp.eot]
         assert len(text) >= 100, len(text)
@@ -225,9 +219,35 @@ def test_fp8_decode_word_alignment_large_v3_heads(ct):
         oti, otj, probs, jt, ref = O.find_alignment(W, d, encs[b], sp.lang0, "transcribe", text, r.seek_frames,
                                                      align_heads=heads, return_matrix=True)
         e = rel_l2(dev, ref)
-        within = float(np.mean(np.abs(r.jump_times - jt) <= 0.02 + 1e-6))
-        print(f"{ct} window {b}: {len(text)} text tokens, matrix rel_l2 {e:.2e}, jump times within 1 frame {within:.3f}, "
-              f"token probs max err {float(np.max(np.abs(r.text_token_probs - probs))):.2e}")
-        assert e <= 5e-2, e
-        assert within >= 0.90, within
+        near = np.abs(r.jump_times - jt) <= 0.02 + 1e-6
+        ex, bd, rex = A.path_check(dev, ref, ti, tj, oti, otj)
+        print(f"{ct} window {b}: {len(text)} text tokens, matrix rel_l2 {e:.2e}, jump times within 1 frame "
+              f"{float(np.mean(near)):.3f} ({int((~near).sum())} off), token probs max err "
+              f"{float(np.max(np.abs(r.text_token_probs - probs))):.2e}; device path excess cost {ex:.4f} <= {bd:.4f}")
         np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)
+        out.append((e, float(np.mean(near)), int((~near).sum()), len(text), rex))
+    return out
+
+
+def test_fp8_decode_word_alignment_large_v3_heads():
+    """The word-alignment pass of the fp8 model (the alignment forward over sot + text + eot runs its > 256-row
+    projections on the dequantized row-major copies, its cross attention on the fp8 images, its logits on the 8-bit
+    embedding) held to the bf16 model's numbers on the same two windows and protocol.
+
+    * bf16 leg: tests/test_gpu_align.py's criteria -- matrix rel-L2 <= 3e-2, the device DTW path near-optimal on the
+      oracle's matrix (path_check: excess cost <= the summed matrix error over both paths, exact when both DTWs are),
+      and the coarse >= 90 % of jump times within one frame (the oracle's own path moves at near-ties with its BLAS
+      order: this same bf16 leg gave 99.2 % on one box and 94.2 % on another with identical device matrices).
+    * fp8 leg, relative to the bf16 leg window by window: matrix rel-L2 <= 1.6 x bf16's (the e4m3 K images add one
+      rounding on top of bf16's: an element a 16-bit ulp from the oracle's can land on the neighbouring e4m3 code, a
+      6 % step; measured 1.45-1.52 x), the same path criterion, and its relative path excess <= 2 x bf16's + 1e-3.
+    Both legs: token probabilities within 2e-2 of the oracle's, and jump times equal to the library DTW of the device
+    matrix."""
+    legs = {ct: _alignment_legs(ct) for ct in ("bfloat16", "float8")}
+    for b, ((e16, w16, off16, _, rx16), (e8, w8, off8, _, rx8)) in enumerate(zip(legs["bfloat16"], legs["float8"])):
+        print(f"window {b}: fp8 / bf16 matrix rel-L2 {e8 / e16:.2f}, off by > 1 frame {off8} vs {off16}, relative "
+              f"path excess {rx8:.2e} vs {rx16:.2e}")
+        assert e16 <= 3e-2, e16
+        assert w16 >= 0.90 and w8 >= 0.90, (w16, w8)
+        assert e8 <= 1.6 * e16, (e8, e16)
+        assert rx8 <= 2 * rx16 + 1e-3, (rx8, rx16)
