@@ -855,6 +855,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   // (fused path: unconditional -- a wave without keys reads past the image, zeros by the descriptor's range, and
   // never uses them; a conditional batch would make the compiler's waits for the projection's loads count as if
   // the K loads had not been issued, i.e. wait for them too)
+  if (fuse_q && a.issue_bar) __builtin_amdgcn_s_barrier();  // (wave-uniform argument; no memory wait)
   if (fuse_q)
     load_k(kw0);
   else if (kw0 < kw1)
@@ -1179,6 +1180,8 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
     return v ? atoi(v) : 0;
   }();
   a.xcd_remap = remap && a.wq != nullptr;
+  static const int issue_bar = getenv("WMX_XATTN_ISSUE_BAR") ? atoi(getenv("WMX_XATTN_ISSUE_BAR")) : 0;
+  a.issue_bar = issue_bar;
   const int nq = a.rows_per_win * a.Tn;
   const int nwin = a.R / a.rows_per_win;
   const int chunk = std::min(cross_chunk(a.Tk, nq, F8), a.Tk);

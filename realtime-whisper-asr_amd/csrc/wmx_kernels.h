@@ -337,6 +337,9 @@ struct DecAttnArgs {
   // diagnostic phase stamps of the decode cross attention (WMX_PHASE_PROBE with the in-situ probe): [slot][workgroup]
   // [kPhaseStamps] wall-clock ticks at the kernel's phase boundaries (wave 0), the last two words its XCC_ID / HW_ID
   unsigned long long* pphase = nullptr;
+  // decode cross attention with the fused query projection: every wave's query-projection loads are issued before any
+  // wave's K loads (a workgroup barrier between the two batches), so no projection load queues behind K streams
+  int issue_bar = 0;
   // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
   // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
   const float* qpart = nullptr;

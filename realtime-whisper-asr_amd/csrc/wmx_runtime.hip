@@ -830,8 +830,8 @@ static void alloc_ctx(Ctx& c) {
   WMX_HIP(hipMemsetAsync(c.buf, 0, P.off, c.st));
   P.bind(c.buf);
   WMX_HIP(hipHostMalloc(&c.pinned_i, 64));
-  WMX_HIP(hipHostMalloc(&c.h_align, (size_t)B * T * 1500 * sizeof(float)));
-  WMX_HIP(hipHostMalloc(&c.h_tp, (size_t)B * T * sizeof(float)));
+  // (the pinned alignment images, maxB * 448 * 1500 * 4 bytes, are allocated on the first word-alignment pass: a
+  // context without word timestamps never holds them)
   c.a_head_off.assign(Lt, 0);
   c.a_head_cnt.assign(Lt, 0);
   c.a_head_flat.clear();
@@ -2303,6 +2303,10 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
       sync(c);
     }
     c.last_align_ok = false;
+    if (!c.h_align) {
+      WMX_HIP(hipHostMalloc(&c.h_align, (size_t)c.maxB * c.Tctx * 1500 * sizeof(float)));
+      WMX_HIP(hipHostMalloc(&c.h_tp, (size_t)c.maxB * c.Tctx * sizeof(float)));
+    }
     float* const mat = c.h_align;  // [B][Tn][1500], pinned
     float* const tp = c.h_tp;
     WMX_HIP(hipMemcpyAsync(mat, c.align_out, (size_t)B * Tn * 1500 * 4, hipMemcpyDeviceToHost, c.st));

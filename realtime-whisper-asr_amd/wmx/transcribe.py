@@ -15,6 +15,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+from ._lib import WMX_ERR_NUMERIC, WmxError
 from .engine import ALIGNMENT_HEADS, Context, Model
 from .tokenizer import LANGUAGES, load_tokenizer, suppressed_tokens
 
@@ -468,7 +469,9 @@ class WhisperModel:
         ctxs = [self.context(beam, lang_tok, task, word_timestamps, temperature=0.0, best_of=best_of, group=(g, G))
                 for g in range(len(parts))]
         pool = self.__dict__.get("_group_pool")
-        if pool is None:
+        if pool is None or pool._max_workers < G:  # (groups raised since: one thread per lockstep member)
+            if pool is not None:
+                pool.shutdown(wait=True)
             pool = self._group_pool = ThreadPoolExecutor(max_workers=G)
         futs = [pool.submit(c.transcribe, [chunk[j] for j in p], prompts=[pr[j] for j in p])
                 for c, p in zip(ctxs, parts)]
@@ -479,6 +482,29 @@ class WhisperModel:
             res.extend(f.result())
             self._count(c, len(p))
         return res
+
+    def _transcribe_isolating(self, ctx, idx, chunk, pr, out):
+        """ctx.transcribe of a batch; a WMX_ERR_NUMERIC naming one window (one stream's non-finite decode, e.g. NaN
+        samples from one microphone) fails that stream only: its error goes to out[idx[k]] and the batch is re-run
+        without it (the reference runs each stream on its own).  Returns the results of the windows kept,
+        in order; out[] of the failed ones is set."""
+        import re
+        live = list(range(len(idx)))
+        while live:
+            try:
+                res = ctx.transcribe([chunk[k] for k in live], prompts=[pr[k] for k in live])
+                self._count(ctx, len(live))
+                full = [None] * len(idx)
+                for k, r in zip(live, res):
+                    full[k] = r
+                return [r for r in full if r is not None]
+            except WmxError as e:
+                m = re.search(r"window (\d+)", str(e))
+                if e.status != WMX_ERR_NUMERIC or not m or int(m.group(1)) >= len(live):
+                    raise
+                bad = live.pop(int(m.group(1)))
+                out[idx[bad]] = e
+        return []
 
     def transcribe_batch(self, audios, prompts=None, language=None, task="transcribe", beam_size=None,
                          word_timestamps=True, no_speech_threshold=0.6, log_prob_threshold=-1.0, temperature=0.0,
@@ -525,14 +551,22 @@ class WhisperModel:
             G = max(1, int(getattr(self, "groups", 1)))
             try:
                 if G > 1 and temps[0] == 0 and len(idx) >= G:
-                    res = self._transcribe_groups(G, chunk, pr, beam, lang_tok, task, word_timestamps, best_of)
+                    try:
+                        res = self._transcribe_groups(G, chunk, pr, beam, lang_tok, task, word_timestamps, best_of)
+                    except WmxError as e:
+                        if e.status != WMX_ERR_NUMERIC:
+                            raise
+                        # a non-finite window in one group: the one-context path below isolates it
+                        res = self._transcribe_isolating(ctx, idx, chunk, pr, out)
                 else:
-                    res = ctx.transcribe(chunk, prompts=pr)
-                    self._count(ctx, len(idx))
+                    res = self._transcribe_isolating(ctx, idx, chunk, pr, out)
             except Exception as e:
                 for i in idx:
-                    out[i] = e
+                    if out[i] is None:
+                        out[i] = e
                 continue
+            keep = [k for k, i in enumerate(idx) if out[i] is None]  # (windows that failed alone already hold it)
+            idx, chunk = [idx[k] for k in keep], [chunk[k] for k in keep]
             for i, a, r in zip(idx, chunk, res):
                 lang = language or sp.language_code(r.language)
                 segs, _, _, _ = self._window_segments(r, 0, min(N_FRAMES, len(a) // HOP), word_timestamps, lang,

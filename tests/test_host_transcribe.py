@@ -430,3 +430,29 @@ def test_vad_filter_transcribes_speech_only_and_restores_times():
     segs = list(segs)
     assert info.duration == 4.8 and info.duration_after_vad == 2.4
     assert (segs[0].start, segs[0].end) == (0.0, 1.0) and (segs[1].start, segs[1].end) == (1.0, 4.4)
+
+
+def test_batched_call_isolates_a_non_finite_window():
+    """One stream's non-finite decode fails that stream only: the engine names the window in its
+    WMX_ERR_NUMERIC error, transcribe_batch puts that error on the stream and re-runs the batch without it; the other
+    streams get their segments (as they would from separate calls, the reference's per-stream processing)."""
+    from wmx._lib import WMX_ERR_NUMERIC, WmxError
+
+    class NaNCtx(FakeCtx):
+        def transcribe(self, audios, prompts=None, seek=None):
+            self.log.append({"n": len(audios)})
+            for k, a in enumerate(audios):
+                if np.isnan(a).any():
+                    raise WmxError(f"non-finite decoder logits at decode step 3 (slot 5), row {5 * k + 1} "
+                                   f"(window {k})", WMX_ERR_NUMERIC)
+            return [window(0, i) for i in range(len(audios))]
+
+    m = make_model(window, max_batch=4)
+    m.context = lambda *a, **kw: NaNCtx(m.log, None, window)
+    audios = [np.zeros(16000 * 3, np.float32) for _ in range(4)]
+    audios[2][100] = np.nan
+    out = m.transcribe_batch(audios, [""] * 4, word_timestamps=False)
+    assert isinstance(out[2], WmxError) and out[2].status == WMX_ERR_NUMERIC
+    for i in (0, 1, 3):
+        assert isinstance(out[i], list) and out[i], i
+    assert [e["n"] for e in m.log if "n" in e] == [4, 3]  # the batch, then the batch without the failed stream
