@@ -70,9 +70,10 @@ def parse():
     p.add_argument("--groups", type=int, default=2, help="concurrent decoding contexts the streams are split over")
     p.add_argument("--beam", type=int, default=5)
     p.add_argument("--max-new-tokens", type=int, default=224)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8"],
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8", "int8"],
                    help="fp8: BASELINE config 5 (encoder projections on the MX-fp8 MFMA, decoder and logits "
-                        "projections on 8-bit weights, fp8 cross-K/V images; activations bf16)")
+                        "projections on 8-bit weights, fp8 cross-K/V images; activations bf16); int8: the reference's "
+                        "int8_float16 (CTranslate2's int8 grid for the decoder and logits projections, f16 activations)")
     p.add_argument("--task", default="transcribe", choices=["transcribe", "translate"])
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--no-graph", action="store_true")
@@ -368,7 +369,7 @@ def main():
         dist = D.init("nccl", torch.device("cuda", local))  # RCCL
     from wmx import engine, synth
 
-    dt = {"bf16": "bfloat16", "f16": "float16", "fp8": "float8"}[args.dtype]
+    dt = {"bf16": "bfloat16", "f16": "float16", "fp8": "float8", "int8": "int8_float16"}[args.dtype]
     model = engine.Model(args.model, local, dt)
     t = time.time()
     if world > 1:

@@ -48,7 +48,13 @@ enum {
  *    power-of-two scale per (layer, window, head) image).  WMX_DEC_FP8=0 in the environment keeps the decode bf16.
  * The reference's own 8-bit GPU mode is CTranslate2's int8_float16 (int8 weights with per-row scales): the host
  * layer maps compute_type "int8_float16" / "int8" to this dtype (wmx/engine.py). */
-enum { WMX_DTYPE_BF16 = 0, WMX_DTYPE_F16 = 1, WMX_DTYPE_MX8 = 2 };
+/* WMX_DTYPE_I8 / WMX_DTYPE_I8_BF16 (the reference's CTranslate2 int8 modes, int8_float16 / int8:
+ * 一键实时识别麦克风.py:304, asr_components.py:256-261): every decoder projection and the logits projection on
+ * int8 weights with CTranslate2's per-row scales (q = rint(w * scale), scale = 127 / max|row| or a CT2 int8
+ * checkpoint's own weight_scale, wmx_model_set_row_scales), widened exactly to 16 bits in registers, the row's
+ * 1 / scale applied to the fp32 result; f16 (I8) or bf16 (I8_BF16) activations and storage; the encoder, the
+ * cross-K/V projection and the embedding lookup on the 16-bit weights (q / scale rounded to 16 bits). */
+enum { WMX_DTYPE_BF16 = 0, WMX_DTYPE_F16 = 1, WMX_DTYPE_MX8 = 2, WMX_DTYPE_I8 = 3, WMX_DTYPE_I8_BF16 = 4 };
 enum { WMX_TASK_TRANSCRIBE = 0, WMX_TASK_TRANSLATE = 1 };
 
 typedef struct wmx_model wmx_model;
@@ -133,6 +139,11 @@ wmx_status wmx_model_set_tensor(wmx_model* m, const char* name, const float* dat
 /* read back one tensor (logical HF layout, values as stored) — tests / checkpoint export */
 wmx_status wmx_model_get_tensor(wmx_model* m, const char* name, float* out, int64_t n);
 int64_t wmx_model_n_params(const wmx_model* m);
+/* int8 models only: set the CTranslate2 row scales of a decoder projection or of decoder.embed_tokens.weight (HF
+ * names, e.g. "decoder.layers.3.fc1.weight"; n = its rows), after its weight; wmx_model_get_int8 reads back the
+ * device's int8 bytes [rows][cols] and scales of one such weight (tests). */
+wmx_status wmx_model_set_row_scales(wmx_model* m, const char* name, const float* scale, int64_t n);
+wmx_status wmx_model_get_int8(wmx_model* m, const char* name, int8_t* q, float* scale, int64_t rows, int64_t cols);
 /* the parameter region of the weight arena: [device_ptr, device_ptr + bytes) holds every parameter (what an RCCL
  * broadcast of the weights must carry); the derived copies (row-major, MX-fp8, 8-bit, LayerNorm-folded, log-mel
  * constants) live after it and are rebuilt on each rank by wmx_model_arena_loaded */

@@ -199,6 +199,49 @@ def fp8_decoder_weights(W: dict, d: Dims) -> dict:
     return V
 
 
+# ----------------------------------------------------------------------------------------------
+# The CTranslate2 int8 grid (the reference's compute_type int8_float16 / int8: 一键实时识别麦克风.py:304,
+# asr_components.py:256-261; CTranslate2 4.x int8 quantization, restated -- the engine is not installed here):
+#   * every weight row: scale = 127 / max|row| (1 for an all-zero row), q = rint(w * scale) in [-127, 127] (int8);
+#     a CT2 int8 checkpoint stores q and scale (w = q / scale);
+#   * the device's int8 model keeps every decoder projection (the FP8_DEC_LINEARS) and the logits projection (the tied
+#     token embedding) on that grid -- q from its 16-bit weights by the rule, or with a checkpoint's own scales, which
+#     recovers the checkpoint's q exactly -- and computes with q / scale (the 16-bit q is exact, the fp32 result is
+#     multiplied by 1 / scale); the embedding LOOKUP, the encoder and the cross-attention K / V projection keep the
+#     16-bit weights.  (CT2 also quantizes the activations of its int8 GEMMs per row; the device keeps them 16-bit:
+#     weight-only int8, parity with CT2's own arithmetic unpinned.)
+# ----------------------------------------------------------------------------------------------
+def int8_rows(w: np.ndarray, scale=None):
+    """(q int8 [N][K], scale f32 [N]) of a weight matrix by CTranslate2's int8 rule; `scale` given (a checkpoint's
+    weight_scale) or 127 / max|row| in float32 (the device's arithmetic: f32 division, f32 product, rint half-even)."""
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    if scale is None:
+        amax = np.abs(w).max(axis=1)
+        scale = np.where(amax > 0, np.float32(127.0) / np.where(amax > 0, amax, np.float32(1.0)), np.float32(1.0))
+    scale = np.asarray(scale, np.float32).reshape(-1)
+    q = np.clip(np.rint(w * scale[:, None]), -127, 127).astype(np.int8)
+    return q, scale.astype(np.float32)
+
+
+def int8_decoder_weights(W: dict, d: Dims, scales: dict | None = None) -> dict:
+    """The weights the int8 model's decode computes with: a copy of W whose decoder projections are q / scale of
+    int8_rows (scales: a CT2 int8 checkpoint's per-row scales by weight name, else CT2's rule on W), and the logits
+    projection ("decoder.proj_out.weight") the same of the token embedding; the lookup keeps W's embedding."""
+    scales = scales or {}
+    V = dict(W)
+
+    def deq(name):
+        q, s = int8_rows(W[name], scales.get(name))
+        return (q.astype(np.float32) / s[:, None]).astype(np.float32)
+
+    for i in range(d.n_text_layer):
+        for n in FP8_DEC_LINEARS:
+            k = f"decoder.layers.{i}.{n}.weight"
+            V[k] = deq(k)
+    V["decoder.proj_out.weight"] = deq("decoder.embed_tokens.weight")
+    return V
+
+
 def kv8_images(x: np.ndarray, n_head: int) -> np.ndarray:
     """Cross K or V [T][d] of one window through the fp8 image rule: bf16, then e4m3 with one MX scale per head."""
     T, dm = x.shape

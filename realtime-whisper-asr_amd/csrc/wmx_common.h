@@ -270,6 +270,40 @@ template <DT T> __device__ inline void fp8x16_to16(const u32x4& w, u16x8& lo, u1
   hi = fp8x8_to16<T>(w[2], w[3]);
 }
 
+// int8 weights (the CTranslate2 int8 grid, model dtype I8): 8 signed bytes -> 8 exact 16-bit values (|x| <= 127 is
+// exact in f16 and bf16; the row scale is applied outside, as for e4m3).  f16: the byte x + 128 placed under the
+// exponent byte 0x64 is the f16 1024 + x + 128 (ulp 1 in [1024, 2048)), minus 1152 on the packed adder; bf16: under
+// 0x4B it is the f32 2^23 + x + 128, minus 2^23 + 128, then rounded to bf16 (exact)
+template <DT T> __device__ inline u16x8 i8x8_to16(uint32_t a, uint32_t b);
+template <> __device__ inline u16x8 i8x8_to16<DT::F16>(uint32_t a, uint32_t b) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  const uint32_t xa = a ^ 0x80808080u, xb = b ^ 0x80808080u;
+  const h2 off = {(_Float16)-1152.0f, (_Float16)-1152.0f};
+  const h2 r0 = __builtin_bit_cast(h2, __builtin_amdgcn_perm(0x64646464u, xa, 0x05010400u)) + off;
+  const h2 r1 = __builtin_bit_cast(h2, __builtin_amdgcn_perm(0x64646464u, xa, 0x05030402u)) + off;
+  const h2 r2 = __builtin_bit_cast(h2, __builtin_amdgcn_perm(0x64646464u, xb, 0x05010400u)) + off;
+  const h2 r3 = __builtin_bit_cast(h2, __builtin_amdgcn_perm(0x64646464u, xb, 0x05030402u)) + off;
+  const u32x4 r = {__builtin_bit_cast(uint32_t, r0), __builtin_bit_cast(uint32_t, r1), __builtin_bit_cast(uint32_t, r2),
+                   __builtin_bit_cast(uint32_t, r3)};
+  return __builtin_bit_cast(u16x8, r);
+}
+template <> __device__ inline u16x8 i8x8_to16<DT::BF16>(uint32_t a, uint32_t b) {
+  const uint32_t x[2] = {a ^ 0x80808080u, b ^ 0x80808080u};
+  u16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t sel = 0x040c0c00u | (uint32_t)(e & 3);  // [byte e, 0, 0, 0x4B]
+    const float f = __builtin_bit_cast(float, __builtin_amdgcn_perm(0x4B4B4B4Bu, x[e >> 2], sel)) - 8388736.0f;
+    o[e] = from_f32<DT::BF16>(f);
+  }
+  return o;
+}
+// 16 int8 bytes of one lane -> the two 8-element operands they hold (bytes 0..7, bytes 8..15)
+template <DT T> __device__ inline void i8x16_to16(const u32x4& w, u16x8& lo, u16x8& hi) {
+  lo = i8x8_to16<T>(w[0], w[1]);
+  hi = i8x8_to16<T>(w[2], w[3]);
+}
+
 // four values (already divided by the block scale) -> four e4m3 bytes, little-endian in one dword
 __device__ inline uint32_t mx8_pack4(float a, float b, float c, float d) {
   int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);

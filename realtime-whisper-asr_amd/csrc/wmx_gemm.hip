@@ -1886,7 +1886,7 @@ enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2, kPackedTail = 3 };
 // W8: the weights are e4m3 bytes in the packed8_index layout with per-row scales wsc (a k-step is 64 deep: the
 // same 16-byte lane load as a bf16 k-step, widened in registers into the B fragments of two MFMAs; the row scale
 // multiplies the reduced fp32 tile before any epilogue or partial store)
-template <DT T, int MT, int NCT, int NW, int EPK, bool W8 = false>
+template <DT T, int MT, int NCT, int NW, int EPK, int W8 = 0>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
                                                               int S, Epi e, float* __restrict__ part, RedTail rt,
@@ -1957,7 +1957,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
 #pragma unroll
           for (int j = 0; j < NCT; ++j) {
             u16x8 blo, bhi;
-            fp8x16_to16<T>(b[u][j], blo, bhi);
+            if constexpr (W8 == 2)
+              i8x16_to16<T>(b[u][j], blo, bhi);
+            else
+              fp8x16_to16<T>(b[u][j], blo, bhi);
 #pragma unroll
             for (int i = 0; i < MT; ++i) {
               acc[i][j] = mfma16<T>(av[u][i][0], blo, acc[i][j]);
@@ -2145,11 +2148,11 @@ static int packed_nw(int K, int S, long wgs = 1L << 30, bool w8 = false) {
   return 16;
 }
 
-template <DT T, int MT, int NCT, bool W8>
+template <DT T, int MT, int NCT, int W8>
 static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ntiles = (g.N + 15) / 16;
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
-  const int nw = packed_nw<MT, NCT>(g.K, g.S, (long)grid.x * grid.y * grid.z, W8);
+  const int nw = packed_nw<MT, NCT>(g.K, g.S, (long)grid.x * grid.y * grid.z, W8 != 0);
   const bool tail = g.tail.cnt != nullptr;
   const int epk = tail ? kPackedTail
                  : g.S > 1 ? kPackedPart
@@ -2242,7 +2245,7 @@ PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct, bool w
   return e;
 }
 
-template <DT T, int NCT, bool W8>
+template <DT T, int NCT, int W8>
 static void launch_packed_mt(const PackedCall& g, hipStream_t st) {
   const int mt = (std::min(g.M, 128) + 15) / 16;
   switch (mt) {
@@ -2255,7 +2258,7 @@ static void launch_packed_mt(const PackedCall& g, hipStream_t st) {
     default: launch_packed_cfg<T, 4, 2, W8>(g, st); break;  // 7..8 row tiles: 64-row chunks (LDS budget)
   }
 }
-template <DT T, bool W8>
+template <DT T, int W8>
 static void launch_packed_nct(int nct, const PackedCall& g, hipStream_t st) {
   if (nct == 4) launch_packed_mt<T, 4, W8>(g, st);
   else if (nct == 1) launch_packed_mt<T, 1, W8>(g, st);
@@ -2293,12 +2296,16 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
                     g.epi.kind != EPI_LNFOLD_GELU16),
             "packed gemm: 8-bit weights need K % 64 == 0 and no folded-LayerNorm / in-launch tail epilogue");
   const int nct = g.nct ? g.nct : packed_nct(g.M, g.N, g.K);
+  // (8-bit weights: e4m3 bytes (w8kind 1, the fp8 decode) or int8 bytes (w8kind 2, the CTranslate2 int8 grid))
+  const int kind = w8 ? (g.w8kind == 2 ? 2 : 1) : 0;
   if (dt == DT::BF16) {
-    if (w8) launch_packed_nct<DT::BF16, true>(nct, g, st);
-    else launch_packed_nct<DT::BF16, false>(nct, g, st);
+    if (kind == 2) launch_packed_nct<DT::BF16, 2>(nct, g, st);
+    else if (kind == 1) launch_packed_nct<DT::BF16, 1>(nct, g, st);
+    else launch_packed_nct<DT::BF16, 0>(nct, g, st);
   } else {
-    if (w8) launch_packed_nct<DT::F16, true>(nct, g, st);
-    else launch_packed_nct<DT::F16, false>(nct, g, st);
+    if (kind == 2) launch_packed_nct<DT::F16, 2>(nct, g, st);
+    else if (kind == 1) launch_packed_nct<DT::F16, 1>(nct, g, st);
+    else launch_packed_nct<DT::F16, 0>(nct, g, st);
   }
   WMX_HIP(hipGetLastError());
 }

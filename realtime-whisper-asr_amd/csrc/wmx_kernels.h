@@ -146,6 +146,10 @@ __host__ __device__ inline long packed8_index(long n, long k, long K) {
 }
 // src: a packed 16-bit [N][K] matrix (packed_index) -> q8 (packed8_index, N padded to 16 rows), scale[n] = 2^e_n
 // (N padded entries 0), and optionally rm = the dequantized row-major [N][K] 16-bit copy (many-row passes)
+// the CTranslate2 int8 grid (model dtype I8): per-row CT2 scales (derived: 127 / max|row|, or given), int8 bytes in the
+// packed8_index layout, the GEMM's row multipliers 1 / scale, and the row-major dequantized copy (rm, optional)
+void launch_i8_quantize(DT dt, const uint16_t* src, int N, int K, float* ct2s, bool derive, uint8_t* q8, float* mult,
+                        uint16_t* rm, hipStream_t st);
 void launch_w8_quantize(DT dt, const uint16_t* src, int N, int K, uint8_t* q8, float* scale, uint16_t* rm,
                         hipStream_t st);
 // fp8 cross K / V^T images: per (layer, kv, window, head) image one power-of-two scale (mx8_exp of the image's
@@ -177,6 +181,7 @@ struct PackedCall {
   int S = 1;
   Epi epi;
   const float* wscale = nullptr;  // 8-bit weights: per-row scales (result = scale[n] * acc, before the epilogue)
+  int w8kind = 1;                 // with wscale: 1 e4m3 bytes (fp8 decode), 2 int8 bytes (CTranslate2 int8 grid)
   float* part = nullptr;
   RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
   // in-situ probe: [slot][workgroup][start, end] wall-clock ticks (probe_record) at slot *pslot, or null

@@ -320,6 +320,66 @@ void launch_w8_quantize(DT dt, const uint16_t* src, int N, int K, uint8_t* q8, f
   WMX_HIP(hipGetLastError());
 }
 
+// ---------------- the CTranslate2 int8 grid (model dtype I8) ----------------
+// One wave per weight row n of a packed 16-bit [N][K] matrix: the CT2 row scale s = 127 / max|w| (1 for an all-zero
+// row; CTranslate2's int8 quantization, oracle/whisper_np.py int8_rows) written to ct2s[n] when `derive`, else read
+// from it (a CT2 int8 checkpoint's own weight_scale); q = rint(w s) clamped to [-127, 127] as int8 bytes in the
+// packed8_index layout, the GEMM's row multiplier 1 / s, and the row-major copy q / s rounded to 16 bits.  With the
+// 16-bit weight w = round16(q_ckpt / s_ckpt) and the checkpoint's scale, |q_ckpt| <= 127 makes rint(w s) = q_ckpt
+// exactly (the relative rounding of w is <= 2^-9, so |w s - q_ckpt| <= 127 / 512 < 1/2).
+template <DT T>
+__global__ __launch_bounds__(256) void i8_quantize_kernel(const uint16_t* __restrict__ src, int N, int Np, int K,
+                                                          float* __restrict__ ct2s, int derive, uint8_t* __restrict__ q8,
+                                                          float* __restrict__ mult, uint16_t* __restrict__ rm) {
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= Np) return;  // (wave-uniform)
+  float s = 1.f;
+  if (n < N) {
+    if (derive) {
+      float am = 0.f;
+      for (int k = 8 * lane; k < K; k += 512) {
+        const u16x8 h = *reinterpret_cast<const u16x8*>(src + packed_index(n, k, K));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(to_f32<T>(h[e])));
+      }
+      am = wave_max(am);
+      s = am > 0.f ? 127.f / am : 1.f;
+      if (lane == 0) ct2s[n] = s;
+    } else {
+      s = ct2s[n];
+    }
+  }
+  for (int k = 8 * lane; k < K; k += 512) {
+    uint32_t b[2] = {0u, 0u};
+    u16x8 o;
+    if (n < N) {
+      const u16x8 h = *reinterpret_cast<const u16x8*>(src + packed_index(n, k, K));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float q = fminf(127.f, fmaxf(-127.f, rintf(to_f32<T>(h[e]) * s)));
+        b[e >> 2] |= (uint32_t)((int)q & 0xff) << (8 * (e & 3));
+        o[e] = from_f32<T>(q / s);
+      }
+    }
+    *reinterpret_cast<uint2*>(q8 + packed8_index(n, k, K)) = make_uint2(b[0], b[1]);
+    if (rm && n < N) *reinterpret_cast<u16x8*>(rm + (long)n * K + k) = o;
+  }
+  if (lane == 0) mult[n] = n < N ? 1.f / s : 0.f;
+}
+
+void launch_i8_quantize(DT dt, const uint16_t* src, int N, int K, float* ct2s, bool derive, uint8_t* q8, float* mult,
+                        uint16_t* rm, hipStream_t st) {
+  WMX_CHECK(K % 64 == 0 && N >= 1, "int8 quantize: K must be a multiple of 64");
+  const int Np = (N + 15) / 16 * 16;
+  if (dt == DT::BF16)
+    hipLaunchKernelGGL(i8_quantize_kernel<DT::BF16>, dim3(cdiv(Np, 4)), dim3(256), 0, st, src, N, Np, K, ct2s,
+                       derive ? 1 : 0, q8, mult, rm);
+  else
+    hipLaunchKernelGGL(i8_quantize_kernel<DT::F16>, dim3(cdiv(Np, 4)), dim3(256), 0, st, src, N, Np, K, ct2s,
+                       derive ? 1 : 0, q8, mult, rm);
+  WMX_HIP(hipGetLastError());
+}
+
 // ---------------- fp8 cross K / V^T images (fp8 decode): one 1024-thread workgroup per (layer-kv, window, head) image ---
 // The image (192 KB of 16-bit values) is read ONCE into registers: wave w owns the fp8 piece blocks blk = w + 16 i
 // (94 blocks of 64 pieces), and lane l loads the two 16-bit pieces (2 blk + hh) 64 + l, hh = 0, 1, that fp8 piece

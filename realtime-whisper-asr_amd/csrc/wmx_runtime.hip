@@ -18,6 +18,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -140,6 +141,9 @@ struct DecLayer {
   // after every weight load (launch_w8_quantize); the row-major copies above then hold their dequantized values
   uint8_t *q8qkv = nullptr, *q8o = nullptr, *q8cq = nullptr, *q8co = nullptr, *q8fc1 = nullptr, *q8fc2 = nullptr;
   float *s8qkv = nullptr, *s8o = nullptr, *s8cq = nullptr, *s8co = nullptr, *s8fc1 = nullptr, *s8fc2 = nullptr;
+  // the CTranslate2 int8 grid (Model::i8): the CT2 per-row scales of the six projections (parameters: a CT2 int8
+  // checkpoint's weight_scale, or derived by CT2's rule 127 / max|row|); q8* then hold int8 bytes and s8* 1 / scale
+  float *i8sqkv = nullptr, *i8so = nullptr, *i8scq = nullptr, *i8sco = nullptr, *i8sfc1 = nullptr, *i8sfc2 = nullptr;
 };
 
 struct Model {
@@ -153,6 +157,15 @@ struct Model {
   bool w8 = false;
   uint8_t* tok8 = nullptr;  // the token embedding as the logits projection's 8-bit weights (packed8_index)
   float* tok8s = nullptr;
+  // the CTranslate2 int8 grid (model dtypes WMX_DTYPE_I8 / I8_BF16, the reference's int8_float16 / int8): the 8-bit
+  // decode path with int8 bytes and CT2's per-row scales instead of e4m3 (w8 is set too); the cross K / V images stay
+  // 16-bit (kv8 false) and the cross-q projection runs as its own launch on the int8 weights (no fused 8-bit form);
+  // the encoder and the cross-K/V projection run on the 16-bit weights (a CT2 int8 checkpoint's dequantized q / s)
+  bool i8 = false;
+  bool kv8 = false;  // the fp8 cross K / V images (the MX8 model's fp8 decode)
+  float* i8stok = nullptr;  // CT2 scales of the token embedding (the logits projection)
+  std::set<std::string> i8_given;  // weights whose CT2 scales were set (wmx_model_set_row_scales), not derived
+  std::map<std::string, std::pair<float*, long>> i8_scale_dst;  // weight name -> (its scale rows, row count)
   size_t param_bytes = 0;  // the arena's parameter region [0, param_bytes): what a weight broadcast must carry
   char* arena = nullptr;
   size_t arena_bytes = 0;
@@ -255,6 +268,17 @@ static void build_model(Model& m) {
   P.add(&m.lng, dt);
   P.add(&m.lnb, dt);
   P.add(&m.enc_pos, (size_t)1500 * da);  // (settable: encoder.embed_positions.weight)
+  if (m.i8) {  // CT2 row scales: parameters (a CT2 int8 checkpoint sets them; a broadcast carries them)
+    for (auto& L : m.dec) {
+      P.add(&L.i8sqkv, (size_t)3 * dt);
+      P.add(&L.i8so, dt);
+      P.add(&L.i8scq, dt);
+      P.add(&L.i8sco, dt);
+      P.add(&L.i8sfc1, (size_t)4 * dt);
+      P.add(&L.i8sfc2, dt);
+    }
+    P.add(&m.i8stok, (size_t)(V + 15) / 16 * 16);
+  }
   m.param_bytes = P.off;
   // ---- derived on every rank ----
   if (m.mx8) {
@@ -397,6 +421,21 @@ static void build_model(Model& m) {
     lin(p + ".fc2", dt, 4 * dt, L.wfc2, L.bfc2, true);
   }
   ln("decoder.layer_norm", dt, m.lng, m.lnb);
+  if (m.i8) {  // weight name -> its CT2 row scales (wmx_model_set_row_scales)
+    m.i8_scale_dst["decoder.embed_tokens.weight"] = {m.i8stok, V};
+    for (int i = 0; i < d.n_text_layer; ++i) {
+      DecLayer& L = m.dec[i];
+      const std::string p = "decoder.layers." + std::to_string(i);
+      m.i8_scale_dst[p + ".self_attn.q_proj.weight"] = {L.i8sqkv, dt};
+      m.i8_scale_dst[p + ".self_attn.k_proj.weight"] = {L.i8sqkv + dt, dt};
+      m.i8_scale_dst[p + ".self_attn.v_proj.weight"] = {L.i8sqkv + 2 * dt, dt};
+      m.i8_scale_dst[p + ".self_attn.out_proj.weight"] = {L.i8so, dt};
+      m.i8_scale_dst[p + ".encoder_attn.q_proj.weight"] = {L.i8scq, dt};
+      m.i8_scale_dst[p + ".encoder_attn.out_proj.weight"] = {L.i8sco, dt};
+      m.i8_scale_dst[p + ".fc1.weight"] = {L.i8sfc1, 4 * dt};
+      m.i8_scale_dst[p + ".fc2.weight"] = {L.i8sfc2, dt};
+    }
+  }
 
   // constants: sinusoids, DFT basis (Hann folded, re | im blocks of 208), sparse mel filterbank
   auto pos = sinusoids(1500, da);
@@ -502,6 +541,28 @@ static void prepare_mx8(Model& m) {
 static void prepare_w8(Model& m) {
   if (!m.w8) return;
   const int dt = m.d.n_text_state;
+  if (m.i8) {  // the CTranslate2 int8 grid: int8 bytes with CT2's row scales (given, or derived by CT2's rule)
+    auto given = [&](const std::string& nm) { return m.i8_given.count(nm) > 0; };
+    for (int i = 0; i < (int)m.dec.size(); ++i) {
+      DecLayer& L = m.dec[i];
+      const std::string p = "decoder.layers." + std::to_string(i);
+      // (the fused q | k | v rows: derived only when none of the three was given; a checkpoint gives all three)
+      const bool gqkv = given(p + ".self_attn.q_proj.weight") && given(p + ".self_attn.k_proj.weight") &&
+                        given(p + ".self_attn.v_proj.weight");
+      launch_i8_quantize(m.dt, L.wqkv, 3 * dt, dt, L.i8sqkv, !gqkv, L.q8qkv, L.s8qkv, L.rqkv, m.st);
+      launch_i8_quantize(m.dt, L.wo, dt, dt, L.i8so, !given(p + ".self_attn.out_proj.weight"), L.q8o, L.s8o, L.ro, m.st);
+      launch_i8_quantize(m.dt, L.wcq, dt, dt, L.i8scq, !given(p + ".encoder_attn.q_proj.weight"), L.q8cq, L.s8cq, L.rcq,
+                         m.st);
+      launch_i8_quantize(m.dt, L.wco, dt, dt, L.i8sco, !given(p + ".encoder_attn.out_proj.weight"), L.q8co, L.s8co,
+                         L.rco, m.st);
+      launch_i8_quantize(m.dt, L.wfc1, 4 * dt, dt, L.i8sfc1, !given(p + ".fc1.weight"), L.q8fc1, L.s8fc1, L.rfc1, m.st);
+      launch_i8_quantize(m.dt, L.wfc2, dt, 4 * dt, L.i8sfc2, !given(p + ".fc2.weight"), L.q8fc2, L.s8fc2, L.rfc2, m.st);
+    }
+    launch_i8_quantize(m.dt, m.tok_emb, m.d.n_vocab, dt, m.i8stok, !given("decoder.embed_tokens.weight"), m.tok8,
+                       m.tok8s, nullptr, m.st);
+    WMX_HIP(hipStreamSynchronize(m.st));
+    return;
+  }
   for (auto& L : m.dec) {
     launch_w8_quantize(m.dt, L.wqkv, 3 * dt, dt, L.q8qkv, L.s8qkv, L.rqkv, m.st);
     launch_w8_quantize(m.dt, L.wo, dt, dt, L.q8o, L.s8o, L.ro, m.st);
@@ -756,7 +817,7 @@ static void alloc_ctx(Ctx& c) {
     P.add(&c.ef8s, (size_t)B * 1500 * 4 * da / 32);
   }
   P.add(&c.ckv, (size_t)B * kXS * Lt * 2 * dt);  // K and V^T images, key stride kXS (pad stays zero)
-  if (c.m->w8) {
+  if (c.m->kv8) {
     P.add(&c.ckv8, (size_t)B * kXS * Lt * 2 * dt);
     P.add(&c.ckv8s, (size_t)Lt * 2 * B * d.n_text_head);
   }
@@ -932,10 +993,12 @@ static Epi epi(int kind, const float* bias, void* out, long ldc) {
 struct W8 {
   const uint8_t* q8 = nullptr;
   const float* s8 = nullptr;
+  bool i8 = false;  // int8 bytes (the CTranslate2 grid) instead of e4m3
 };
 static void set_w(PackedCall& g, const uint16_t* Wp, W8 w8) {
   g.W = w8.q8 ? reinterpret_cast<const uint16_t*>(w8.q8) : Wp;
   g.wscale = w8.q8 ? w8.s8 : nullptr;
+  g.w8kind = w8.i8 ? 2 : 1;
 }
 
 static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, const Epi& e,
@@ -1196,7 +1259,7 @@ static void set_cross_images(const Ctx& c, DecAttnArgs& a, int l) {
   const Model& m = *c.m;
   a.x_wstride = (long)kXS * m.d.n_text_state;
   a.x_hstride = (long)kXS * 64;
-  if (m.w8) {
+  if (m.kv8) {
     const size_t img = (size_t)c.maxB * kXS * m.d.n_text_state;  // bytes per (layer, kv) block of images
     const size_t nsc = (size_t)c.maxB * m.d.n_text_head;
     a.ck = reinterpret_cast<const uint16_t*>(c.ckv8 + (2 * l) * img);
@@ -1210,7 +1273,7 @@ static void set_cross_images(const Ctx& c, DecAttnArgs& a, int l) {
 }
 
 // the 8-bit copy of a decoder projection (fp8 decode), or none
-static W8 w8_of(const Model& m, const uint8_t* q, const float* s) { return m.w8 ? W8{q, s} : W8{}; }
+static W8 w8_of(const Model& m, const uint8_t* q, const float* s) { return m.w8 ? W8{q, s, m.i8} : W8{}; }
 
 static void cross_kv(Ctx& c, int B) {
   Model& m = *c.m;
@@ -1223,7 +1286,7 @@ static void cross_kv(Ctx& c, int B) {
   gemm(c, c.enc_out, dt, m.wckv, dt, B * 1500, Lt * 2 * dt, dt, e);
   // fp8 decode: every (layer-kv, window, head) image to e4m3 with its own power-of-two scale (once per call; the
   // decode steps then stream half the bytes)
-  if (m.w8) launch_crosskv_quant(c.ckv, c.ckv8, c.ckv8s, 2 * Lt, c.maxB, B, m.d.n_text_head, c.st);
+  if (m.kv8) launch_crosskv_quant(c.ckv, c.ckv8, c.ckv8s, 2 * Lt, c.maxB, B, m.d.n_text_head, c.st);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1323,8 +1386,8 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.qbias = L.bcq;
     if (c.xq_fused) {
       x.qS = 0;
-      x.wq = m.w8 ? reinterpret_cast<const uint16_t*>(L.q8cq) : L.wcq;
-      x.wq_scale = m.w8 ? L.s8cq : nullptr;
+      x.wq = m.kv8 ? reinterpret_cast<const uint16_t*>(L.q8cq) : L.wcq;
+      x.wq_scale = m.kv8 ? L.s8cq : nullptr;
       x.qin = c.dhb;
       x.qin_ld = dt;
     }
@@ -2073,13 +2136,13 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   }
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
      // (fp8 decode: weights and cross K/V images at 1 byte per element; activations stay 16-bit)
-    const double d = m.d.n_text_state, w2 = 2.0, r = R, ww = m.w8 ? 1.0 : 2.0;
+    const double d = m.d.n_text_state, w2 = 2.0, r = R, ww = m.w8 ? 1.0 : 2.0, iw = m.kv8 ? 1.0 : 2.0;
     auto proj = [&](double n, double k) { return n * k * ww + r * k * w2 + r * n * w2; };
     // (fused cross-q: the cross attention also streams the d x d query weights and reads the LN2 rows)
     const bool xqf = c.xq_fused && !m.fold;  // (the folded step keeps its cross-q launch)
     const double xq = xqf ? d * d * ww + r * d * w2 : 0.0;
     const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), xqf ? 0.0 : proj(d, d), proj(d, d),
-                                      proj(4 * d, d), proj(d, 4 * d), (double)B * 1500 * 2 * d * ww + 2.0 * r * d * w2 + xq};
+                                      proj(4 * d, d), proj(d, 4 * d), (double)B * 1500 * 2 * d * iw + 2.0 * r * d * w2 + xq};
     for (int k = 0; k < kProbeLaunches; ++k) c.probe_bytes[k] = v[k];
   }
   if (c.o.use_graph && steps < max_new) ensure_step_graphs(c, B);
@@ -2417,17 +2480,23 @@ int wmx_device_count(void) {
 wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_model** out) {
   return guard([&] {
     WMX_CHECK(dims && out, "null argument");
-    WMX_CHECK(dtype == WMX_DTYPE_BF16 || dtype == WMX_DTYPE_F16 || dtype == WMX_DTYPE_MX8, "dtype");
+    WMX_CHECK(dtype == WMX_DTYPE_BF16 || dtype == WMX_DTYPE_F16 || dtype == WMX_DTYPE_MX8 || dtype == WMX_DTYPE_I8 ||
+                  dtype == WMX_DTYPE_I8_BF16,
+              "dtype");
     auto* w = new wmx_model();
     try {
       w->m.d = *dims;
       w->m.device = device;
-      w->m.dt = dtype == WMX_DTYPE_F16 ? DT::F16 : DT::BF16;
+      w->m.dt = (dtype == WMX_DTYPE_F16 || dtype == WMX_DTYPE_I8) ? DT::F16 : DT::BF16;
       w->m.mx8 = dtype == WMX_DTYPE_MX8;
       {  // the fp8 decode of the MX8 model (WMX_DEC_FP8=0: encoder-only MX-fp8, the round-3 model, for A/B runs)
         const char* df = getenv("WMX_DEC_FP8");
         w->m.w8 = w->m.mx8 && !(df && df[0] == '0');
+        w->m.kv8 = w->m.w8;
       }
+      // the CTranslate2 int8 grid: the 8-bit decode path on int8 bytes + CT2 row scales, 16-bit cross K / V images
+      w->m.i8 = dtype == WMX_DTYPE_I8 || dtype == WMX_DTYPE_I8_BF16;
+      if (w->m.i8) w->m.w8 = true;
       // opt-in (WMX_FOLD=1): the LayerNorm-folded decode step passes every parity test but measured slower than
       // the split-K + reduce_ln step (356-390 vs 389-393x real time, interleaved on one box); it has
       // no 8-bit form (the fp8 decode ignores the switch)
@@ -2464,6 +2533,7 @@ wmx_status wmx_model_init_synthetic(wmx_model* w, uint64_t seed) {
   return guard([&] {
     Model& m = w->m;
     WMX_HIP(hipSetDevice(m.device));
+    m.i8_given.clear();  // (int8 model: every CT2 scale by CT2's rule from the synthetic weights)
     for (const TensorEntry& e : m.entries) {
       InitSpec s{};
       s.tid = e.tid;
@@ -2511,6 +2581,7 @@ wmx_status wmx_model_set_tensor(wmx_model* w, const char* name, const float* dat
     }
     const TensorEntry& e = find_entry(m, name, n);
     m.dirty = true;
+    m.i8_given.erase(name);  // (int8 model: a new weight takes CT2's rule for its scales unless they are set after it)
     if (e.store_f32) {
       WMX_HIP(hipMemcpy(e.dst, data, n * 4, hipMemcpyHostToDevice));
       return;
@@ -2568,6 +2639,66 @@ wmx_status wmx_model_get_tensor(wmx_model* w, const char* name, float* out, int6
       }
       out[i] = m.dt == DT::BF16 ? host_bf16_to_f32(h[di]) : host_f16_to_f32(h[di]);
     }
+  });
+}
+
+// the CTranslate2 int8 grid (model dtypes I8 / I8_BF16): a decoder projection's (or the token embedding's) CT2 row
+// scales, q = rint(w * scale) -- a CT2 int8 checkpoint's weight_scale, set after its weight (reference int8 models:
+// 一键实时识别麦克风.py:304, asr_components.py:256-261).  Without it the scales follow CT2's rule 127 / max|row|.
+wmx_status wmx_model_set_row_scales(wmx_model* w, const char* name, const float* scale, int64_t n) {
+  return guard([&] {
+    Model& m = w->m;
+    WMX_CHECK(m.i8, "set_row_scales: the model is not an int8 model (WMX_DTYPE_I8 / WMX_DTYPE_I8_BF16)");
+    auto it = m.i8_scale_dst.find(name);
+    WMX_CHECK(it != m.i8_scale_dst.end(), std::string("set_row_scales: no int8 weight named ") + name);
+    WMX_CHECK(n == it->second.second, "set_row_scales: size mismatch");
+    for (int64_t i = 0; i < n; ++i)
+      WMX_CHECK(std::isfinite(scale[i]) && scale[i] > 0.f, "set_row_scales: scales must be finite and positive");
+    WMX_HIP(hipSetDevice(m.device));
+    WMX_HIP(hipMemcpy(it->second.first, scale, n * 4, hipMemcpyHostToDevice));
+    m.i8_given.insert(name);
+    m.dirty = true;
+  });
+}
+
+// the device's int8 weights of one such projection (tests: bytes and scales against the checkpoint / CT2's rule):
+// q [rows][cols] row-major, scale [rows] the CT2 scales (derived ones included)
+wmx_status wmx_model_get_int8(wmx_model* w, const char* name, int8_t* q, float* scale, int64_t rows, int64_t cols) {
+  return guard([&] {
+    Model& m = w->m;
+    WMX_CHECK(m.i8, "get_int8: the model is not an int8 model");
+    WMX_HIP(hipSetDevice(m.device));
+    ensure_prepared(m);
+    auto it = m.i8_scale_dst.find(name);
+    WMX_CHECK(it != m.i8_scale_dst.end(), std::string("get_int8: no int8 weight named ") + name);
+    WMX_CHECK(rows == it->second.second, "get_int8: rows");
+    const int dt = m.d.n_text_state;
+    // the 8-bit matrix holding this weight and its first row
+    const std::string nm = name;
+    const uint8_t* q8 = nullptr;
+    long K = dt, r0 = 0, Nall = rows;
+    if (nm == "decoder.embed_tokens.weight") {
+      q8 = m.tok8;
+    } else {
+      const int l = std::atoi(nm.c_str() + std::strlen("decoder.layers."));
+      const DecLayer& L = m.dec.at(l);
+      auto ends = [&](const char* sfx) { return nm.size() > std::strlen(sfx) && nm.compare(nm.size() - std::strlen(sfx), std::string::npos, sfx) == 0; };
+      if (ends(".self_attn.q_proj.weight")) q8 = L.q8qkv, r0 = 0, Nall = 3 * dt;
+      else if (ends(".self_attn.k_proj.weight")) q8 = L.q8qkv, r0 = dt, Nall = 3 * dt;
+      else if (ends(".self_attn.v_proj.weight")) q8 = L.q8qkv, r0 = 2 * dt, Nall = 3 * dt;
+      else if (ends(".self_attn.out_proj.weight")) q8 = L.q8o;
+      else if (ends(".encoder_attn.q_proj.weight")) q8 = L.q8cq;
+      else if (ends(".encoder_attn.out_proj.weight")) q8 = L.q8co;
+      else if (ends(".fc1.weight")) q8 = L.q8fc1;
+      else if (ends(".fc2.weight")) q8 = L.q8fc2, K = 4 * dt;
+    }
+    WMX_CHECK(q8 != nullptr && cols == K, "get_int8: shape");
+    const long Np = (Nall + 15) / 16 * 16;
+    std::vector<uint8_t> h((size_t)Np * K);
+    WMX_HIP(hipMemcpy(h.data(), q8, h.size(), hipMemcpyDeviceToHost));
+    for (long r = 0; r < rows; ++r)
+      for (long k = 0; k < K; ++k) q[r * K + k] = (int8_t)h[packed8_index(r0 + r, k, K)];
+    WMX_HIP(hipMemcpy(scale, it->second.first, rows * 4, hipMemcpyDeviceToHost));
   });
 }
 
@@ -2663,7 +2794,9 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       WMX_HIP(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
       // fused cross-q is the default (397-398 vs 383-384x real time, gpurun_out/r02za); WMX_XQ_FUSED=0 restores the
       // separate split-K launch (A/B runs)
-      c.xq_fused = !(getenv("WMX_XQ_FUSED") && atoi(getenv("WMX_XQ_FUSED")) == 0);
+      // (the int8 model: the cross-q projection on its int8 weights, its own launch -- the fused 8-bit query
+      // projection reads e4m3 weights beside fp8 images only)
+      c.xq_fused = !(getenv("WMX_XQ_FUSED") && atoi(getenv("WMX_XQ_FUSED")) == 0) && !w->m.i8;
       c.mlp_fused = getenv("WMX_MLP_FUSED") && atoi(getenv("WMX_MLP_FUSED")) == 1 && !w->m.w8;
       gemm_init_attributes();
       alloc_ctx(c);
@@ -3329,12 +3462,12 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       set_cross_images(c, a, 0);
       a.Tk = 1500;
       a.rows_per_win = c.K;
-      const double eb = m.w8 ? 1.0 : 2.0;  // image / weight bytes per element (fp8 decode: 1)
+      const double eb = m.kv8 ? 1.0 : 2.0;  // image / weight bytes per element (fp8 decode: 1)
       by = (double)B * 1500 * 2 * dt * eb + 2.0 * R * dt * 2;
       fl = 4.0 * R * 1500 * dt;
       if (c.xq_fused && !m.fold) {  // the decode step's form: the query projection inside (reads LN2 rows + wcq)
-        a.wq = m.w8 ? reinterpret_cast<const uint16_t*>(m.dec[0].q8cq) : m.dec[0].wcq;
-        a.wq_scale = m.w8 ? m.dec[0].s8cq : nullptr;
+        a.wq = m.kv8 ? reinterpret_cast<const uint16_t*>(m.dec[0].q8cq) : m.dec[0].wcq;
+        a.wq_scale = m.kv8 ? m.dec[0].s8cq : nullptr;
         a.qin = c.dhb;
         a.qin_ld = dt;
         a.qbias = m.dec[0].bcq;

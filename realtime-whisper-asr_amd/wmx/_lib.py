@@ -12,7 +12,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("WMX_LIB", os.path.join(_HERE, "libwmx.so"))
 
-WMX_DTYPE_BF16, WMX_DTYPE_F16, WMX_DTYPE_MX8 = 0, 1, 2
+WMX_DTYPE_BF16, WMX_DTYPE_F16, WMX_DTYPE_MX8, WMX_DTYPE_I8, WMX_DTYPE_I8_BF16 = 0, 1, 2, 3, 4
 WMX_TASK_TRANSCRIBE, WMX_TASK_TRANSLATE = 0, 1
 
 
@@ -52,7 +52,7 @@ class Result(C.Structure):
 EXPORTS = [
     "wmx_last_error", "wmx_version", "wmx_device_count", "wmx_model_create", "wmx_model_free",
     "wmx_model_init_synthetic", "wmx_model_set_tensor", "wmx_model_get_tensor", "wmx_model_n_params",
-    "wmx_model_arena", "wmx_model_arena_loaded", "wmx_opts_default", "wmx_ctx_create", "wmx_ctx_destroy",
+    "wmx_model_arena", "wmx_model_arena_loaded", "wmx_model_set_row_scales", "wmx_model_get_int8", "wmx_opts_default", "wmx_ctx_create", "wmx_ctx_destroy",
     "wmx_ctx_stream", "wmx_logmel", "wmx_logmel_device", "wmx_encode", "wmx_encode_device",
     "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device", "wmx_result_free",
     "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_probe_ticks", "wmx_ctx_probe_phases", "wmx_ctx_set_lockstep", "wmx_debug_lockstep_arrive", "wmx_ctx_set_phase_offset",
@@ -79,6 +79,8 @@ def _load():
         "wmx_model_init_synthetic": (C.c_int, [VP, C.c_uint64]),
         "wmx_model_set_tensor": (C.c_int, [VP, C.c_char_p, P(F), I64]),
         "wmx_model_get_tensor": (C.c_int, [VP, C.c_char_p, P(F), I64]),
+        "wmx_model_set_row_scales": (C.c_int, [VP, C.c_char_p, P(C.c_float), C.c_int64]),
+        "wmx_model_get_int8": (C.c_int, [VP, C.c_char_p, P(C.c_int8), P(C.c_float), C.c_int64, C.c_int64]),
         "wmx_model_n_params": (I64, [VP]),
         "wmx_model_arena": (C.c_int, [VP, P(VP), P(C.c_size_t)]),
         "wmx_model_arena_loaded": (C.c_int, [VP]),

@@ -137,10 +137,27 @@ def ct2_dims(v):
                 n_text_head=int(dt) // 64, n_text_layer=dec_l)
 
 
-def ct2_to_hf(v):
-    """CT2 Whisper variables -> the HF state dict (f32, without the "model." prefix) wmx_model_set_tensor takes."""
+# the weights an int8 model (WMX_DTYPE_I8) keeps on CTranslate2's int8 grid: every decoder projection the decode step
+# streams and the token embedding (the logits projection); the encoder and the cross-attention K / V projection run
+# on the dequantized 16-bit weights
+_I8_KEPT = re.compile(r"decoder\.(embed_tokens|layers\.\d+\.(self_attn\.(q|k|v|out)_proj|encoder_attn\.(q|out)_proj|fc1|fc2))"
+                      r"\.weight$")
+
+
+def ct2_to_hf(v, row_scales: dict | None = None):
+    """CT2 Whisper variables -> the HF state dict (f32, without the "model." prefix) wmx_model_set_tensor takes.
+    row_scales (optional dict, filled): the CT2 int8 weight_scale rows of the weights an int8 model keeps on the int8
+    grid, by HF weight name (wmx_model_set_row_scales), so that model's q = rint(w * scale) is the checkpoint's q."""
     dims = ct2_dims(v)
     out = {}
+
+    def keep_scale(src, dst, r0=None, r1=None):
+        if row_scales is None or not _I8_KEPT.match(dst) or src + "/weight_scale" not in v:
+            return
+        if v[src + "/weight"].dtype != np.int8:
+            return
+        sc = np.asarray(v[src + "/weight_scale"], np.float32).reshape(-1)
+        row_scales[dst] = sc if r0 is None else sc[r0:r1]
 
     def ln(src, dst):
         out[dst + ".weight"] = np.asarray(v[src + "/gamma"], np.float32)
@@ -149,6 +166,7 @@ def ct2_to_hf(v):
     def lin(src, dst, bias=True):
         w = _weight(v, src)
         out[dst + ".weight"] = w
+        keep_scale(src, dst + ".weight")
         if bias:
             out[dst + ".bias"] = _bias(v, src, w.shape[0])
 
@@ -157,6 +175,7 @@ def ct2_to_hf(v):
         b = _bias(v, src, w.shape[0])
         for j, (dst, has_bias) in enumerate(dsts):
             out[dst + ".weight"] = w[j * d:(j + 1) * d]
+            keep_scale(src, dst + ".weight", j * d, (j + 1) * d)
             if has_bias:
                 out[dst + ".bias"] = b[j * d:(j + 1) * d]
 
@@ -181,6 +200,7 @@ def ct2_to_hf(v):
         lin(s + "/ffn/linear_1", h + ".fc2")
     out["decoder.embed_tokens.weight"] = _weight(v, "decoder/embeddings") if "decoder/embeddings/weight_scale" in v \
         else np.asarray(v["decoder/embeddings/weight"], np.float32)
+    keep_scale("decoder/embeddings", "decoder.embed_tokens.weight")
     out["decoder.embed_positions.weight"] = np.asarray(v["decoder/position_encodings/encodings"], np.float32)
     ln("decoder/layer_norm", "decoder.layer_norm")
     for i in range(dims["n_text_layer"]):
@@ -282,7 +302,7 @@ def resolve_aliases(v: dict, aliases: dict) -> dict:
     return out
 
 
-def load_ct2_dir(model_dir: str):
-    """(dims, HF state dict) of a CT2 Whisper model directory (model.bin), aliases resolved."""
+def load_ct2_dir(model_dir: str, row_scales: dict | None = None):
+    """(dims, HF state dict) of a CT2 Whisper model directory (model.bin), aliases resolved; row_scales as ct2_to_hf."""
     _, _, v, aliases = read_model_bin(os.path.join(model_dir, "model.bin"))
-    return ct2_to_hf(resolve_aliases(v, aliases))
+    return ct2_to_hf(resolve_aliases(v, aliases), row_scales)

@@ -71,14 +71,14 @@ class Model:
             # BASELINE config 5: encoder projections on the CDNA4 MX-fp8 MFMA, the decode on 8-bit weights and fp8
             # cross-K/V images (include/wmx.h WMX_DTYPE_MX8), activations bf16
             self.dtype = L.WMX_DTYPE_MX8
-        elif ct in ("int8_float16", "int8_bfloat16", "int8", "int8_float32"):
-            # CTranslate2's 8-bit modes (the reference's int8_float16, 一键实时识别麦克风.py:304): 8-bit weights with
-            # one scale per row.  Served by this build's 8-bit path, whose weight format is e4m3 with a power-of-two
-            # row scale (not int8): the same bytes per weight, a different rounding grid -- said out loud, not
-            # substituted silently
-            warnings.warn(f"compute_type {compute_type!r}: MI355X runs 8-bit weights as e4m3 with per-row scales "
-                          "(WMX_DTYPE_MX8, the float8 model), not CTranslate2's int8 grid", stacklevel=2)
-            self.dtype = L.WMX_DTYPE_MX8
+        elif ct in ("int8_float16", "int8", "int8_float32"):
+            # CTranslate2's int8 modes (the reference's int8_float16, 一键实时识别麦克风.py:304; int8 on the CPU path,
+            # asr_components.py:256-261): CT2's int8 grid -- int8 weights with CT2's per-row scales for every decoder
+            # projection and the logits projection (include/wmx.h WMX_DTYPE_I8), f16 activations ("int8" /
+            # "int8_float32" run them in f16 too: CT2 computes those in f32)
+            self.dtype = L.WMX_DTYPE_I8
+        elif ct == "int8_bfloat16":
+            self.dtype = L.WMX_DTYPE_I8_BF16
         else:
             raise ValueError(f"compute_type {compute_type!r} is not supported on MI355X "
                              "(use float16 / bfloat16 / float8 / int8_float16)")
@@ -105,13 +105,36 @@ class Model:
         check(lib.wmx_model_get_tensor(self._h, name.encode(), fptr(out), out.size))
         return out
 
-    def load_state_dict(self, sd: dict):
-        """HF/openai-named fp32 tensors (a converted checkpoint); strips a leading 'model.'."""
+    @property
+    def int8(self) -> bool:
+        """The CTranslate2 int8 grid (compute_type int8_float16 / int8 / int8_bfloat16)."""
+        return self.dtype in (L.WMX_DTYPE_I8, L.WMX_DTYPE_I8_BF16)
+
+    def set_row_scales(self, name: str, scale: np.ndarray):
+        """int8 model: a decoder projection's (or the token embedding's) CT2 row scales, after its weight."""
+        v = np.ascontiguousarray(scale, dtype=np.float32).reshape(-1)
+        check(lib.wmx_model_set_row_scales(self._h, name.encode(), fptr(v), v.size))
+
+    def get_int8(self, name: str, shape):
+        """int8 model: (q int8 [rows][cols], CT2 scales [rows]) of one decoder projection as the device holds them."""
+        q = np.empty(shape, np.int8)
+        sc = np.empty(shape[0], np.float32)
+        check(lib.wmx_model_get_int8(self._h, name.encode(), q.ctypes.data_as(C.POINTER(C.c_int8)), fptr(sc),
+                                     shape[0], shape[1]))
+        return q, sc
+
+    def load_state_dict(self, sd: dict, row_scales: dict | None = None):
+        """HF/openai-named fp32 tensors (a converted checkpoint); strips a leading 'model.'.  row_scales: a CT2 int8
+        checkpoint's per-row scales by weight name (int8 models keep the checkpoint's exact int8 grid; other models
+        ignore them -- the weights are the dequantized q / scale either way)."""
         for k, v in sd.items():
             k = k[6:] if k.startswith("model.") else k
             if k == "proj_out.weight":
                 continue
             self.set_tensor(k, np.asarray(v, dtype=np.float32))
+        if row_scales and self.int8:
+            for k, v in row_scales.items():
+                self.set_row_scales(k, v)
         check(lib.wmx_model_arena_loaded(self._h))
 
     def n_params(self) -> int:

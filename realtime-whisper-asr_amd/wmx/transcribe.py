@@ -617,7 +617,8 @@ def _load_checkpoint(model, model_dir):
     import os
     if os.path.exists(os.path.join(model_dir, "model.bin")):  # CTranslate2 (faster-whisper) directory
         from .ct2 import load_ct2_dir
-        model.load_state_dict(load_ct2_dir(model_dir)[1])
+        scales = {}  # (an int8 model keeps an int8 checkpoint's own grid: its q and row scales)
+        model.load_state_dict(load_ct2_dir(model_dir, scales)[1], row_scales=scales)
         return
     files = sorted(glob.glob(os.path.join(model_dir, "*.safetensors")))
     if not files:

@@ -120,3 +120,47 @@ def test_aliased_layer_variables_resolve(tmp_path):
     np.testing.assert_array_equal(chained["a"], np.ones(2))
     with pytest.raises(KeyError):
         ct2.resolve_aliases({}, {"a": "missing"})
+
+
+def test_int8_grid_rule_and_exact_recovery():
+    """The CTranslate2 int8 rule (oracle.int8_rows: scale = 127 / max|row|, 1 for a zero row, q = rint(w scale); the
+    formula of the CT2 export restatement wmx.ct2.hf_to_ct2), and a CT2 int8 checkpoint's q is recovered EXACTLY from its
+    dequantized weights rounded to 16 bits with the checkpoint's own scales -- the property the int8 model's device
+    quantization relies on (|q| <= 127 and a 16-bit rounding <= 2^-9 relative keep |w scale - q| < 1/2)."""
+    import torch
+    from oracle import whisper_np as O
+    rng = np.random.default_rng(4)
+    w = (rng.standard_normal((256, 640)) * 0.05).astype(np.float32)
+    w[7] = 0.0  # an all-zero row: scale 1, q 0
+    q, s = O.int8_rows(w)
+    assert q.dtype == np.int8 and np.abs(q).max() == 127 and s[7] == 1.0 and not q[7].any()
+    for dt in (torch.bfloat16, torch.float16):
+        w16 = torch.from_numpy(q.astype(np.float32) / s[:, None]).to(dt).float().numpy()
+        q2, s2 = O.int8_rows(w16, s)
+        np.testing.assert_array_equal(q2, q)
+        np.testing.assert_array_equal(s2, s)
+
+
+def test_ct2_to_hf_keeps_int8_row_scales():
+    """An int8 CT2 export read back: ct2_to_hf returns the dequantized weights and, for the weights an int8 model keeps
+    on the int8 grid (decoder projections, the fused q | k | v split per projection, the token embedding), the
+    checkpoint's row scales by HF name -- never for the encoder or the cross-attention K / V projection."""
+    from oracle import whisper_np as O
+    d = O.DIMS["micro"]
+    W = O.make_weights(d, 3, "bf16")
+    sd = {k: v for k, v in W.items() if k != "encoder.embed_positions.weight"}
+    sd["encoder.embed_positions.weight"] = W["encoder.embed_positions.weight"]
+    v, al = ct2.hf_to_ct2(sd, dict(n_audio_layer=d.n_audio_layer, n_text_layer=d.n_text_layer), "int8")
+    scales = {}
+    dims, out = ct2.ct2_to_hf(ct2.resolve_aliases(v, al), scales)
+    dt = d.n_text_state
+    want = {"decoder.embed_tokens.weight"}
+    for i in range(d.n_text_layer):
+        for n in O.FP8_DEC_LINEARS:
+            want.add(f"decoder.layers.{i}.{n}.weight")
+    assert set(scales) == want
+    s_qkv = v["decoder/layer_0/self_attention/linear_0/weight_scale"]
+    np.testing.assert_array_equal(scales["decoder.layers.0.self_attn.k_proj.weight"], s_qkv[dt:2 * dt])
+    q_fc1 = v["decoder/layer_0/ffn/linear_0/weight"]
+    np.testing.assert_array_equal(O.int8_rows(out["decoder.layers.0.fc1.weight"],
+                                              scales["decoder.layers.0.fc1.weight"])[0], q_fc1)

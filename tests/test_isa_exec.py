@@ -65,6 +65,8 @@ def test_no_unexpected_scratch():
     assert not bad, "kernels with an unexpected private segment:\n" + "\n".join(bad)
     # the default decode kernels are in the library and scratch-free
     for pat in (r"dec_cross_attn_kernelILNS_2DTE0ELi4ELi8ELb1ELb0ELb0E", r"dec_cross_attn_kernelILNS_2DTE0ELi2ELi8ELb1ELb1ELb0E",
-                r"gemm_packed_kernelILNS_2DTE0ELi2ELi4ELi16ELi2ELb0E", r"dec_self_attn_kernel"):
+                r"gemm_packed_kernelILNS_2DTE0ELi2ELi4ELi16ELi2ELi0E", r"dec_self_attn_kernel",
+                # the int8 model's decode (f16 activations, int8 weights: split-K partials and the GELU fc1)
+                r"gemm_packed_kernelILNS_2DTE1ELi2ELi2ELi8ELi0ELi2E", r"gemm_packed_kernelILNS_2DTE1ELi2ELi2ELi16ELi1ELi2E"):
         hits = [n for n in ks if re.search(pat, n)]
         assert hits and all(ks[n][0] == 0 for n in hits), pat
