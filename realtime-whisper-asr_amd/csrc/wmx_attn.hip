@@ -1083,6 +1083,9 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     const long row = (long)(w0 + ww) * nq + i0 + q;
     if (KS == 1) {
       a.o[row * a.d + h * 64 + e] = from_f32<T>(O / L * vsc);
+    } else if (a.rec_o) {  // records for the consumer's merge (KS == 2; plain stores, the kernel boundary publishes)
+      a.rec_o[((long)ks * a.R + row) * a.d + h * 64 + e] = O;
+      if (e == 0) a.rec_ml[((long)ks * a.R + row) * a.H + h] = make_float2(M, L);
     } else {
       // chunk record, stored write-through (sc1) so the last arriver can read it without an L2 release
       gf32* pr = (gf32*)(part + (((long)((w0 + ww) * a.H + h) * KS + ks) * nq + i0 + q) * 66);
@@ -1093,7 +1096,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
       __hip_atomic_store(pr + 2 + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (KS == 1) {
+  if (KS == 1 || a.rec_o) {
     probe_end();
     return;
   }
@@ -1141,9 +1144,10 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
+        // (explicit fmas: the cross out-projection's record-merge A loads repeat this sum bit for bit)
         const float sc2 = rec[k][0] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(rec[k][0] - M);
-        l += rec[k][1] * sc2;
-        o2 += rec[k][2] * sc2;
+        l = __builtin_fmaf(rec[k][1], sc2, l);
+        o2 = __builtin_fmaf(rec[k][2], sc2, o2);
       }
     }
     a.o[((long)(w0 + ww) * nq + q) * a.d + h * 64 + e] = from_f32<T>(o2 / l * vsc);
@@ -1168,6 +1172,13 @@ static int cross_chunk(int Tk, int nq, bool f8) {
   return f8 ? 512 : 1024;
 }
 
+// the key chunks launch_cross_attn will use for a decode step of these arguments (the pair form aside)
+int cross_attn_key_chunks(const DecAttnArgs& a) {
+  const int nq = a.rows_per_win * a.Tn;
+  const int chunk = std::min(cross_chunk(a.Tk, nq, a.ck_scale != nullptr), a.Tk);
+  return (a.Tk + chunk - 1) / chunk;
+}
+
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
   return (size_t)cross_records_floats(H, nwin, nq_max, kMaxSplits);
 }
@@ -1190,6 +1201,7 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
   WMX_CHECK(KS <= kMaxSplits, "cross attn: too many key chunks");
   WMX_CHECK(KS == 1 || chunk % 32 == 0, "cross attn: key chunks must be whole 32-key blocks");
   WMX_CHECK(KS == 1 || (ws != nullptr && a.xcnt != nullptr && nq <= 16), "cross attn: split workspace required");
+  WMX_CHECK(!a.rec_o || (KS == 2 && a.rec_ml && !F8 && a.Tn == 1), "cross attn: consumer-merged records need 2 key chunks");
   dim3 grid(a.H, nwin, KS * QT);
   // decode: 8 waves per workgroup (a 1024-key chunk is one 128-key batch per wave); WMX_XATTN_WAVES=4 for tuning
   static const int waves = [] {
@@ -1211,6 +1223,7 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
     // window) form's 1024-key chunks over 8 waves; 20 heads x 2 pairs x 3 = 120 workgroups per 4-window group
     const int pchunk = std::min(env_chunk > 0 ? env_chunk : 512, a.Tk);
     const int pKS = (a.Tk + pchunk - 1) / pchunk;
+    WMX_CHECK(!a.rec_o, "cross attn (pairs): no consumer-merged records");
     WMX_CHECK(pKS <= kMaxSplits && (pKS == 1 || pchunk % 32 == 0), "cross attn (pairs): key chunks");
     dim3 pgrid(a.H, nwin / 2, pKS);
     const int per_wave = ((pchunk + 3) / 4 + 31) / 32;

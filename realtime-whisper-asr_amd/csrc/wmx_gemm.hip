@@ -1886,13 +1886,17 @@ enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2, kPackedTail = 3 };
 // W8: the weights are e4m3 bytes in the packed8_index layout with per-row scales wsc (a k-step is 64 deep: the
 // same 16-byte lane load as a bf16 k-step, widened in registers into the B fragments of two MFMAs; the row scale
 // multiplies the reduced fp32 tile before any epilogue or partial store)
-template <DT T, int MT, int NCT, int NW, int EPK, int W8 = 0>
+// AREC: A is the merge of a decode cross attention's two key-chunk records (PackedCall::arec): the lane loads both
+// chunks' 8 fp32 outputs and (max, sum) of its row and head in the batch, and merges them after the batch's loads
+// exactly as the cross attention's in-launch merge does (same operations, same order: bit-identical A)
+template <DT T, int MT, int NCT, int NW, int EPK, int W8 = 0, bool AREC = false>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
                                                               int S, Epi e, float* __restrict__ part, RedTail rt,
                                                               unsigned long long* __restrict__ tprobe,
                                                               const int* __restrict__ pslot,
-                                                              const float* __restrict__ wsc) {
+                                                              const float* __restrict__ wsc,
+                                                              const float2* __restrict__ arec) {
   constexpr int KU = W8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>();
   constexpr int LDR = 16 * NCT + 1;
   constexpr bool TAIL = EPK == kPackedTail;
@@ -1971,6 +1975,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   }
   for (int kk = ks0; !W8 && kk < ks1; kk += KU) {
     u16x8 b[KU][NCT], av[KU][MT];
+    [[maybe_unused]] f32x4 ro[AREC ? KU : 1][AREC ? MT : 1][4];
+    [[maybe_unused]] float2 rml[AREC ? KU : 1][AREC ? MT : 1][2];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
 #ifdef WMX_PACKED_GUARDED
@@ -1994,8 +2000,43 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
 #endif
 #pragma unroll
       for (int j = 0; j < NCT; ++j) b[u][j] = stream_load(reinterpret_cast<const u16x8*>(wt[j] + ((long)k << 9)));
+      if constexpr (AREC) {
+        const float* ro0 = reinterpret_cast<const float*>(A);
+        const int kc = k * 32 + 8 * fq, hd = kc >> 6;
 #pragma unroll
-      for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + k * 32);
+        for (int i = 0; i < MT; ++i) {
+          const long row = min(m0 + i * 16 + fr, M - 1);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const float* o = ro0 + ((long)c * M + row) * lda + kc;
+            ro[u][i][2 * c] = *reinterpret_cast<const f32x4*>(o);
+            ro[u][i][2 * c + 1] = *reinterpret_cast<const f32x4*>(o + 4);
+            rml[u][i][c] = arec[((long)c * M + row) * (lda >> 6) + hd];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + k * 32);
+      }
+    }
+    if constexpr (AREC) {  // the cross attention's merge (wmx_attn.hip, KS = 2): max, weights, sums, o / l
+#pragma unroll
+      for (int u = 0; u < KU; ++u)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          float Mx = -INFINITY;
+          Mx = fmaxf(Mx, rml[u][i][0].x);
+          Mx = fmaxf(Mx, rml[u][i][1].x);
+          const float s0 = rml[u][i][0].x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(rml[u][i][0].x - Mx);
+          const float s1 = rml[u][i][1].x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(rml[u][i][1].x - Mx);
+          const float l = __builtin_fmaf(rml[u][i][1].y, s1, __builtin_fmaf(rml[u][i][0].y, s0, 0.f));
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float o2 = __builtin_fmaf(ro[u][i][2 + (q >> 2)][q & 3], s1,
+                                            __builtin_fmaf(ro[u][i][q >> 2][q & 3], s0, 0.f));
+            av[u][i][q] = from_f32<T>(o2 / l);
+          }
+        }
     }
     // the whole batch is in flight before the first MFMA: without this fence the scheduler may interleave a
     // load behind an MFMA and wait for it with vmcnt(0), two round trips per batch instead of one (measured +1 us
@@ -2160,12 +2201,22 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
                                                                                                  : kPackedGeneric;
 #define WMX_PACKED_EPK(NWV, EPKV)                                                                                  \
   hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, EPKV, W8>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W,  \
-                     g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot, g.wscale)
+                     g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot, g.wscale, nullptr)
 #define WMX_PACKED_LAUNCH(NWV)                                                                                     \
   do {                                                                                                             \
     switch (epk) {                                                                                                 \
       case kPackedTail: WMX_PACKED_EPK(NWV, kPackedTail); break;                                                   \
-      case kPackedPart: WMX_PACKED_EPK(NWV, kPackedPart); break;                                                   \
+      case kPackedPart:                                                                                            \
+        if constexpr (W8 == 0 && NWV <= 8) { /* (16 waves: the merge's registers spill; host-checked) */          \
+          if (g.arec) {                                                                                            \
+            hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, kPackedPart, 0, true>), grid, dim3(64 * NWV), 0,  \
+                               st, g.A, g.lda, g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot,     \
+                               g.wscale, g.arec);                                                                   \
+            break;                                                                                                 \
+          }                                                                                                        \
+        }                                                                                                          \
+        WMX_PACKED_EPK(NWV, kPackedPart);                                                                          \
+        break;                                                                                                     \
       case kPackedGelu: WMX_PACKED_EPK(NWV, kPackedGelu); break;                                                   \
       default: WMX_PACKED_EPK(NWV, kPackedGeneric); break;                                                         \
     }                                                                                                              \
@@ -2292,6 +2343,9 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
                                                   : (g.epi.out16 != nullptr && g.N <= 2048))),
             "packed gemm: folded-LayerNorm epilogue arguments");
   const bool w8 = g.wscale != nullptr;
+  WMX_CHECK(!g.arec || (!w8 && g.S > 1 && g.tail.cnt == nullptr && g.K % 64 == 0 && g.lda == g.K &&
+                        packed_plan(g.M, g.N, g.K, g.S, g.nct, false).NW <= 8),
+            "packed gemm: record-merge A needs 16-bit weights, split-K partials, lda == K and <= 8 waves");
   WMX_CHECK(!w8 || (g.K % 64 == 0 && g.tail.cnt == nullptr && g.epi.kind != EPI_RESID_STATS &&
                     g.epi.kind != EPI_LNFOLD_GELU16),
             "packed gemm: 8-bit weights need K % 64 == 0 and no folded-LayerNorm / in-launch tail epilogue");

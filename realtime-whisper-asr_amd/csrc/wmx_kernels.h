@@ -182,6 +182,10 @@ struct PackedCall {
   Epi epi;
   const float* wscale = nullptr;  // 8-bit weights: per-row scales (result = scale[n] * acc, before the epilogue)
   int w8kind = 1;                 // with wscale: 1 e4m3 bytes (fp8 decode), 2 int8 bytes (CTranslate2 int8 grid)
+  // A = the merge of a decode cross attention's two key-chunk records (DecAttnArgs::rec_o / rec_ml): A points at
+  // rec_o (fp32 [2][M][K], lda = K) and arec at rec_ml ([2][M][K / 64]); the lane's 8 k-values of a row are merged
+  // exactly as the cross attention's own merge does and rounded to 16 bits (16-bit weights, split-K partials only)
+  const float2* arec = nullptr;
   float* part = nullptr;
   RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
   // in-situ probe: [slot][workgroup][start, end] wall-clock ticks (probe_record) at slot *pslot, or null
@@ -345,6 +349,11 @@ struct DecAttnArgs {
   // decode cross attention with the fused query projection: every wave's query-projection loads are issued before any
   // wave's K loads (a workgroup barrier between the two batches), so no projection load queues behind K streams
   int issue_bar = 0;
+  // decode cross attention, 2 key chunks (KS == 2): the chunks' records go to the consumer instead of an in-launch
+  // merge -- rec_o [2][R][d] fp32 (each chunk's unnormalised output), rec_ml [2][R][H] (max, sum) -- and the cross
+  // out-projection merges them in its A loads (PackedCall::arec); no arrival ticket, no last-arriver merge
+  float* rec_o = nullptr;
+  float2* rec_ml = nullptr;
   // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
   // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
   const float* qpart = nullptr;
@@ -374,6 +383,7 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);
 // ws: cross_attn_ws_floats(H, nwin, nq_max) floats for the key-chunk records (decode steps), a.xcnt: nwin*H
 // zero-initialised ints (the merging workgroup re-arms its counter)
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max);
+int cross_attn_key_chunks(const DecAttnArgs& a);
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st);
 // raw cross-attention scores of selected heads (alignment): out [nh][R*Tn][Tk] f32
 void launch_cross_scores(DT dt, const DecAttnArgs& a, const int* heads_layer_local, int nh, float* out, hipStream_t st);

@@ -755,6 +755,7 @@ struct Ctx {
   long lockstep_timeouts = 0;                 // chunk barriers that timed out (this member then left the barrier)
   bool xq_fused = true;         // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED=0: off)
   bool mlp_fused = false;       // decode step: fc1 -> fc2 in one launch, in-launch hand-off (WMX_MLP_FUSED=1)
+  bool xa_recsplit = false;     // decode step: cross-attention records merged by the cross out-projection (env at creation)
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -1023,9 +1024,11 @@ static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int 
 }
 
 // decoder projection on packed weights, split-K raw partials into c.part; returns the split count
-static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, W8 w8 = {}) {
+static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, W8 w8 = {},
+                       const float2* arec = nullptr) {
   PackedCall g;
   g.A = A;
+  g.arec = arec;
   g.lda = lda;
   set_w(g, Wp, w8);
   g.M = M;
@@ -1047,13 +1050,13 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
 // carrying the reduction and the LayerNorm when the shape allows (RedTail), else the GEMM and reduce_ln
 static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K,
                          const float* bias, const float* g, const float* b, unsigned long long* redprobe = nullptr,
-                         W8 w8 = {}, int ablate = 0) {
+                         W8 w8 = {}, int ablate = 0, const float2* arec = nullptr) {
   // opt-in (WMX_REDLN_FUSED): measured slower than the separate reduce_ln launch, 798 vs 587 ms per call on the
   // default bench -- the in-launch chain (sc1 partial loads, write-through x, a second arrival, the single
   // normalising workgroup's row loads) costs ~10 us more than the kernel boundary it removes
   static const bool fused = getenv("WMX_REDLN_FUSED") != nullptr;
   const int S = packed_splits(M, N, K, c.part_elems);
-  if (fused && !w8.q8 && packed_tail_ok(M, N, K, S)) {
+  if (fused && !w8.q8 && !arec && packed_tail_ok(M, N, K, S)) {
     PackedCall p;
     p.A = A;
     p.lda = lda;
@@ -1073,7 +1076,7 @@ static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp
     return;
   }
   // (ablate: timing-only WMX_ABLATE bits of dec_step_fast; 16 = leave out the GEMM, 4 = leave out reduce_ln)
-  const int S2 = (ablate & 16) ? S : gemm_p_part(c, A, lda, Wp, M, N, K, w8);
+  const int S2 = (ablate & 16) ? S : gemm_p_part(c, A, lda, Wp, M, N, K, w8, arec);
   c.cur_probe = nullptr;
   if (!(ablate & 4)) launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st, redprobe, c.slot);
 }
@@ -1397,10 +1400,19 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
       x.tprobe = c.probe_buf + kProbeCross * probe_stride;
       x.pphase = c.phase_buf;
     }
+    // (WMX_XATTN_RECSPLIT, the 16-bit fused form with two key chunks: the chunks' records merged in the cross
+    // out-projection's A loads instead of by the last-arriving chunk: no ticket, no merge pass in the attention)
+    const float2* arec = nullptr;
+    if (c.xa_recsplit && c.xq_fused && !m.w8 && !m.fold && cross_attn_key_chunks(x) == 2 &&
+        packed_plan(R, dt, dt, packed_splits(R, dt, dt, c.part_elems), 0, false).NW <= 8) {
+      x.rec_o = c.xa_ws;
+      x.rec_ml = reinterpret_cast<float2*>(c.xa_ws + (size_t)2 * R * dt);
+      arec = x.rec_ml;
+    }
     if (!(ab & 2)) launch_cross_attn(c.dt, x, c.xa_ws, c.st);
     probe(kProbeCrossOut);
-    gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b, pbuf(kProbeRedCrossOut),
-                 w8_of(m, L.q8co, L.s8co), ab);
+    gemm_p_redln(c, arec ? reinterpret_cast<const uint16_t*>(x.rec_o) : c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g,
+                 L.ln3b, pbuf(kProbeRedCrossOut), w8_of(m, L.q8co, L.s8co), ab, arec);
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
     if (c.mlp_fused && mlp_fused_ok(R, dt)) {  // one launch for fc1 -> fc2 (its span is recorded as the fc1 probe), then reduce_ln
       MlpCall mc;
@@ -2798,6 +2810,7 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       // projection reads e4m3 weights beside fp8 images only)
       c.xq_fused = !(getenv("WMX_XQ_FUSED") && atoi(getenv("WMX_XQ_FUSED")) == 0) && !w->m.i8;
       c.mlp_fused = getenv("WMX_MLP_FUSED") && atoi(getenv("WMX_MLP_FUSED")) == 1 && !w->m.w8;
+      c.xa_recsplit = getenv("WMX_XATTN_RECSPLIT") && atoi(getenv("WMX_XATTN_RECSPLIT")) == 1;
       gemm_init_attributes();
       alloc_ctx(c);
     } catch (...) {

@@ -126,6 +126,37 @@ def test_forced_steps_wide_beam5_4windows(wide20):
     _check_forced("wide beam5 B=4", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
 
 
+def test_cross_records_merged_by_the_out_projection_bit_identical(wide20):
+    """WMX_XATTN_RECSPLIT=1 (read at context creation): the decode cross attention's two key-chunk records are merged
+    in the cross out-projection's A loads instead of by the last-arriving chunk (no ticket, no in-launch merge).  The
+    consumer repeats the attention's merge operation for operation, so the teacher-forced logits of every step and
+    row are bit-identical to the default form's, at the bench's per-group shape (4 windows x beam 5, prompted)."""
+    import os
+    from wmx import engine as E
+    dt, m, W, mels, encs = wide20
+    sp = O.special_tokens(WIDE2.n_vocab)
+    n = 12
+    tok, par = _forced_stream(np.random.default_rng(23), n, 20, 5)
+    prefix = [[sp.sot_prev] + list(range(1000, 1000 + L)) + [sp.sot, sp.lang0, sp.transcribe] for L in (0, 5, 11, 2)]
+    prefix[0] = [sp.sot, sp.lang0, sp.transcribe]
+    out = []
+    for flag in ("0", "1"):
+        old = os.environ.get("WMX_XATTN_RECSPLIT")
+        os.environ["WMX_XATTN_RECSPLIT"] = flag
+        try:
+            ctx = E.Context(m, max_batch=4, beam_size=5, max_new_tokens=64, word_timestamps=False)
+        finally:
+            if old is None:
+                del os.environ["WMX_XATTN_RECSPLIT"]
+            else:
+                os.environ["WMX_XATTN_RECSPLIT"] = old
+        ctx.encode(mels[:4], want_output=False)
+        out.append(ctx.forced_decode(prefix, tok, par, logits_every=1))
+        ctx.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 def test_forced_steps_micro_beam5_224():
     """224 steps with beams reordered every step: self attention over up to 227 ancestry-gathered slots."""
     from wmx import engine as E
