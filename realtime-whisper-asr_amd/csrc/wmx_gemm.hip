@@ -297,6 +297,9 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
 // by global_load_lds_dwordx4.  Up to three slices stay in flight across raw s_barriers: each slice is waited
 // for with a COUNTED vmcnt (cdna_hip_programming.md §5 "Pipelining across barriers"), never vmcnt(0) and never
 // __syncthreads() inside the loop.  All LDS is one extern array (§5 item 4(a)).
+// Default (WMX_G256_BK = 64, wmx_kernels.h): the half-tile ring below the staging comment, whole 128-B lines per
+// row and K-tile; TCP -> L2 read requests halve against the 32-deep ring (qkv 13.8 M -> 7.2 M per launch) and the
+// main loop takes 23 % fewer clocks (tools/mb_gemm256, profiles/r05h_g256_k64/).  The 32-deep ring (BK = 32):
 // LDS rows are 64 B (32 k); the 16-B piece p of row r sits at p ^ sw(r), sw(r) = (-(r >> 2)) & 3.  gfx950 serves a
 // ds_read_b128 in four 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
 // {36-43,48-51,60-63} (MI355X_MICROARCH.md, LDS table); with fragment lane (r = l & 15, p = l >> 4) this swizzle
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
 #endif
 #ifdef WMX_G256_STAMPS
 constexpr int kG256Stamps = 16384;
-__device__ unsigned long long g256_stamps[kG256Stamps][3];
+__device__ unsigned long long g256_stamps[kG256Stamps][5];  // memtime: start, loop end, end; memrealtime: start, end
 #endif
 #ifndef WMX_G256_PHASES
 #define WMX_G256_PHASES 2  // barrier-separated MFMA segments per 32-deep slice (1: one 32-MFMA segment per slice)
@@ -345,7 +348,9 @@ constexpr bool g256_lnf() { return KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GE
 template <int KIND>
 constexpr int g256_slots() { return (g256_lnf<KIND>() || WMX_G256_PHASES == 1) ? 4 : WMX_G256_SLOTS; }
 template <int KIND>
-constexpr int g256_lds() { return g256_lnf<KIND>() ? kG256Lds : g256_slots<KIND>() * kG256Slot; }
+constexpr int g256_lds() {
+  return g256_lnf<KIND>() ? kG256Lds : (WMX_G256_BK == 64 ? 4 : g256_slots<KIND>()) * kG256Slot;
+}
 static_assert(5 * kG256Slot <= 163840 && kG256Lds <= 163840, "gemm256 LDS");
 // s_waitcnt vmcnt(n) for a runtime n in {0, 2, ..., 14} (uniform): the count must be an immediate
 __device__ inline void vmcnt_even(int n) {
@@ -707,7 +712,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   // slices are in flight, and the workgroup's LDS is not released and re-acquired per tile
   for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
 #ifdef WMX_G256_STAMPS
-  const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   int bid = tile;
   {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles
@@ -724,7 +729,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
+#if WMX_G256_BK != 64
   const int nk = K >> 5;
+#endif
   constexpr int NS = g256_slots<KIND>();  // ring slots: NS - 1 slices in flight ahead of the one being read
   // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias, loaded now so its latency hides behind
   // the main loop (the epilogue's column quads are the same in all four rounds)
@@ -757,6 +764,129 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
   }
 
+#if WMX_G256_BK == 64
+  // Half-tile ring (the geometry of cdna_hip_programming.md §5's 256² template): K-tiles of 64 (128-B rows = whole
+  // cache lines, where the 32-deep slices below fetch every line in two halves one slice apart) in two 64 KiB buffers
+  // (t & 1) of four 16 KiB units, each 128 rows x 128 B:
+  //   unit 0 = A rows m0 + 128 wm + [0, 64)   (quadrant row 0 of every wave)    read in phase 0
+  //   unit 1 = W rows n0 + 64 wn + [0, 32)    (quadrant column 0)                read in phases 0 and 3
+  //   unit 2 = W rows n0 + 64 wn + [32, 64)   (quadrant column 1)                read in phase 1
+  //   unit 3 = A rows m0 + 128 wm + [64, 128) (quadrant row 1)                   read in phase 2
+  // Phase p of K-tile t: [LDS reads of its unit(s) + 2 DMAs of one unit] s_barrier [16 MFMAs: one 64 x 32 quadrant
+  // of the wave's 128 x 64 tile, K = 64] s_barrier, quadrants (0,0) (0,1) (1,1) (1,0); waves 4..7 one barrier behind.
+  // A unit is restaged one phase after its last read (every memory segment retires its reads before its barrier):
+  // phase 0 stages unit 1 of K-tile t + 1, phases 1..3 units 0, 2, 3 of K-tile t + 2; one counted wait per K-tile,
+  // vmcnt(6) in phase 3 (the three units of t + 2 may fly), completes K-tile t + 1 three to six phases after issue.
+  // Row r of a unit sits at r * 128 B with its 16-B chunk c at position c ^ ((r >> 1) & 7): a fragment read (16 rows
+  // fr, chunk 4s + fq) puts every ds_read_b128 lane group on 16 distinct (r & 1, position) pairs = all 64 banks.
+  const int nk = K >> 6;
+  uint32_t uoff[4][2];  // element offsets from A (units 0, 3) or W (units 1, 2) of this lane's two pieces (w, w + 8)
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = 8 * (wave + 8 * j) + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      if (u == 0 || u == 3) {
+        const int m = min(m0 + (r >> 6) * 128 + (u == 3 ? 64 : 0) + (r & 63), M - 1);
+        uoff[u][j] = (uint32_t)((long)m * lda + c * 8);
+      } else {
+        const int n = min(n0 + (r >> 5) * 64 + (u == 2 ? 32 : 0) + (r & 31), N - 1);
+        uoff[u][j] = (uint32_t)((long)n * ldw + c * 8);
+      }
+    }
+  auto issue_unit = [&](int t, int u) {
+    char* dst = smem + (t & 1) * 65536 + u * 16384;
+    const uint16_t* base = (u == 0 || u == 3) ? A : W;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + uoff[u][j] + (long)t * 64),
+                                       (__attribute__((address_space(3))) void*)(dst + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw0 = (fq ^ (fr >> 1)) << 4, sw1 = ((4 + fq) ^ (fr >> 1)) << 4;
+  const int arow = (wm * 64 + fr) * 128, brow = (wn * 32 + fr) * 128;
+  u16x8 af[4][2], bfr[2][2];
+  auto read_a = [&](const char* U) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      af[ii][0] = *reinterpret_cast<const u16x8*>(U + arow + ii * 2048 + sw0);
+      af[ii][1] = *reinterpret_cast<const u16x8*>(U + arow + ii * 2048 + sw1);
+    }
+  };
+  auto read_b = [&](const char* U) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      bfr[jj][0] = *reinterpret_cast<const u16x8*>(U + brow + jj * 2048 + sw0);
+      bfr[jj][1] = *reinterpret_cast<const u16x8*>(U + brow + jj * 2048 + sw1);
+    }
+  };
+  auto quadrant = [&](int g, int h) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          acc[4 * g + ii][2 * h + jj] = WMX_G256_MFMA(af[ii][s], bfr[jj][s], acc[4 * g + ii][2 * h + jj]);
+  };
+  // prologue: K-tile 0 whole, then units 0, 2, 3 of K-tile 1 (its unit 1 goes out in phase 0 of K-tile 0)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) issue_unit(0, u);
+  if (nk > 1) {
+    issue_unit(1, 0);
+    issue_unit(1, 2);
+    issue_unit(1, 3);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  if (lagging) __builtin_amdgcn_s_barrier();
+#if WMX_G256_PRIO == 1
+  if (lagging) __builtin_amdgcn_s_setprio(1);
+#endif
+#define WMX_G256_SEG(QG, QH)                                 \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
+  __builtin_amdgcn_sched_barrier(0);                         \
+  __builtin_amdgcn_s_barrier();                              \
+  WMX_G256_PRIO_ON;                                          \
+  quadrant(QG, QH);                                          \
+  WMX_G256_PRIO_OFF;                                         \
+  __builtin_amdgcn_sched_barrier(0);                         \
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const char* U = smem + (t & 1) * 65536;
+    read_a(U);  // phase 0: units 0 and 1
+    read_b(U + 16384);
+    if (t + 1 < nk) issue_unit(t + 1, 1);
+    WMX_G256_SEG(0, 0)
+    read_b(U + 2 * 16384);  // phase 1: unit 2
+    if (t + 2 < nk) issue_unit(t + 2, 0);
+    WMX_G256_SEG(0, 1)
+    read_a(U + 3 * 16384);  // phase 2: unit 3
+    if (t + 2 < nk) issue_unit(t + 2, 2);
+    WMX_G256_SEG(1, 1)
+    read_b(U + 16384);  // phase 3: unit 1 again
+    if (t + 2 < nk) {
+      issue_unit(t + 2, 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-tile t + 1 complete
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    WMX_G256_SEG(1, 0)
+  }
+#undef WMX_G256_SEG
+#else
   // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
   // Wave w issues pieces w, w + 8, w + 16, w + 24; lane l covers row l >> 2, 16-B column (l & 3).
   const int srow = lane >> 2;
@@ -890,6 +1020,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     __builtin_amdgcn_s_barrier();
   }
 #endif
+#endif  // WMX_G256_BK
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
   if constexpr (kLnf) {  // Chan merge of the equal-count (256-column) groups of each of the tile's rows
@@ -990,6 +1121,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
       g256_stamps[tile][0] = st0;
       g256_stamps[tile][1] = st1;
       g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
+      g256_stamps[tile][3] = rt0;
+      g256_stamps[tile][4] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     __syncthreads();  // the next tile's DMA must not overwrite the ring before every wave left this tile
@@ -1027,6 +1160,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     g256_stamps[tile][0] = st0;
     g256_stamps[tile][1] = st1;
     g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
+    g256_stamps[tile][3] = rt0;
+    g256_stamps[tile][4] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
   }  // tile loop
@@ -2644,7 +2779,7 @@ static void launch_t(const GemmCall& g, hipStream_t st) {
     return;
   }
   if (g.tile == TILE_256) {
-    WMX_CHECK(g.K % 32 == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm256: K / leading dimensions");
+    WMX_CHECK(g.K % WMX_G256_BK == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm256: K / leading dimensions");
     WMX_CHECK(g.epi.kind != EPI_CROSSKV || (g.epi.d % 256 == 0 && g.epi.xt % 4 == 0), "gemm256: cross K/V shape");
     const bool lns = g.epi.kind == EPI_RESID32_LNS || g.epi.kind == EPI_GELU_POS32_LNS;
     const bool lnf = g.epi.kind == EPI_LNF_STORE16 || g.epi.kind == EPI_LNF_GELU16;

@@ -87,6 +87,11 @@ __host__ __device__ inline long crossv8_off(int t, int c) {
 }
 
 enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3, TILE_256 = 4 };
+// K depth of one staged slice of the 256 x 256 GEMM (gemm256_kernel): 64 = the half-tile ring of whole 128-B lines
+// (default, K % 64 == 0), 32 = the 32-deep slice ring (every 128-B line fetched in two halves one slice apart)
+#ifndef WMX_G256_BK
+#define WMX_G256_BK 64
+#endif
 
 struct GemmCall {
   const uint16_t* A;

@@ -941,7 +941,7 @@ static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ld
     return;
   }
   static const bool no_g256 = getenv("WMX_NO_G256") != nullptr;  // A/B switch for tuning runs
-  if (!no_g256 && M >= 4096 && K % 32 == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
+  if (!no_g256 && M >= 4096 && K % WMX_G256_BK == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
       (e.kind != EPI_CROSSKV || e.d % 256 == 0) && e.kind != EPI_QKV_CACHE) {
     // encoder / conv front end / cross-K/V: 256x256 ping-pong tile, every tile on its own CU
     g.tile = TILE_256;

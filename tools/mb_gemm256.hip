@@ -95,15 +95,21 @@ int main(int argc, char** argv) {
     const float t2 = timeit([&] { launch_gemm(DT::BF16, h, 0); }, iters);
 #ifdef WMX_G256_STAMPS
     {  // per-tile phase clocks of the last timed launch: main loop (incl. prologue) vs epilogue, in shader clocks
-      static unsigned long long stv[kG256Stamps][3];
+      static unsigned long long stv[kG256Stamps][5];
       hipMemcpyFromSymbol(stv, HIP_SYMBOL(g256_stamps), sizeof(stv));
       const int nt = std::min(kG256Stamps, ((s.M + 255) / 256) * ((s.N + 255) / 256));
-      double mainc = 0, epic = 0;
+      double mainc = 0, epic = 0, clk = 0;
+      unsigned long long rmin = ~0ull, rmax = 0;
       for (int t = 0; t < nt; ++t) {
         mainc += (double)(stv[t][1] - stv[t][0]);
         epic += (double)(stv[t][2] - stv[t][1]);
+        clk += (double)(stv[t][2] - stv[t][0]) / (double)std::max(1ull, stv[t][4] - stv[t][3]) * 0.1;  // GHz
+        rmin = std::min(rmin, stv[t][3]);
+        rmax = std::max(rmax, stv[t][4]);
       }
-      printf("  stamps %s: main %.0f clk, epilogue %.0f clk per tile (%d tiles)\n", s.name, mainc / nt, epic / nt, nt);
+      printf("  stamps %s: main %.0f clk, epilogue %.0f clk per tile (%d tiles), in-kernel clock %.3f GHz, "
+             "first tile start to last tile end %.1f us\n",
+             s.name, mainc / nt, epic / nt, nt, clk / nt, (rmax - rmin) * 0.01);
     }
 #endif
     hipDeviceSynchronize();
