@@ -19,6 +19,8 @@
 #include "wmx_common.h"
 #include "wmx_kernels.h"
 
+#include <type_traits>
+
 namespace wmx {
 
 // K and V^T of [L][xw][H] (window, head) images, each kXS x 64 in the fragment-major order of crossk_off /
@@ -325,6 +327,15 @@ __device__ unsigned long long g256_stamps[kG256Stamps][5];  // memtime: start, l
 #endif
 #ifndef WMX_G256_PRIO
 #define WMX_G256_PRIO 1  // 1: static priority 1 for waves 4..7 only (19.52-19.58 vs 19.81-19.84 ms per encoder pass); 0: s_setprio 1 around every MFMA segment (T5)
+#endif
+#ifndef WMX_G256_PIN_SEGMENTS
+#define WMX_G256_PIN_SEGMENTS 1  // a scheduling barrier after each segment's opening s_barrier (0: the compiler hoists
+                                 // the segment's first MFMA above it, into the partner's compute segment)
+#endif
+#if WMX_G256_PIN_SEGMENTS
+#define WMX_G256_PIN __builtin_amdgcn_sched_barrier(0)
+#else
+#define WMX_G256_PIN (void)0
 #endif
 #if WMX_G256_PRIO == 0
 #define WMX_G256_PRIO_ON __builtin_amdgcn_s_setprio(1)
@@ -859,6 +870,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
   __builtin_amdgcn_sched_barrier(0);                         \
   __builtin_amdgcn_s_barrier();                              \
+  WMX_G256_PIN;                                              \
   WMX_G256_PRIO_ON;                                          \
   quadrant(QG, QH);                                          \
   WMX_G256_PRIO_OFF;                                         \
@@ -1378,9 +1390,12 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
 // 16..31 (g = l >> 5), i.e. 16-B pieces g and 2 + g of its 64-B row; its scale operand is the byte of (row l & 31,
 // 32-k block g) (tools/mx8_check32.hip measures both maps).  Epilogues through the 64 x 256 fp32 LDS image.
 // ------------------------------------------------------------------------------------------------
+#ifndef WMX_MX8_BK
+#define WMX_MX8_BK 128  // 128: the half-tile ring of whole 128-B lines; 64: 64-deep slices (half lines)
+#endif
 constexpr int kMx8bSlot = 512 * 64 + 512 * 4;  // 256 A + 256 W rows x 64 B, + the scale dword of each row
 constexpr int kMx8bNS = 4;
-constexpr int kMx8bLds = kMx8bNS * kMx8bSlot;  // 132 KiB
+constexpr int kMx8bLds = WMX_MX8_BK == 128 ? 4 * 32768 + 2 * 2048 : kMx8bNS * kMx8bSlot;  // 132 / 136 KiB
 static_assert(kMx8bLds <= 163840 && 64 * (256 + 4) * 4 <= kMx8bLds, "gemm_mx8_256 LDS");
 // s_waitcnt vmcnt(n), n in 0..15 (uniform)
 __device__ inline void vmcnt_upto15(int n) {
@@ -1429,10 +1444,166 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
+#if WMX_MX8_BK != 128
   const int nk = K >> 6;
+#endif
   float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#if WMX_MX8_BK != 128  // (the 128-deep ring loads it after the main loop: no VGPRs to spare inside)
   if (e.bias && n0 + 4 * (tid & 63) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (tid & 63));
+#endif
 
+#if WMX_MX8_BK == 128
+  // 128-deep half-tile ring (as gemm256's 64-deep one, WMX_G256_BK): a K-tile is 128 e4m3 = one 128-B line per row,
+  // four 16 KiB units of 128 rows in two buffers (unit 0 = A rows m0 + 128 wm + [0, 64), 1 = W rows n0 + 64 wn +
+  // [0, 32), 2 = W rows n0 + 64 wn + [32, 64), 3 = A rows m0 + 128 wm + [64, 128)) plus the K-tile's scale dword of
+  // every row (4 e8m0 bytes) in a 2 KiB buffer per K-tile, staged with unit 1.  Phase p: one 64 x 32 quadrant of the
+  // wave's 128 x 64 tile (2 A blocks x 1 W block x 2 K-steps = 4 MFMAs of 64 cycles), quadrants (0,0) (0,1) (1,1)
+  // (1,0); unit 1 + scales of K-tile t + 1 in phase 0, units 0, 2, 3 of t + 2 in phases 1..3, one vmcnt(6) per
+  // K-tile.  Row r holds chunk c at c ^ ((r >> 1) & 7): conflict-free for the 32-row fragments' lane groups.
+  const int nk = K >> 7;
+  // this lane's unit row (pieces w and w + 8) and swizzled source chunk; the row offsets are recomputed per issue
+  // (the f32x16 accumulators leave no room for eight resident offsets)
+  const int ur = 8 * wave + (lane >> 3);
+  const int uc = ((lane & 7) ^ ((ur >> 1) & 7)) * 16;  // (ur + 64) has the same (r >> 1) & 7
+  // scales: wave w < 4 stages A rows 64 w + lane, wave w >= 4 W rows 64 (w - 4) + lane (K-tile t: dword t of the row)
+  const uint8_t* ssrc = wave < 4 ? AS + (long)min(m0 + 64 * wave + lane, M - 1) * ldas
+                                 : WS + (long)min(n0 + 64 * (wave - 4) + lane, N - 1) * ldws;
+  constexpr int kSc = 4 * 32768;  // scale buffers after the two 64 KiB unit buffers
+  auto issue_unit = [&](int t, int u) {
+    char* dst = smem + (t & 1) * 65536 + u * 16384;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = ur + 64 * j;
+      const uint8_t* src;
+      if (u == 0 || u == 3)
+        src = A + (long)min(m0 + (r >> 6) * 128 + (u == 3 ? 64 : 0) + (r & 63), M - 1) * lda;
+      else
+        src = W + (long)min(n0 + (r >> 5) * 64 + (u == 2 ? 32 : 0) + (r & 31), N - 1) * ldw;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + uc + (long)t * 128),
+                                       (__attribute__((address_space(3))) void*)(dst + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+  auto issue_scales = [&](int t) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc + (long)t * 4),
+                                     (__attribute__((address_space(3))) void*)(smem + kSc + (t & 1) * 2048 + wave * 256),
+                                     4, 0, 0);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  const int fr = lane & 31, g = lane >> 5;
+  const int sw = (fr >> 1) & 7;
+  // K-step s of a fragment: 16-B chunks 4 s + g and 4 s + 2 + g of the lane's row (bytes 16 g.. and 32 + 16 g..)
+  const int q00 = ((0 + g) ^ sw) << 4, q01 = ((2 + g) ^ sw) << 4, q10 = ((4 + g) ^ sw) << 4, q11 = ((6 + g) ^ sw) << 4;
+  const int arow = (wm * 64 + fr) * 128, brow = (wn * 32 + fr) * 128;
+  const int sarow = (wm * 128 + fr) * 4 + g, sbrow = 1024 + (wn * 64 + fr) * 4 + g;
+  i32x8 af[2][2], bfr[2];
+  int sa[2][2], sb[2];
+  auto frag2 = [&](const char* U, int off, i32x8& f0, i32x8& f1) {
+    const i32x4 a0 = *reinterpret_cast<const i32x4*>(U + off + q00);
+    const i32x4 a1 = *reinterpret_cast<const i32x4*>(U + off + q01);
+    const i32x4 b0 = *reinterpret_cast<const i32x4*>(U + off + q10);
+    const i32x4 b1 = *reinterpret_cast<const i32x4*>(U + off + q11);
+    f0 = i32x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    f1 = i32x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  };
+  // A blocks 2 g2 + ii (ii = 0, 1) of unit 0 (g2 = 0) or 3 (g2 = 1), with their scale bytes (block 2 s + g of the tile)
+  auto read_a = [&](const char* U, const char* SC, int g2) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      frag2(U, arow + ii * 4096, af[ii][0], af[ii][1]);
+      const char* sp = SC + sarow + (64 * g2 + 32 * ii) * 4;
+      sa[ii][0] = (int)*reinterpret_cast<const uint8_t*>(sp);
+      sa[ii][1] = (int)*reinterpret_cast<const uint8_t*>(sp + 2);
+    }
+  };
+  auto read_b = [&](const char* U, const char* SC, int h) {
+    frag2(U, brow, bfr[0], bfr[1]);
+    const char* sp = SC + sbrow + 32 * h * 4;
+    sb[0] = (int)*reinterpret_cast<const uint8_t*>(sp);
+    sb[1] = (int)*reinterpret_cast<const uint8_t*>(sp + 2);
+  };
+  auto quadrant = [&](int g2, int h) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+        acc[2 * g2 + ii][h] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[ii][s], bfr[s], acc[2 * g2 + ii][h], 0,
+                                                                              0, 0, sa[ii][s], 0, sb[s]);
+  };
+  issue_scales(0);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) issue_unit(0, u);
+  if (nk > 1) {
+    issue_unit(1, 0);
+    issue_unit(1, 2);
+    issue_unit(1, 3);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  if (lagging) __builtin_amdgcn_s_barrier();
+#if WMX_G256_PRIO == 1
+  if (lagging) __builtin_amdgcn_s_setprio(1);
+#endif
+#define WMX_MX8_SEG(QG, QH)                          \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+  __builtin_amdgcn_sched_barrier(0);                 \
+  __builtin_amdgcn_s_barrier();                      \
+  WMX_G256_PIN;                                      \
+  WMX_G256_PRIO_ON;                                  \
+  quadrant(QG, QH);                                  \
+  WMX_G256_PRIO_OFF;                                 \
+  __builtin_amdgcn_sched_barrier(0);                 \
+  __builtin_amdgcn_s_barrier();
+  // one K-tile; I1 / I2: K-tile t + 1 / t + 2 exists.  The three forms are separate straight-line bodies: a
+  // conditional issue inside the body let the compiler sink three phases' MFMAs past their barriers into the block
+  // after the last branch (and spill the accumulators that then overlapped)
+  auto ktile = [&](int t, auto I1, auto I2) {
+    const char* U = smem + (t & 1) * 65536;
+    const char* SC = smem + kSc + (t & 1) * 2048;
+    read_a(U, SC, 0);  // phase 0: units 0 and 1
+    read_b(U + 16384, SC, 0);
+    if constexpr (decltype(I1)::value) {
+      issue_unit(t + 1, 1);
+      issue_scales(t + 1);
+    }
+    WMX_MX8_SEG(0, 0)
+    read_b(U + 2 * 16384, SC, 1);  // phase 1: unit 2
+    if constexpr (decltype(I2)::value) issue_unit(t + 2, 0);
+    WMX_MX8_SEG(0, 1)
+    read_a(U + 3 * 16384, SC, 1);  // phase 2: unit 3
+    if constexpr (decltype(I2)::value) issue_unit(t + 2, 2);
+    WMX_MX8_SEG(1, 1)
+    read_b(U + 16384, SC, 0);  // phase 3: unit 1 again
+    if constexpr (decltype(I2)::value) {
+      issue_unit(t + 2, 3);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-tile t + 1 complete (unit 1 + scales, then 0, 2, 3)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    WMX_MX8_SEG(1, 0)
+  };
+  using Yes = std::integral_constant<bool, true>;
+  using No = std::integral_constant<bool, false>;
+  for (int t = 0; t + 2 < nk; ++t) ktile(t, Yes{}, Yes{});
+  if (nk >= 2) ktile(nk - 2, Yes{}, No{});
+  ktile(nk - 1, No{}, No{});
+  // anchor every accumulator here: the epilogue reads each one inside a wave-row branch, where the compiler would
+  // otherwise sink the last K-tile's MFMAs (out of their barrier segments)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i][j]));
+#undef WMX_MX8_SEG
+#else
   // staging as gemm256: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 A rows, 16..31 W rows; wave w
   // issues pieces w, w + 8 (A) and w + 16, w + 24 (W); lane l: row l >> 2, 16-B column (l & 3) swizzled at the source
   const int srow = lane >> 2;
@@ -1548,6 +1719,10 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   }
+#endif  // WMX_MX8_BK
+#if WMX_MX8_BK == 128
+  if (e.bias && n0 + 4 * (tid & 63) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (tid & 63));
+#endif
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
 
