@@ -434,7 +434,9 @@ __device__ inline void resid_load(Resid8& R, const Epi& e, int mb, int n0, int M
   }
 }
 
-template <DT T, int KIND>
+// UB: rows per batch of loads (8: all of the thread's rows at once; 4: two batches, for a caller whose accumulators
+// leave no room for 64 more VGPRs)
+template <DT T, int KIND, int UB = 8>
 __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int mb, int n0, int M, int N, int tid,
                                   const float4* bpre = nullptr, const Resid8* pre = nullptr) {
   constexpr int KD = KIND;
@@ -446,27 +448,31 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
     b = *bpre;
   else if (e.bias)
     b = *reinterpret_cast<const float4*>(e.bias + n);
-  float4 v[8], aux[8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int ub = 0; ub < 8; ub += UB) {
+  float4 v[UB], aux[UB];
+#pragma unroll
+  for (int uu = 0; uu < UB; ++uu) {
+    const int u = ub + uu;
     const int row = r0 + 8 * u, m = mb + row;
-    v[u] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
-    v[u] = make_float4(v[u].x + b.x, v[u].y + b.y, v[u].z + b.z, v[u].w + b.w);
+    v[uu] = *reinterpret_cast<const float4*>(img + row * ldt + c4);
+    v[uu] = make_float4(v[uu].x + b.x, v[uu].y + b.y, v[uu].z + b.z, v[uu].w + b.w);
     if (KD == EPI_RESID32 && pre)
-      aux[u] = pre->f[u];
+      aux[uu] = pre->f[u];
     else if (KD == EPI_RESID32 && m < M)
-      aux[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
+      aux[uu] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e.out) + (long)m * e.ldc + n);
     if (KD == EPI_GELU_POS32 && m < M)
-      aux[u] = *reinterpret_cast<const float4*>(e.pos + (long)(m % e.posT) * e.ldc + n);
+      aux[uu] = *reinterpret_cast<const float4*>(e.pos + (long)(m % e.posT) * e.ldc + n);
   }
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int uu = 0; uu < UB; ++uu) {
+    const int u = ub + uu;
     const int m = mb + r0 + 8 * u;
     if (m >= M) continue;
-    float4 x = v[u];
+    float4 x = v[uu];
     if (KD == EPI_GELU16 || KD == EPI_GELU_POS32 || KD == EPI_GELU_MX8) x = gelu_erf4(x);
     if (KD == EPI_RESID32 || KD == EPI_GELU_POS32)
-      x = make_float4(x.x + aux[u].x, x.y + aux[u].y, x.z + aux[u].z, x.w + aux[u].w);
+      x = make_float4(x.x + aux[uu].x, x.y + aux[uu].y, x.z + aux[uu].z, x.w + aux[uu].w);
     if (KD == EPI_GELU_MX8) {
       // the 8 lanes of a 32-column block (c4 = 4 * (tid & 63)) agree on the block scale; every lane of the wave
       // is on the same row, so the shuffles never cross an inactive lane
@@ -483,6 +489,7 @@ __device__ inline void epi_rows64(const Epi& e, const float* img, int ldt, int m
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n) = x;
     }
+  }
   }
 }
 
@@ -1465,6 +1472,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
   // (the f32x16 accumulators leave no room for eight resident offsets)
   const int ur = 8 * wave + (lane >> 3);
   const int uc = ((lane & 7) ^ ((ur >> 1) & 7)) * 16;  // (ur + 64) has the same (r >> 1) & 7
+  // unit rows: A (units 0, 3) m0 + ur + 128 j + 64 [u == 3]; W (units 1, 2) n0 + 64 (ur >> 5) + (ur & 31) + 128 j +
+  // 32 [u == 2] (N % 256 == 0 here: W rows need no clamp)
+  const int arb = m0 + ur, wrb = n0 + 64 * (ur >> 5) + (ur & 31);
   // scales: wave w < 4 stages A rows 64 w + lane, wave w >= 4 W rows 64 (w - 4) + lane (K-tile t: dword t of the row)
   const uint8_t* ssrc = wave < 4 ? AS + (long)min(m0 + 64 * wave + lane, M - 1) * ldas
                                  : WS + (long)min(n0 + 64 * (wave - 4) + lane, N - 1) * ldws;
@@ -1473,12 +1483,15 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
     char* dst = smem + (t & 1) * 65536 + u * 16384;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int r = ur + 64 * j;
+      // the row base goes through an empty asm per issue, so the compiler recomputes the row instead of holding
+      // eight row pointers across the K loop (they spilled beside the f32x16 accumulators)
+      int rb = (u == 0 || u == 3) ? arb : wrb;
+      asm volatile("" : "+v"(rb));
       const uint8_t* src;
       if (u == 0 || u == 3)
-        src = A + (long)min(m0 + (r >> 6) * 128 + (u == 3 ? 64 : 0) + (r & 63), M - 1) * lda;
+        src = A + (long)min(rb + 128 * j + (u == 3 ? 64 : 0), M - 1) * lda;
       else
-        src = W + (long)min(n0 + (r >> 5) * 64 + (u == 2 ? 32 : 0) + (r & 31), N - 1) * ldw;
+        src = W + (long)(rb + 128 * j + (u == 2 ? 32 : 0)) * ldw;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + uc + (long)t * 128),
                                        (__attribute__((address_space(3))) void*)(dst + (wave + 8 * j) * 1024), 16, 0,
                                        0);
@@ -1499,16 +1512,20 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
   const int fr = lane & 31, g = lane >> 5;
   const int sw = (fr >> 1) & 7;
   // K-step s of a fragment: 16-B chunks 4 s + g and 4 s + 2 + g of the lane's row (bytes 16 g.. and 32 + 16 g..)
-  const int q00 = ((0 + g) ^ sw) << 4, q01 = ((2 + g) ^ sw) << 4, q10 = ((4 + g) ^ sw) << 4, q11 = ((6 + g) ^ sw) << 4;
+  // chunk 4 s + 2 h + g sits at ((4 s + 2 h + g) ^ sw) << 4 = (((g ^ sw) << 4) ^ (64 s + 32 h)): the row base plus
+  // the step-0 chunk offset, XORed (row bases are multiples of 128)
+  const int q00 = (g ^ sw) << 4;
   const int arow = (wm * 64 + fr) * 128, brow = (wn * 32 + fr) * 128;
   const int sarow = (wm * 128 + fr) * 4 + g, sbrow = 1024 + (wn * 64 + fr) * 4 + g;
   i32x8 af[2][2], bfr[2];
   int sa[2][2], sb[2];
   auto frag2 = [&](const char* U, int off, i32x8& f0, i32x8& f1) {
-    const i32x4 a0 = *reinterpret_cast<const i32x4*>(U + off + q00);
-    const i32x4 a1 = *reinterpret_cast<const i32x4*>(U + off + q01);
-    const i32x4 b0 = *reinterpret_cast<const i32x4*>(U + off + q10);
-    const i32x4 b1 = *reinterpret_cast<const i32x4*>(U + off + q11);
+    int o = off + q00;
+    asm volatile("" : "+v"(o));
+    const i32x4 a0 = *reinterpret_cast<const i32x4*>(U + o);
+    const i32x4 a1 = *reinterpret_cast<const i32x4*>(U + (o ^ 32));
+    const i32x4 b0 = *reinterpret_cast<const i32x4*>(U + (o ^ 64));
+    const i32x4 b1 = *reinterpret_cast<const i32x4*>(U + (o ^ 96));
     f0 = i32x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
     f1 = i32x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
   };
@@ -1749,6 +1766,8 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
     __syncthreads();
     if constexpr (KIND == EPI_GELU_MX8)
       epi_gelu_mx8_blocks<T>(e, img, LDT, m0 + rd * 64, n0, M, tid);
+    else if constexpr (KIND == EPI_RESID32 && WMX_MX8_BK == 128)  // (8 rows at once spilled beside the accumulators)
+      epi_rows64<T, EPI_RESID32, 4>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
     else
       epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4, kPre ? &pre : nullptr);
     if constexpr (kPre) {
