@@ -557,8 +557,8 @@ def main():
         ratio = evs["cross_attn"][0] / sum(evs[k][0] for k in chain)
         decode_mode = {"mode": "fast" if ratio >= 0.35 else "slow", "cross_to_chain_ratio": round(ratio, 4),
                        "rule": "cross attention / (packed GEMMs + reduce_ln) in situ >= 0.35 -> fast"}
-        if args.dtype == "fp8":  # the fp8 decode halves the cross attention's bytes: the bf16 calibration does not hold
-            decode_mode["mode"] = "n/a (rule calibrated on the bf16 decode)"
+        if args.dtype in ("fp8", "int8"):  # 8-bit weights halve the GEMMs' bytes (fp8 also the cross attention's): the
+            decode_mode["mode"] = "n/a (rule calibrated on the bf16 decode)"  # bf16 calibration does not hold
         # per context group: the slow mode can hit one group alone, and the call takes the
         # slower group's time; each group's decode stage and its own ratio
         per_group = []
