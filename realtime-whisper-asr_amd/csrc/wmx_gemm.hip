@@ -328,6 +328,10 @@ __device__ unsigned long long g256_stamps[kG256Stamps][5];  // memtime: start, l
 #ifndef WMX_G256_PRIO
 #define WMX_G256_PRIO 1  // 1: static priority 1 for waves 4..7 only (19.52-19.58 vs 19.81-19.84 ms per encoder pass); 0: s_setprio 1 around every MFMA segment (T5)
 #endif
+#ifndef WMX_G256_SWAP
+#define WMX_G256_SWAP 0  // 1: direct-epilogue kinds compute C^T fragments (a lane holds 4 consecutive columns of a row, no
+                         // transpose); 2: every kind.  Measured slower (the 32-B row pieces per store), opt-in
+#endif
 #ifndef WMX_G256_PIN_SEGMENTS
 #define WMX_G256_PIN_SEGMENTS 1  // a scheduling barrier after each segment's opening s_barrier (0: the compiler hoists
                                  // the segment's first MFMA above it, into the partner's compute segment)
@@ -351,6 +355,7 @@ constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
 // 128 KiB ring + the LayerNorm-folded kinds' raw row statistics [8 groups][256 rows] float2 and merged (mean, rstd)
 constexpr int kG256StatRaw = 4 * kG256Slot, kG256StatRow = kG256StatRaw + 8 * 256 * 8;
 constexpr int kG256Lds = kG256StatRow + 256 * 8;
+constexpr int kG256Bias = kG256Lds;  // the swapped direct epilogue's tile bias (c2) and c1 columns, [2][256] fp32
 #ifndef WMX_G256_SLOTS
 #define WMX_G256_SLOTS 5  // ring slots of the kinds without the LayerNorm-folded statistics (5 = 160 KiB; 4 slots measured 0.6 % slower)
 #endif
@@ -359,10 +364,17 @@ constexpr bool g256_lnf() { return KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GE
 template <int KIND>
 constexpr int g256_slots() { return (g256_lnf<KIND>() || WMX_G256_PHASES == 1) ? 4 : WMX_G256_SLOTS; }
 template <int KIND>
-constexpr int g256_lds() {
-  return g256_lnf<KIND>() ? kG256Lds : (WMX_G256_BK == 64 ? 4 : g256_slots<KIND>()) * kG256Slot;
+constexpr bool g256_swap() {  // the direct-epilogue kinds on the 64-deep ring compute C^T tiles (WMX_G256_SWAP)
+  return WMX_G256_SWAP && WMX_G256_BK == 64 &&
+         (KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GELU16 ||
+          (WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16)));
 }
-static_assert(5 * kG256Slot <= 163840 && kG256Lds <= 163840, "gemm256 LDS");
+template <int KIND>
+constexpr int g256_lds() {
+  return g256_swap<KIND>() ? kG256Bias + 2048
+                           : g256_lnf<KIND>() ? kG256Lds : (WMX_G256_BK == 64 ? 4 : g256_slots<KIND>()) * kG256Slot;
+}
+static_assert(5 * kG256Slot <= 163840 && kG256Bias + 2048 <= 163840, "gemm256 LDS");
 // s_waitcnt vmcnt(n) for a runtime n in {0, 2, ..., 14} (uniform): the count must be an immediate
 __device__ inline void vmcnt_even(int n) {
   switch (n) {
@@ -760,8 +772,22 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   constexpr bool kLnf = KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GELU16;
   constexpr bool kGelu = KIND == EPI_GELU16 || KIND == EPI_LNF_GELU16;
   constexpr bool kDirect = kLnf || (WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16));
+  constexpr bool kSwap = g256_swap<KIND>();
+  // every kind on the 64-deep ring computes C^T fragments (WMX_G256_SWAP = 2; 1: the direct-epilogue kinds only):
+  // the LDS-image epilogues then write a lane's 4 consecutive columns with one ds_write_b128 instead of 4 b32
+  constexpr bool kSwapAll = kSwap || (WMX_G256_SWAP == 2 && WMX_G256_BK == 64);
   const int bcol = kDirect ? (wave & 3) * 64 + 16 * (lane & 3) + 4 * ((lane >> 2) & 3) : 4 * (tid & 63);
   float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f), c14 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (kSwap) {
+    // the tile's 256 bias (c2) and c1 columns go to LDS by DMA ahead of the ring (wave 7: bias, wave 6: c1; one
+    // 1 KiB piece each, columns clamped to N - 4), covered by the main loop's first counted wait
+    if (wave >= 6 && (wave == 7 || kLnf) && e.bias) {
+      const float* src = wave == 7 ? e.bias : e.c1;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + min(n0 + 4 * lane, N - 4)),
+                                       (__attribute__((address_space(3))) void*)(smem + kG256Bias + (7 - wave) * 1024),
+                                       16, 0, 0);
+    }
+  }
   if constexpr (kLnf) {
     // the tile's raw statistics go to LDS by DMA ahead of the ring's first slices (wave g < lng: group g's 256 rows,
     // two 1 KiB pieces; rows past M clamped, never stored), so the counted vmcnt of the main loop covers them and no
@@ -775,10 +801,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
             (__attribute__((address_space(3))) void*)(smem + kG256StatRaw + (wave * 256 + 128 * pc) * 8), 16, 0, 0);
       }
     }
-    const int bc = min(n0 + bcol, N - 4);
-    bias4 = *reinterpret_cast<const float4*>(e.bias + bc);
-    c14 = *reinterpret_cast<const float4*>(e.c1 + bc);
-  } else if (KIND >= 0 && e.bias && n0 + bcol < N) {
+    if constexpr (!kSwap) {
+      const int bc = min(n0 + bcol, N - 4);
+      bias4 = *reinterpret_cast<const float4*>(e.bias + bc);
+      c14 = *reinterpret_cast<const float4*>(e.c1 + bc);
+    }
+  } else if (!kSwap && KIND >= 0 && e.bias && n0 + bcol < N) {
     bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
   }
 
@@ -854,7 +882,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
-          acc[4 * g + ii][2 * h + jj] = WMX_G256_MFMA(af[ii][s], bfr[jj][s], acc[4 * g + ii][2 * h + jj]);
+          acc[4 * g + ii][2 * h + jj] = kSwapAll ? WMX_G256_MFMA(bfr[jj][s], af[ii][s], acc[4 * g + ii][2 * h + jj])
+                                                 : WMX_G256_MFMA(af[ii][s], bfr[jj][s], acc[4 * g + ii][2 * h + jj]);
   };
   // prologue: K-tile 0 whole, then units 0, 2, 3 of K-tile 1 (its unit 1 goes out in phase 0 of K-tile 0)
 #pragma unroll
@@ -1074,7 +1103,52 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     continue;
   }
 #endif
-  if constexpr (kDirect) {
+  if constexpr (kSwap) {
+    // C^T fragments: lane (fr, fq) holds C[16 i + fr][16 j + 4 fq .. + 3] of the wave tile, four consecutive
+    // columns of one row: bias (c2) and c1 from the LDS stage, (mean, rstd) of the row from the merged statistics,
+    // one 8-byte store per (i, j), no transpose
+    const float* bl = reinterpret_cast<const float*>(smem + kG256Bias);
+    const int cb = wn * 64 + 4 * fq;
+    float4 b4[4], c4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      b4[j] = e.bias ? *reinterpret_cast<const float4*>(bl + cb + 16 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (kLnf) c4[j] = *reinterpret_cast<const float4*>(bl + 256 + cb + 16 * j);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rt = wm * 128 + 16 * i + fr, m = m0 + rt;
+      float2 ls = make_float2(0.f, 1.f);
+      if constexpr (kLnf) ls = reinterpret_cast<const float2*>(smem + kG256StatRow)[rt];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = acc[i][j];
+        float4 o;
+        if constexpr (kLnf)
+          o = make_float4(ls.y * (v[0] - ls.x * c4[j].x) + b4[j].x, ls.y * (v[1] - ls.x * c4[j].y) + b4[j].y,
+                          ls.y * (v[2] - ls.x * c4[j].z) + b4[j].z, ls.y * (v[3] - ls.x * c4[j].w) + b4[j].w);
+        else
+          o = make_float4(v[0] + b4[j].x, v[1] + b4[j].y, v[2] + b4[j].z, v[3] + b4[j].w);
+        if (kGelu) o = gelu_erf4(o);
+        const int n = n0 + cb + 16 * j;
+        if (m < M && n < N) {
+          const u16x4 hv = {from_f32<T>(o.x), from_f32<T>(o.y), from_f32<T>(o.z), from_f32<T>(o.w)};
+          *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = hv;
+        }
+      }
+    }
+#ifdef WMX_G256_STAMPS
+    if (tid == 0 && tile < kG256Stamps) {
+      g256_stamps[tile][0] = st0;
+      g256_stamps[tile][1] = st1;
+      g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
+      g256_stamps[tile][3] = rt0;
+      g256_stamps[tile][4] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+    __syncthreads();  // the next tile's DMA must not overwrite the ring or the bias stage before every wave left
+    continue;
+  } else if constexpr (kDirect) {
     // LDS-free epilogue: for every (fragment row i, register r) the 16 lanes of a row group hold columns
     // 16 j + fr (j = 0..3) of one output row; a 4 x 4 transpose inside each lane quad (lane-dependent register
     // rotation, three DPP quad rotations, rotation back) leaves lane (fr) with the 4 consecutive columns
@@ -1162,9 +1236,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
       for (int ii = 0; ii < 4; ++ii) {
         const int i = (rd & 1) * 4 + ii;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (kSwapAll) {  // C^T fragment: 4 consecutive columns of row ii 16 + fr, one ds_write_b128
+            *reinterpret_cast<f32x4*>(img + (ii * 16 + fr) * LDT + wn * 64 + j * 16 + 4 * fq) = acc[i][j];
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) img[(ii * 16 + fq * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r) img[(ii * 16 + fq * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
+          }
+        }
       }
     }
     __syncthreads();

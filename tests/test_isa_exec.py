@@ -45,6 +45,8 @@ SCRATCH_ALLOWED = [
     (r"gemm256_kernelILNS_2DTE\dELin1E", "generic-epilogue fallback for N % 4 != 0 (no hot-path shape)"),
     (r"gemm256_kernelILNS_2DTE1ELi11E", "f16 only, 12 bytes"),
     (r"gemm_mx8_256_kernelILNS_2DTE\dELi2E", "MX-fp8 residual epilogue, 3 dwords outside the main loop"),
+    (r"gemm_mx8_256_kernelILNS_2DTE\dELi7E",
+     "MX-fp8 GELU->MX8 on the 128-deep ring: 6 dwords saved at entry, reloaded outside the steady-state K loop"),
     (r"enc_attn_kernelILNS_2DTE\dELi8ELi4E", "one VGPR stored before and reloaded after the key loop"),
     (r"gemm_packed_kernelILNS_2DTE\dELi\dELi\dELi16ELi3E", "RedTail (opt-in WMX_REDLN_FUSED)"),
     (r"dec_cross_attn_kernelILNS_2DTE\dELi[12]ELi\dELb\dELb0E",
