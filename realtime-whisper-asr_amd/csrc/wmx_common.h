@@ -133,8 +133,8 @@ __device__ inline f32x2 gelu_erf2(f32x2 x) {
   p = __builtin_elementwise_fma(p, t, f32x2{0.5f * 0.254829592f, 0.5f * 0.254829592f});
   const f32x2 e2 = x * (x * f32x2{-0.72134752044448170f, -0.72134752044448170f});
   const f32x2 q = p * t * f32x2{__builtin_amdgcn_exp2f(e2.x), __builtin_amdgcn_exp2f(e2.y)};
-  // x Phi(x) = max(x, 0) - |x| q with q = Phi(-|x|): one fma, no sign select
-  return __builtin_elementwise_fma(-ax, q, __builtin_elementwise_max(x, f32x2{0.f, 0.f}));
+  const f32x2 phi = {x.x >= 0.f ? 1.0f - q.x : q.x, x.y >= 0.f ? 1.0f - q.y : q.y};
+  return x * phi;
 }
 __device__ inline float4 gelu_erf4(float4 v) {
   const f32x2 a = gelu_erf2(f32x2{v.x, v.y}), b = gelu_erf2(f32x2{v.z, v.w});
@@ -148,7 +148,7 @@ __device__ inline float gelu_erf(float x) {
   p = fmaf(p, t, 0.5f * -0.284496736f);
   p = fmaf(p, t, 0.5f * 0.254829592f);
   const float q = p * t * __builtin_amdgcn_exp2f(x * (x * -0.72134752044448170f));  // exp(-x^2 / 2)
-  return fmaf(-fabsf(x), q, fmaxf(x, 0.f));  // x Phi(x) = max(x, 0) - |x| Phi(-|x|)
+  return x * (x >= 0.f ? 1.0f - q : q);
 }
 
 // ---- cross-lane reductions on DPP and permlane swaps (VALU latency, no LDS round trip as ds_bpermute has).
