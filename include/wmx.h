@@ -312,6 +312,9 @@ wmx_status wmx_ctx_set_phase_offset(wmx_ctx* c, double us);
  * decoding (WMX_LOCKSTEP_CHUNKS=0: the start barrier only). Every member must call wmx_transcribe concurrently with
  * the others; a member that does not costs the others the timeout once. key 0 leaves the group. */
 wmx_status wmx_ctx_set_lockstep(wmx_ctx* c, int key, int n_members);
+/* chunk barriers of this context that timed out since it was created (the member then leaves the barrier for the
+ * rest of its call): 0 while the group's members arrive together and leave when their decode loops end */
+wmx_status wmx_ctx_lockstep_timeouts(wmx_ctx* c, int64_t* n);
 /* the lockstep barriers alone (host tests, no GPU), group `key` of n members: op 0 = the start barrier (all n),
  * 1 = a chunk barrier (the members still decoding), 2 = leave (this member's decode loop ended); *ok = 1 when every
  * expected member arrived within timeout_us, else 0 (the member leaves that round; the next one starts clean) */

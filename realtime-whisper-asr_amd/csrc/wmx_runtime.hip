@@ -3169,6 +3169,11 @@ wmx_status wmx_ctx_stage_ms(wmx_ctx* x, float* out7) {
 }
 
 int wmx_ctx_last_steps(wmx_ctx* x) { return x->c.last_steps; }
+wmx_status wmx_ctx_lockstep_timeouts(wmx_ctx* x, int64_t* n) {
+  if (!x || !n) return WMX_ERR_ARG;
+  *n = (int64_t)x->c.lockstep_timeouts;
+  return WMX_OK;
+}
 
 // ---- pre-ASR DSP ----
 static void grow_bytes(void** p, size_t& cap, size_t need, size_t elem) {

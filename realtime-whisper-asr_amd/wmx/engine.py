@@ -396,6 +396,13 @@ class Context:
         loops start together (wmx_ctx_set_lockstep)."""
         check(lib.wmx_ctx_set_lockstep(self._h, int(key), int(n_members)))
 
+    @property
+    def lockstep_timeouts(self) -> int:
+        """Chunk barriers of this context that timed out since it was created (wmx_ctx_lockstep_timeouts)."""
+        n = C.c_int64(0)
+        check(lib.wmx_ctx_lockstep_timeouts(self._h, C.byref(n)))
+        return int(n.value)
+
     def probe_ticks(self):
         """(ticks [steps][12][2] uint64 earliest start / latest end per probed launch, wall-clock kHz) of the last
         transcribe (wmx_ctx_probe_ticks; 0 = not recorded)."""

@@ -147,3 +147,30 @@ def test_lockstep_groups_equal_alone_and_a_lone_member_proceeds():
     for c in ctxs:
         c.set_lockstep(0, 0)
     print(f"lone member call {1e3 * dt:.1f} ms")
+
+
+def test_lockstep_member_with_a_shorter_decode_leaves_the_chunk_barrier():
+    """two lockstep contexts whose decode loops have different lengths (8 and 40 steps, word timestamps
+    on, so the short member goes on to the alignment forward and the host DTW while the long one still decodes).  The
+    short member leaves the chunk barrier when its decode loop ends, so the long member meets no chunk-barrier
+    timeout (wmx_ctx_lockstep_timeouts), and both results equal each context run alone."""
+    from wmx import engine as E
+    m = E.Model(_edims(WIDE2), 0, "bfloat16").init_synthetic(8)
+    ctxs = [E.Context(m, max_batch=2, beam_size=5, max_new_tokens=n, language=None, word_timestamps=True,
+                      use_graph=True) for n in (8, 40)]
+    audios = [synth.speech_like(970 + i, 480000) for i in range(4)]
+    batches = [audios[:2], audios[2:]]
+    alone = [ctxs[g].transcribe(batches[g]) for g in range(2)]
+    for c in ctxs:
+        c.set_lockstep(12, 2)
+    before = [c.lockstep_timeouts for c in ctxs]
+    for rep in range(2):
+        both = _run_concurrently(ctxs, batches)
+        for g in range(2):
+            for b in range(2):
+                _same(both[g][b], alone[g][b], f"uneven lockstep rep {rep} group {g} window {b}")
+    after = [c.lockstep_timeouts for c in ctxs]
+    for c in ctxs:
+        c.set_lockstep(0, 0)
+    print("chunk-barrier timeouts before / after", before, after, "steps", [c.last_steps() for c in ctxs])
+    assert after == before, (before, after)
