@@ -328,6 +328,10 @@ __device__ unsigned long long g256_stamps[kG256Stamps][5];  // memtime: start, l
 #ifndef WMX_G256_PRIO
 #define WMX_G256_PRIO 1  // 1: static priority 1 for waves 4..7 only (19.52-19.58 vs 19.81-19.84 ms per encoder pass); 0: s_setprio 1 around every MFMA segment (T5)
 #endif
+#ifndef WMX_G256_GM
+#define WMX_G256_GM 4  // row panels that walk the columns together inside an XCD's tile range (8: qkv alone 5 % faster,
+                       // the encoder pass unchanged within noise, profiles/r05t_g256_gm/)
+#endif
 #ifndef WMX_G256_SWAP
 #define WMX_G256_SWAP 0  // 1: direct-epilogue kinds compute C^T fragments (a lane holds 4 consecutive columns of a row, no
                          // transpose); 2: every kind.  Measured slower (the 32-B row pieces per store), opt-in
@@ -751,7 +755,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   }
   // grouped order inside that range: 4 row panels walk the columns together, so the ~32 tiles an XCD runs at
   // once share 4 A panels and ~8 W panels in its L2 (row-major order shared 2 A panels but 16+ W panels)
-  constexpr int GM = 4;
+  constexpr int GM = WMX_G256_GM;
   const int gsz = GM * tilesN;
   const int grp = bid / gsz, gr = bid - grp * gsz;
   const int gm = min(GM, tilesM - grp * GM);
