@@ -511,13 +511,13 @@ def main():
     roof["frac_isolated_replay"] = round(by / (rep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if rep_ms > 0 else None
     # HBM traffic per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py: FETCH_SIZE x2 +
     # WRITE_SIZE, separate passes) of the same launches replayed alone at this context's batch
-    for tag in ("r04", "r03", "r02", "r01g"):
+    for tag in ("r05", "r04", "r03", "r02", "r01g"):
         pmc = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")
         if not os.path.exists(pmc):
             continue
         recs = json.load(open(pmc))
         # (entries keyed launch@windows-per-group; the fp8 decode's launches carry a /fp8 suffix)
-        sfx = "/fp8" if args.dtype == "fp8" else ""
+        sfx = {"fp8": "/fp8", "int8": "/int8"}.get(args.dtype, "")
         got = [recs.get(f"{replay_id[k]}@{Bg}{sfx}") for k in fams[dom]]
         if all(got):
             tb = sum(g["traffic_bytes"] for g in got)

@@ -52,16 +52,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("kernels", nargs="+")
     ap.add_argument("--batch", type=int, nargs="+", default=[4, 8], help="windows per launch")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05_pmc_traffic.json"))
     ap.add_argument("--dtype", nargs="+", default=["bfloat16"],
-                    help="model dtypes; float8 entries are keyed kernel@batch/fp8 (the 8-bit weights / fp8 images)")
+                    help="model dtypes; float8 entries are keyed kernel@batch/fp8 (the 8-bit weights / fp8 images), "
+                         "int8_float16 ones kernel@batch/int8 (CTranslate2's int8 grid)")
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     args = ap.parse_args()
     res = {}
     if os.path.exists(args.out):  # passes are added to an existing summary (one GPU call per dtype / batch set)
         res = json.load(open(args.out))
     for dt in args.dtype:
-        sfx = "/fp8" if dt == "float8" else ""
+        sfx = "/fp8" if dt == "float8" else "/int8" if dt.startswith("int8") else ""
         for k in args.kernels:
             for b in args.batch:
                 fetch_kb, n1 = run_pass(k, "FETCH_SIZE", args.work, b, dt)
