@@ -328,6 +328,9 @@ __device__ unsigned long long g256_stamps[kG256Stamps][5];  // memtime: start, l
 #ifndef WMX_G256_PRIO
 #define WMX_G256_PRIO 1  // 1: static priority 1 for waves 4..7 only (19.52-19.58 vs 19.81-19.84 ms per encoder pass); 0: s_setprio 1 around every MFMA segment (T5)
 #endif
+#ifndef WMX_G256_LATE1
+#define WMX_G256_LATE1 0  // 1: the 64-deep ring stages unit 1 of K-tile t + 1 in phase 1 instead of phase 0 (A/B)
+#endif
 #ifndef WMX_G256_GM
 #define WMX_G256_GM 4  // row panels that walk the columns together inside an XCD's tile range (8: qkv alone 5 % faster,
                        // the encoder pass unchanged within noise, profiles/r05t_g256_gm/)
@@ -920,9 +923,16 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     const char* U = smem + (t & 1) * 65536;
     read_a(U);  // phase 0: units 0 and 1
     read_b(U + 16384);
+#if WMX_G256_LATE1 == 0
     if (t + 1 < nk) issue_unit(t + 1, 1);
+#endif
     WMX_G256_SEG(0, 0)
     read_b(U + 2 * 16384);  // phase 1: unit 2
+#if WMX_G256_LATE1
+    // unit 1 of K-tile t + 1 issued here instead of in phase 0 (the 12-read segment), ahead of unit 0 of t + 2 so
+    // the phase-3 vmcnt(6) still completes it
+    if (t + 1 < nk) issue_unit(t + 1, 1);
+#endif
     if (t + 2 < nk) issue_unit(t + 2, 0);
     WMX_G256_SEG(0, 1)
     read_a(U + 3 * 16384);  // phase 2: unit 3
