@@ -81,9 +81,39 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="CPU rehearsal of the launch / rendezvous / broadcast / max-over-ranks plumbing (gloo, no GPU)")
     p.add_argument("--no-stream", action="store_true", help="skip the per-stream process_iter latency lines")
-    p.add_argument("--phase-offset-us", type=float, default=0.0,
-                   help="idle offset of context group g's decode loop: g x this many microseconds")
     return p.parse_args()
+
+
+# WMX_* variables a measured line may run under: documented knobs that select a configuration the line then reports
+# (each is recorded in the line's "env").  Anything else named WMX_* is a timing-only or removed experiment switch
+# (WMX_ABLATE dropped launches from the decode step, results wrong by construction; WMX_PHASE_PROBE / _DUMP, WMX_FOLD,
+# WMX_MLP_FUSED, WMX_REDLN_FUSED, WMX_XATTN_* were measured-slower variants, removed in round 6): the bench refuses
+# to print a line under one.
+BENCH_ENV_KNOBS = {
+    "WMX_LIB": "library path (A/B builds)",
+    "WMX_ROOT": "repository root (test harness)",
+    "WMX_LOCKSTEP": "0: the context groups' decode loops start independently",
+    "WMX_LOCKSTEP_CHUNKS": "0: lockstep barrier at the decode start only",
+    "WMX_STREAM_GROUPS": "contexts per batched stream call (stream_load line)",
+    "WMX_DEC_MIXED": "1: the mixed decode step (out / cross-out projections unsplit, LN2 / LN3 folded)",
+    "WMX_DEC_FP8": "0: keep the fp8 model's decode on 16-bit weights",
+    "WMX_ENC_FOLD": "0: encoder LayerNorms as their own launches",
+    "WMX_XQ_FUSED": "0: the cross-q projection as its own split-K launch",
+    "WMX_CROSS_CHUNK": "decode cross-attention key chunk",
+    "WMX_SILERO_WEIGHTS": "Silero v5 safetensors path (VAD line)",
+}
+
+
+def check_env():
+    """The WMX_* environment of this run: returns it (recorded in the line); exits with status 2 and no line when a
+    variable outside BENCH_ENV_KNOBS is set."""
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("WMX_")}
+    bad = [k for k in env if k not in BENCH_ENV_KNOBS]
+    if bad:
+        log(f"bench.py: refusing to measure under timing-only / unknown switches {bad}: a line measured under them "
+            f"is not the product path (documented knobs: {sorted(BENCH_ENV_KNOBS)})")
+        sys.exit(2)
+    return env
 
 
 def _cpu_sample(W, d, args, steps_done, n_text):
@@ -269,8 +299,6 @@ def stream_load(name, dtype, n_per_gpu, seconds, max_new_tokens, world=1, rank=0
     out = SL.summarize(parts)
     out.update({"model": f"whisper-{name}", "dtype": dtype, "audio_s_per_stream": seconds,
                 "streams_per_gpu": n_per_gpu,
-                "per_rank_p50_ms": [round(1000 * float(np.median([dt for _, _, dt in p["lat"]])), 2) if p["lat"] else None
-                                    for p in parts],
                 "feed": "VAC (1 s online chunks, scripted VAD track), 0.5 s per tick, streams staggered by one tick; "
                         "one batched transcribe per tick per rank over its due streams (StreamBatcher); streams sharded "
                         "over ranks (wmx.dist.shard_streams), records and latencies gathered to rank 0",
@@ -348,6 +376,7 @@ def dry_run(args):
 
 def main():
     args = parse()
+    wmx_env = check_env()
     from wmx import dist as D
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `bench.py --gpus N` outside torch.distributed.run: start N rank processes here, before any torch / HIP
@@ -421,7 +450,6 @@ def main():
     probe_layer = model.dims.n_text_layer // 2
     for g, c in enumerate(ctxs):
         c.set_probe(True, probe_layer)
-        c.set_phase_offset(g * args.phase_offset_us)
     for _ in range(args.warmup):
         step()
     if dist is not None:
@@ -442,9 +470,6 @@ def main():
         elapsed = D.max_over_ranks(elapsed, device=f"cuda:{local}")
     stages = ctx.stage_ms()
     steps_done = ctx.last_steps()
-    if os.environ.get("WMX_PHASE_PROBE") == "1" and os.environ.get("WMX_PHASE_DUMP"):  # diagnostics only
-        ph = [c.probe_phases() for c in ctxs]
-        np.savez(os.environ["WMX_PHASE_DUMP"], **{f"g{g}": p[0] for g, p in enumerate(ph)}, khz=ph[0][1])
     n_tok = [len(r.tokens) for r in res]
     log(f"[rank {rank}] stage ms (logmel, enc, xkv, lang, prefill, decode, align): "
         f"{[round(s, 2) for s in stages]}  decode steps {steps_done}  tokens/window {n_tok}")
@@ -651,6 +676,7 @@ def main():
                    "parallelism": f"dp{world} (independent streams)", "decode_steps": steps_done,
                    "use_graph": not args.no_graph, "context_groups": G},
         "stage_ms": [round(s, 2) for s in stages],
+        "env": wmx_env,
         "decode_mode": decode_mode,
         "lockstep": lockstep,
         "roofline": roof,

@@ -14,9 +14,6 @@
 #include "wmx_common.h"
 #include "wmx_kernels.h"
 
-#ifndef WMX_ATTN_PRIO
-#define WMX_ATTN_PRIO 0  // encoder attention: static s_setprio 1 for waves 4..7 (A/B switch)
-#endif
 
 namespace wmx {
 
@@ -304,11 +301,6 @@ __global__ __launch_bounds__(64 * NWV, MINW) void enc_attn_kernel(AttnArgs a) {
     }
   };
   stage(0, 0);
-#if WMX_ATTN_PRIO
-  // static priority for the second-dispatched half of an 8-wave workgroup (MI355X_MICROARCH.md "two waves per SIMD"
-  // item 4): it is the arbitration loser of every segment otherwise
-  if (NWV == 8 && __builtin_amdgcn_readfirstlane(wave) >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
 
   // Q^T fragments (B operand): lane holds Q[q0 + c][16s + 8hl .. +8] for dim steps s = 0..3, pre-scaled by
   // C = log2(e) / sqrt(64) and rounded once to T, so the MFMA produces scores in log2 units directly (the
@@ -480,29 +472,17 @@ __global__ __launch_bounds__(64 * NWV, MINW) void enc_attn_kernel(AttnArgs a) {
 }
 
 void launch_attn_encoder(DT dt, const AttnArgs& a, hipStream_t st) {
-  static const bool legacy = getenv("WMX_ENC_ATTN_LEGACY") != nullptr;  // A/B switch for tuning runs
-  if (!a.o8 && (legacy || a.head_stride % 8 != 0 || a.k_ld % 8 != 0 || a.v_ld % 8 != 0 || a.q_ld % 8 != 0 ||
+  if (!a.o8 && (a.head_stride % 8 != 0 || a.k_ld % 8 != 0 || a.v_ld % 8 != 0 || a.q_ld % 8 != 0 ||
                 a.kv_head_stride != 0)) {
     launch_attn_flash(dt, a, 0, 0, nullptr, st);
     return;
   }
-  // A/B switch (WMX_ENC_ATTN): 4 = 4-wave (128-query) workgroups, 82 = 8 waves at <= 256 VGPRs (one workgroup
-  // per CU), default 8 waves at <= 128 VGPRs (two per CU)
-  static const int form = getenv("WMX_ENC_ATTN") ? atoi(getenv("WMX_ENC_ATTN")) : 8;
+  // 8 waves at <= 128 VGPRs (two workgroups per CU); the 4-wave and the 256-VGPR forms measured no faster (round 5,
+  // profiles/r05v_attn_form_ab/) and were removed
   const bool bf = dt == DT::BF16;
-  if (form == 4) {
-    dim3 grid(cdiv(a.Tq, 128) * a.H * a.B);
-    if (bf) hipLaunchKernelGGL((enc_attn_kernel<DT::BF16, 4, 2>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((enc_attn_kernel<DT::F16, 4, 2>), grid, dim3(256), 0, st, a);
-  } else if (form == 82) {
-    dim3 grid(cdiv(a.Tq, 256) * a.H * a.B);
-    if (bf) hipLaunchKernelGGL((enc_attn_kernel<DT::BF16, 8, 2>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((enc_attn_kernel<DT::F16, 8, 2>), grid, dim3(512), 0, st, a);
-  } else {
-    dim3 grid(cdiv(a.Tq, 256) * a.H * a.B);
-    if (bf) hipLaunchKernelGGL((enc_attn_kernel<DT::BF16, 8, 4>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((enc_attn_kernel<DT::F16, 8, 4>), grid, dim3(512), 0, st, a);
-  }
+  dim3 grid(cdiv(a.Tq, 256) * a.H * a.B);
+  if (bf) hipLaunchKernelGGL((enc_attn_kernel<DT::BF16, 8, 4>), grid, dim3(512), 0, st, a);
+  else hipLaunchKernelGGL((enc_attn_kernel<DT::F16, 8, 4>), grid, dim3(512), 0, st, a);
   WMX_HIP(hipGetLastError());
 }
 
@@ -700,33 +680,12 @@ inline long cross_records_floats(int H, int nwin, int nq, int KS) { return (long
 // query projection's weights are 8-bit too (packed8_index, per-row scales a.wq_scale)
 // FQ (with XQ): LN2 folded into the fused query projection (the mixed step); its own instantiation, so the default
 // fused kernel does not carry the statistics registers (at the 128-VGPR cap of 4 waves per SIMD they spilled)
-// WPW = 2 (round 5, decode with the fused query projection): one workgroup per (head, window PAIR, key chunk) instead of
-// (head, window, key chunk): the two windows' query rows (2 nq <= 16) share one 16-row projection tile, so each
-// workgroup streams the head's query weights once for two windows, waves 0 .. NWV/2 - 1 take the first window's keys of
-// the chunk and the rest the second's, and the grid halves for the same key chunk per wave.  With the two context
-// groups in step, 2 x 160 workgroups of the (head, window) form (one per CU at this kernel's ~217 VGPRs) ran as 1.25
-// rounds over the 256 CUs: the last 64 started when the first finished (phase stamps, tools/xattn_phases.py, r05b);
-// 2 x 120 of the pair form (512-key chunks: 3 per window) run as one round.
-template <DT T, int KPW, int NWV, bool XQ = false, bool F8 = false, bool FQ = false, int WPW = 1>
+// (Round 5 measured and removed: window pairs per workgroup, an XCD remap of the heads, a barrier ordering the
+// projection loads before the K loads, and the chunk records merged in the cross out-projection)
+template <DT T, int KPW, int NWV, bool XQ = false, bool F8 = false, bool FQ = false>
 __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cross_attn_kernel(DecAttnArgs a, int KS, int chunk, float* __restrict__ part) {
   constexpr int NT = 64 * NWV;
-  static_assert(WPW == 1 || (WPW == 2 && XQ && !F8 && !FQ && NWV % 2 == 0), "window pairs: the fused 16-bit decode form");
-  constexpr int WVW = NWV / WPW;  // waves per window
-  int h = blockIdx.x, w = blockIdx.y, zz = blockIdx.z;  // (WPW = 2: w = window pair)
-  if (a.xcd_remap) {
-    // workgroups are dispatched round-robin over the 8 XCDs by linear id; this bijection gives each XCD a run of
-    // consecutive (head-major) work items, so the windows and key chunks of one head -- which all stream that head's
-    // query-projection weights -- share one or two XCDs' L2 instead of pulling the slice into up to eight
-    const int N = gridDim.x * gridDim.y * gridDim.z;
-    const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    const int qn = N >> 3, rn = N & 7, xcd = L & 7, j = L >> 3;
-    const int g = xcd < rn ? xcd * (qn + 1) + j : rn * (qn + 1) + (xcd - rn) * qn + j;
-    const int per_h = gridDim.y * gridDim.z;
-    h = g / per_h;
-    const int rem = g - h * per_h;
-    w = rem / gridDim.z;
-    zz = rem - w * gridDim.z;
-  }
+  const int h = blockIdx.x, w = blockIdx.y, zz = blockIdx.z;
   const int ks = zz % KS, qt = zz / KS;
   // wave index as a scalar: the K / V buffer loads below take their block offsets in the scalar soffset operand, and
   // a wave index the compiler cannot prove uniform turns every one of them into a readfirstlane waterfall loop
@@ -735,39 +694,19 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const int nq = a.rows_per_win * a.Tn;
   // in-situ probe: this workgroup's start / end, device wall-clock ticks
   const unsigned long long probe_t0 = (a.tprobe && tid == 0) ? probe_clock() : 0ull;
-  // diagnostic phase stamps (a.pphase): wave 0 reads the clock at each phase boundary, lane 0 stores them at the end
-  const bool pp = a.pphase != nullptr && wave == 0;
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (pp) ph[0] = probe_clock();
   auto probe_end = [&] {
     if (a.tprobe && tid == 0) probe_record(a.tprobe, *a.slot0, probe_t0);
-    if (pp) {
-      ph[7] = probe_clock();
-      const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-      if (lane == 0 && wg < kProbeWG) {
-        unsigned long long* o = a.pphase + ((long)*a.slot0 * kProbeWG + wg) * kPhaseStamps;
-        const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
-        const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
-#pragma unroll
-        for (int i = 0; i < 8; i += 2) *reinterpret_cast<ulonglong2*>(o + i) = make_ulonglong2(ph[i], ph[i + 1]);
-        *reinterpret_cast<ulonglong2*>(o + 8) = make_ulonglong2(xcc, hw);
-      }
-    }
   };
-  const int i0 = qt * 16;  // first query (within the window) of this tile (WPW = 2: one tile, i0 = 0)
+  const int i0 = qt * 16;  // first query (within the window) of this tile
   const int nqt = min(16, nq - i0);
-  // the workgroup's first window, this wave's window (wsub within the group) and its index among that window's waves
-  const int w0 = w * WPW, wsub = wave / WVW, wabs = w0 + wsub, wq_ = wave - wsub * WVW;
-  // the projection tile's rows: WPW = 1 queries i0 .. i0 + nqt of window w; WPW = 2 the nq queries of window w0 then
-  // those of w0 + 1 (rows w0 nq .. w0 nq + 2 nq of qin, contiguous)
-  const int trows = WPW == 1 ? nqt : WPW * nq;
-  const long row0 = (long)w0 * nq + i0;
+  const int trows = nqt;  // the projection tile's rows: queries i0 .. i0 + nqt of window w
+  const long row0 = (long)w * nq + i0;
   const int kc0 = ks * chunk, kc1 = min(a.Tk, kc0 + chunk);
-  const int per = ((kc1 - kc0 + WVW - 1) / WVW + 31) / 32 * 32;  // keys per wave, whole 32-key blocks
-  const int kw0 = kc0 + wq_ * per, kw1 = min(kc1, kw0 + per);
+  const int per = ((kc1 - kc0 + NWV - 1) / NWV + 31) / 32 * 32;  // keys per wave, whole 32-key blocks
+  const int kw0 = kc0 + wave * per, kw1 = min(kc1, kw0 + per);
   constexpr int EB = F8 ? 1 : 2;  // image element bytes
-  const char* kbase = reinterpret_cast<const char*>(a.ck) + ((long)wabs * a.x_wstride + (long)h * a.x_hstride) * EB;
-  const char* vbase = reinterpret_cast<const char*>(a.cv) + ((long)wabs * a.x_wstride + (long)h * a.x_hstride) * EB;
+  const char* kbase = reinterpret_cast<const char*>(a.ck) + ((long)w * a.x_wstride + (long)h * a.x_hstride) * EB;
+  const char* vbase = reinterpret_cast<const char*>(a.cv) + ((long)w * a.x_wstride + (long)h * a.x_hstride) * EB;
   // fp8 images: their scales (scalar loads, issued first; read-only in this launch)
   float ksc = 1.f, vsc = 1.f;
   if constexpr (F8) {
@@ -855,7 +794,6 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   // (fused path: unconditional -- a wave without keys reads past the image, zeros by the descriptor's range, and
   // never uses them; a conditional batch would make the compiler's waits for the projection's loads count as if
   // the K loads had not been issued, i.e. wait for them too)
-  if (fuse_q && a.issue_bar) __builtin_amdgcn_s_barrier();  // (wave-uniform argument; no memory wait)
   if (fuse_q)
     load_k(kw0);
   else if (kw0 < kw1)
@@ -894,7 +832,6 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) so[wave][4 * g + r][16 * j + fr] = qa[j][r];
-    if (pp) ph[1] = probe_clock();
     load_v(kw0);
     __syncthreads();
   }
@@ -949,10 +886,8 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     qsh[q][e] = v;
   }
   __syncthreads();
-  if (pp) ph[2] = probe_clock();
   // Q^T B-fragments: lane (col q = fr, g): dims 32hh + 8g .. +8
-  // (WPW = 2: the wave's window's rows wsub nq .. +nq; lanes past nq repeat its last query, columns never stored)
-  const int qrow = WPW == 1 ? fr : wsub * nq + min(fr, nq - 1);
+  const int qrow = fr;
   u16x8 qb[2];
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) qb[hh] = *reinterpret_cast<const u16x8*>(&qsh[qrow][32 * hh + 8 * g]);
@@ -993,7 +928,6 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
       for (int j = 0; j < 8; ++j) mx = fmaxf(mx, sv[b][j]);
     mx = max_xor32(max_xor16(mx));
-    if (pp && kb0 == kw0) ph[3] = probe_clock();
     const float m_new = fmaxf(m_run, mx);
     float ls = 0.f;
 #pragma unroll
@@ -1050,12 +984,6 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 
   // ---- combine the NWV waves (LDS), then output or a chunk record ----
   __shared__ float sm[NWV][16], sl[NWV][16];
-  if (pp) {  // (the P.V results are in registers once o is read)
-    float z = 0.f;
-#pragma unroll
-    for (int db = 0; db < 4; ++db) z += o[db][0];
-    ph[4] = probe_clock() + (z == 12345.678f ? 1 : 0);
-  }
   if (g == 0) {
     sm[wave][fr] = m_run;
     sl[wave][fr] = l_run;
@@ -1065,30 +993,24 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
     for (int r = 0; r < 4; ++r) so[wave][4 * g + r][16 * db + fr] = o[db][r];
   __syncthreads();
-  if (pp) ph[5] = probe_clock();
-  for (int t = tid; t < WPW * nqt * 64; t += NT) {
-    const int qi = t >> 6, e = t & 63;
-    const int ww = WPW == 1 ? 0 : qi / nqt, q = WPW == 1 ? qi : qi - ww * nqt;  // (window of the group, query)
-    const int v0 = ww * WVW;  // that window's waves
-    float M = sm[v0][q];
+  for (int t = tid; t < nqt * 64; t += NT) {
+    const int q = t >> 6, e = t & 63;
+    float M = sm[0][q];
 #pragma unroll
-    for (int wv = 1; wv < WVW; ++wv) M = fmaxf(M, sm[v0 + wv][q]);
+    for (int wv = 1; wv < NWV; ++wv) M = fmaxf(M, sm[wv][q]);
     float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int wv = 0; wv < WVW; ++wv) {
-      const float f = sm[v0 + wv][q] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sm[v0 + wv][q] - M);
-      L += sl[v0 + wv][q] * f;
-      O += so[v0 + wv][q][e] * f;
+    for (int wv = 0; wv < NWV; ++wv) {
+      const float f = sm[wv][q] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sm[wv][q] - M);
+      L += sl[wv][q] * f;
+      O += so[wv][q][e] * f;
     }
-    const long row = (long)(w0 + ww) * nq + i0 + q;
+    const long row = (long)w * nq + i0 + q;
     if (KS == 1) {
       a.o[row * a.d + h * 64 + e] = from_f32<T>(O / L * vsc);
-    } else if (a.rec_o) {  // records for the consumer's merge (KS == 2; plain stores, the kernel boundary publishes)
-      a.rec_o[((long)ks * a.R + row) * a.d + h * 64 + e] = O;
-      if (e == 0) a.rec_ml[((long)ks * a.R + row) * a.H + h] = make_float2(M, L);
     } else {
       // chunk record, stored write-through (sc1) so the last arriver can read it without an L2 release
-      gf32* pr = (gf32*)(part + (((long)((w0 + ww) * a.H + h) * KS + ks) * nq + i0 + q) * 66);
+      gf32* pr = (gf32*)(part + (((long)(w * a.H + h) * KS + ks) * nq + i0 + q) * 66);
       if (e == 0) {
         __hip_atomic_store(pr, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(pr + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1096,7 +1018,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
       __hip_atomic_store(pr + 2 + e, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (KS == 1 || a.rec_o) {
+  if (KS == 1) {
     probe_end();
     return;
   }
@@ -1105,32 +1027,27 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   //      order with sc1 loads (no acquire fence needed) and re-arms the counter for the next launch ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int* cnt = a.xcnt;  // (WPW = 2: the counter of the pair's first window)
+  int* cnt = a.xcnt;
   if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(cnt + w0 * a.H + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int old = __hip_atomic_fetch_add(cnt + w * a.H + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sm[0][0] = old == KS - 1 ? 1.f : 0.f;
   }
   __syncthreads();
-  if (pp) ph[6] = probe_clock();
   if (sm[0][0] == 0.f) {
     probe_end();
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // every record load is a buffer load with sc1 (aux 16): it bypasses this CU's L1, so no acquire is needed
-  // (WPW = 2: one descriptor over both windows' records of head h, [w0][h] .. [w0 + 1][h])
-  const float* wh = part + (long)(w0 * a.H + h) * KS * nq * 66;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)wh, (short)0,
-                                                      ((WPW - 1) * a.H + 1) * KS * nq * 66 * 4, 0x00020000);
-  for (int t = tid; t < WPW * nq * 64; t += NT) {
-    const int qi = t >> 6, e = t & 63;
-    const int ww = WPW == 1 ? 0 : qi / nq, q = WPW == 1 ? qi : qi - ww * nq;
-    const int wrec = ww * a.H * KS * nq * 66;  // floats from window w0's records to window w0 + ww's (same head)
+  const float* wh = part + (long)(w * a.H + h) * KS * nq * 66;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)wh, (short)0, KS * nq * 66 * 4, 0x00020000);
+  for (int t = tid; t < nq * 64; t += NT) {
+    const int q = t >> 6, e = t & 63;
     float rec[kMaxSplits][3];
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
-        const int off = (wrec + (k * nq + q) * 66) * 4;
+        const int off = ((k * nq + q) * 66) * 4;
         rec[k][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 16));
         rec[k][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 16));
         rec[k][2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off + (2 + e) * 4, 0, 16));
@@ -1144,15 +1061,14 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
 #pragma unroll
     for (int k = 0; k < kMaxSplits; ++k) {
       if (k < KS) {
-        // (explicit fmas: the cross out-projection's record-merge A loads repeat this sum bit for bit)
         const float sc2 = rec[k][0] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(rec[k][0] - M);
         l = __builtin_fmaf(rec[k][1], sc2, l);
         o2 = __builtin_fmaf(rec[k][2], sc2, o2);
       }
     }
-    a.o[((long)(w0 + ww) * nq + q) * a.d + h * 64 + e] = from_f32<T>(o2 / l * vsc);
+    a.o[((long)w * nq + q) * a.d + h * 64 + e] = from_f32<T>(o2 / l * vsc);
   }
-  if (tid == 0) __hip_atomic_store(cnt + w0 * a.H + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(cnt + w * a.H + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   probe_end();
 }
 
@@ -1172,27 +1088,12 @@ static int cross_chunk(int Tk, int nq, bool f8) {
   return f8 ? 512 : 1024;
 }
 
-// the key chunks launch_cross_attn will use for a decode step of these arguments (the pair form aside)
-int cross_attn_key_chunks(const DecAttnArgs& a) {
-  const int nq = a.rows_per_win * a.Tn;
-  const int chunk = std::min(cross_chunk(a.Tk, nq, a.ck_scale != nullptr), a.Tk);
-  return (a.Tk + chunk - 1) / chunk;
-}
-
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max) {
   return (size_t)cross_records_floats(H, nwin, nq_max, kMaxSplits);
 }
 
 template <DT T, bool F8>
-static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
-  DecAttnArgs a = a0;
-  static const int remap = [] {  // WMX_XATTN_REMAP=0/1: A/B switch of the head-per-XCD placement
-    const char* v = getenv("WMX_XATTN_REMAP");
-    return v ? atoi(v) : 0;
-  }();
-  a.xcd_remap = remap && a.wq != nullptr;
-  static const int issue_bar = getenv("WMX_XATTN_ISSUE_BAR") ? atoi(getenv("WMX_XATTN_ISSUE_BAR")) : 0;
-  a.issue_bar = issue_bar;
+static void launch_cross_t(const DecAttnArgs& a, float* ws, hipStream_t st) {
   const int nq = a.rows_per_win * a.Tn;
   const int nwin = a.R / a.rows_per_win;
   const int chunk = std::min(cross_chunk(a.Tk, nq, F8), a.Tk);
@@ -1201,40 +1102,12 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
   WMX_CHECK(KS <= kMaxSplits, "cross attn: too many key chunks");
   WMX_CHECK(KS == 1 || chunk % 32 == 0, "cross attn: key chunks must be whole 32-key blocks");
   WMX_CHECK(KS == 1 || (ws != nullptr && a.xcnt != nullptr && nq <= 16), "cross attn: split workspace required");
-  WMX_CHECK(!a.rec_o || (KS == 2 && a.rec_ml && !F8 && a.Tn == 1), "cross attn: consumer-merged records need 2 key chunks");
   dim3 grid(a.H, nwin, KS * QT);
-  // decode: 8 waves per workgroup (a 1024-key chunk is one 128-key batch per wave); WMX_XATTN_WAVES=4 for tuning
-  static const int waves = [] {
-    const char* v = getenv("WMX_XATTN_WAVES");
-    return v && atoi(v) == 4 ? 4 : 8;
-  }();
+  // decode (nq <= 16): 8 waves per workgroup (a 1024-key chunk is one 128-key batch per wave); prefill: 4 waves
   // the fused query projection holds a wave's whole K share (<= 5 k-steps) in one load batch
   WMX_CHECK(!a.wq || (F8 ? (a.d / 64 + 7) / 8 <= 3 : (a.d / 32 + 7) / 8 <= 5),
             "cross attn: fused query projection: model width too large for one load batch per wave");
-  WMX_CHECK(!a.wq || (waves == 8 && nq <= 16), "cross attn: the fused query projection runs on the 8-wave decode kernel");
-  // window pairs (WPW = 2, round 5): the fused 16-bit decode form when the windows pair up in one 16-row tile
-  // measured slower with the groups in step (r05c: 391.5 / 392.1x against 413.4 / 413.2x): the two groups' K / V
-  // streams then start together and saturate HBM together (19.1 us for both against the (head, window) form's
-  // naturally staggered 14.7 / 24.3 us ends), so it is opt-in (WMX_XATTN_PAIRS=1)
-  static const bool pairs_on = getenv("WMX_XATTN_PAIRS") && atoi(getenv("WMX_XATTN_PAIRS")) == 1;
-  if (a.wq && !F8 && !a.ln_c1 && pairs_on && nwin % 2 == 0 && 2 * nq <= 16 && QT == 1) {
-    static const int env_chunk = getenv("WMX_CROSS_CHUNK") ? atoi(getenv("WMX_CROSS_CHUNK")) : 0;
-    // 512-key chunks: 3 per window, 4 waves per window and chunk = 128 keys (4 blocks) per wave, as the (head,
-    // window) form's 1024-key chunks over 8 waves; 20 heads x 2 pairs x 3 = 120 workgroups per 4-window group
-    const int pchunk = std::min(env_chunk > 0 ? env_chunk : 512, a.Tk);
-    const int pKS = (a.Tk + pchunk - 1) / pchunk;
-    WMX_CHECK(!a.rec_o, "cross attn (pairs): no consumer-merged records");
-    WMX_CHECK(pKS <= kMaxSplits && (pKS == 1 || pchunk % 32 == 0), "cross attn (pairs): key chunks");
-    dim3 pgrid(a.H, nwin / 2, pKS);
-    const int per_wave = ((pchunk + 3) / 4 + 31) / 32;
-    switch (std::min(per_wave, 4)) {
-      case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8, true, false, false, 2>), pgrid, dim3(512), 0, st, a, pKS, pchunk, ws); break;
-      case 2: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 2, 8, true, false, false, 2>), pgrid, dim3(512), 0, st, a, pKS, pchunk, ws); break;
-      case 3: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 3, 8, true, false, false, 2>), pgrid, dim3(512), 0, st, a, pKS, pchunk, ws); break;
-      default: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 4, 8, true, false, false, 2>), pgrid, dim3(512), 0, st, a, pKS, pchunk, ws); break;
-    }
-    return;
-  }
+  WMX_CHECK(!a.wq || nq <= 16, "cross attn: the fused query projection runs on the 8-wave decode kernel");
   if (a.wq) {
     const int per_wave = ((chunk + 7) / 8 + 31) / 32;
     const bool fq = a.ln_c1 != nullptr;  // (16-bit only: launch_cross_attn's check)
@@ -1255,7 +1128,7 @@ static void launch_cross_t(const DecAttnArgs& a0, float* ws, hipStream_t st) {
 #undef WMX_XQ_LAUNCH
     return;
   }
-  if (waves == 8 && nq <= 16) {
+  if (nq <= 16) {
     const int per_wave = ((chunk + 7) / 8 + 31) / 32;
     switch (std::min(per_wave, 4)) {
       case 1: hipLaunchKernelGGL((dec_cross_attn_kernel<T, 1, 8, false, F8>), grid, dim3(512), 0, st, a, KS, chunk, ws); break;

@@ -323,8 +323,6 @@ __device__ inline float max8_lanes(float v) {
 // takes the min start / max end over the workgroups of a slot after the timed region
 constexpr int kProbeWG = 512;
 __device__ inline unsigned long long probe_clock() { return __builtin_amdgcn_s_memrealtime(); }
-// phase stamps per workgroup (DecAttnArgs::pphase): 8 wall-clock ticks + XCC_ID + HW_ID
-constexpr int kPhaseStamps = 10;
 __device__ inline void probe_record(unsigned long long* base, int slot, unsigned long long t0) {
   const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   if (wg < kProbeWG) {

@@ -295,106 +295,28 @@ __global__ __launch_bounds__(WM* WN * 64) void gemm_kernel(const uint16_t* __res
 
 // ------------------------------------------------------------------------------------------------
 // Large-M GEMM (encoder projections, conv front end, cross-K/V): 256 x 256 tile, 8 waves (2 M x 4 N, wave tile
-// 128 x 64 = 8 x 4 MFMA fragments), K staged in 32-deep slices through a 4-slot LDS ring (32 KiB per slot) filled
-// by global_load_lds_dwordx4.  Up to three slices stay in flight across raw s_barriers: each slice is waited
-// for with a COUNTED vmcnt (cdna_hip_programming.md §5 "Pipelining across barriers"), never vmcnt(0) and never
-// __syncthreads() inside the loop.  All LDS is one extern array (§5 item 4(a)).
-// Default (WMX_G256_BK = 64, wmx_kernels.h): the half-tile ring below the staging comment, whole 128-B lines per
-// row and K-tile; TCP -> L2 read requests halve against the 32-deep ring (qkv 13.8 M -> 7.2 M per launch) and the
-// main loop takes 23 % fewer clocks (tools/mb_gemm256, profiles/r05h_g256_k64/).  The 32-deep ring (BK = 32):
-// LDS rows are 64 B (32 k); the 16-B piece p of row r sits at p ^ sw(r), sw(r) = (-(r >> 2)) & 3.  gfx950 serves a
-// ds_read_b128 in four 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59},
-// {36-43,48-51,60-63} (MI355X_MICROARCH.md, LDS table); with fragment lane (r = l & 15, p = l >> 4) this swizzle
-// gives every group 16 distinct (r mod 4, position) pairs = all 64 banks once.  (p ^ ((r >> 2) & 3), the
-// "obvious" form, is 2-way conflicted under that grouping: SQ_LDS_BANK_CONFLICT 3.3x SQ_INSTS_LDS.)  The swizzle
-// is applied on the global SOURCE address; the LDS image stays lane-linear (rule 21).
+// 128 x 64 = 8 x 4 MFMA fragments), K staged in 64-deep K-tiles (whole 128-B lines per row) through a half-tile LDS
+// ring filled by global_load_lds_dwordx4 (the layout and schedule at the ring below).  Each K-tile is waited for with
+// a COUNTED vmcnt (cdna_hip_programming.md §5 "Pipelining across barriers"), never vmcnt(0) in steady state and never
+// __syncthreads() inside the loop.  All LDS is one extern array (§5 item 4(a)).  Against the 32-deep slice ring of
+// rounds 2-4 (every 128-B line fetched in two halves one slice apart) TCP -> L2 read requests halve (qkv 13.8 M ->
+// 7.2 M per launch) and the main loop takes 23 % fewer clocks (profiles/r05h_g256_k64/).
+// Measured and removed in round 6: C^T fragments for the direct epilogues, unit 1 staged one phase
+// later, 8 row panels per XCD group, one 32-MFMA segment per slice, per-segment s_setprio.
 // ------------------------------------------------------------------------------------------------
-// microbenchmark ablations (tools/mb_gemm256.hip): 1 = no MFMA, 2 = no DMA; the library builds mode 0
-#ifndef WMX_G256_MODE
-#define WMX_G256_MODE 0
-#endif
-#if WMX_G256_MODE == 1
-#define WMX_G256_MFMA(a, b, c) ((c) + __builtin_bit_cast(f32x4, (a) ^ (b)))
-#else
 #define WMX_G256_MFMA(a, b, c) mfma16<T>(a, b, c)
-#endif
-#ifdef WMX_G256_STAMPS
-constexpr int kG256Stamps = 16384;
-__device__ unsigned long long g256_stamps[kG256Stamps][5];  // memtime: start, loop end, end; memrealtime: start, end
-#endif
-#ifndef WMX_G256_PHASES
-#define WMX_G256_PHASES 2  // barrier-separated MFMA segments per 32-deep slice (1: one 32-MFMA segment per slice)
-#endif
-#ifndef WMX_G256_PRIO
-#define WMX_G256_PRIO 1  // 1: static priority 1 for waves 4..7 only (19.52-19.58 vs 19.81-19.84 ms per encoder pass); 0: s_setprio 1 around every MFMA segment (T5)
-#endif
-#ifndef WMX_G256_LATE1
-#define WMX_G256_LATE1 0  // 1: the 64-deep ring stages unit 1 of K-tile t + 1 in phase 1 instead of phase 0 (A/B)
-#endif
-#ifndef WMX_G256_GM
-#define WMX_G256_GM 4  // row panels that walk the columns together inside an XCD's tile range (8: qkv alone 5 % faster,
-                       // the encoder pass unchanged within noise, profiles/r05t_g256_gm/)
-#endif
-#ifndef WMX_G256_SWAP
-#define WMX_G256_SWAP 0  // 1: direct-epilogue kinds compute C^T fragments (a lane holds 4 consecutive columns of a row, no
-                         // transpose); 2: every kind.  Measured slower (the 32-B row pieces per store), opt-in
-#endif
-#ifndef WMX_G256_PIN_SEGMENTS
-#define WMX_G256_PIN_SEGMENTS 1  // a scheduling barrier after each segment's opening s_barrier (0: the compiler hoists
-                                 // the segment's first MFMA above it, into the partner's compute segment)
-#endif
-#if WMX_G256_PIN_SEGMENTS
+// a scheduling barrier after each segment's opening s_barrier (without it the compiler hoists the segment's first
+// MFMA above the barrier, into the partner's compute segment)
 #define WMX_G256_PIN __builtin_amdgcn_sched_barrier(0)
-#else
-#define WMX_G256_PIN (void)0
-#endif
-#if WMX_G256_PRIO == 0
-#define WMX_G256_PRIO_ON __builtin_amdgcn_s_setprio(1)
-#define WMX_G256_PRIO_OFF __builtin_amdgcn_s_setprio(0)
-#else
-#define WMX_G256_PRIO_ON (void)0
-#define WMX_G256_PRIO_OFF (void)0
-#endif
-#ifndef WMX_G256_DIRECT
-#define WMX_G256_DIRECT 1  // LDS-free epilogue for the bf16-output kinds (0: the LDS-image epilogue for all)
-#endif
-constexpr int kG256Slot = (256 + 256) * 64;  // bytes per ring slot
+constexpr int kG256Slot = (256 + 256) * 64;  // 32 KiB
 // 128 KiB ring + the LayerNorm-folded kinds' raw row statistics [8 groups][256 rows] float2 and merged (mean, rstd)
 constexpr int kG256StatRaw = 4 * kG256Slot, kG256StatRow = kG256StatRaw + 8 * 256 * 8;
 constexpr int kG256Lds = kG256StatRow + 256 * 8;
-constexpr int kG256Bias = kG256Lds;  // the swapped direct epilogue's tile bias (c2) and c1 columns, [2][256] fp32
-#ifndef WMX_G256_SLOTS
-#define WMX_G256_SLOTS 5  // ring slots of the kinds without the LayerNorm-folded statistics (5 = 160 KiB; 4 slots measured 0.6 % slower)
-#endif
 template <int KIND>
 constexpr bool g256_lnf() { return KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GELU16; }
 template <int KIND>
-constexpr int g256_slots() { return (g256_lnf<KIND>() || WMX_G256_PHASES == 1) ? 4 : WMX_G256_SLOTS; }
-template <int KIND>
-constexpr bool g256_swap() {  // the direct-epilogue kinds on the 64-deep ring compute C^T tiles (WMX_G256_SWAP)
-  return WMX_G256_SWAP && WMX_G256_BK == 64 &&
-         (KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GELU16 ||
-          (WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16)));
-}
-template <int KIND>
-constexpr int g256_lds() {
-  return g256_swap<KIND>() ? kG256Bias + 2048
-                           : g256_lnf<KIND>() ? kG256Lds : (WMX_G256_BK == 64 ? 4 : g256_slots<KIND>()) * kG256Slot;
-}
-static_assert(5 * kG256Slot <= 163840 && kG256Bias + 2048 <= 163840, "gemm256 LDS");
-// s_waitcnt vmcnt(n) for a runtime n in {0, 2, ..., 14} (uniform): the count must be an immediate
-__device__ inline void vmcnt_even(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-  }
-}
+constexpr int g256_lds() { return g256_lnf<KIND>() ? kG256Lds : 4 * kG256Slot; }
+static_assert(kG256Lds <= 163840, "gemm256 LDS");
 
 // apply the epilogue to `rows` rows of an fp32 LDS image [rows][ldt] holding output rows mb.. and columns n0..n0+BN
 template <DT T, int BN, int NT>
@@ -748,17 +670,15 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   // the XCD the remap below assumes); the previous tile's epilogue stores drain while the next tile's first
   // slices are in flight, and the workgroup's LDS is not released and re-acquired per tile
   for (int tile = blockIdx.x; tile < nwg; tile += gridDim.x) {
-#ifdef WMX_G256_STAMPS
-  const unsigned long long st0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
   int bid = tile;
   {  // bijective XCD remap (§5.5 T1): each XCD gets a contiguous range of tiles
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
   // grouped order inside that range: 4 row panels walk the columns together, so the ~32 tiles an XCD runs at
-  // once share 4 A panels and ~8 W panels in its L2 (row-major order shared 2 A panels but 16+ W panels)
-  constexpr int GM = WMX_G256_GM;
+  // once share 4 A panels and ~8 W panels in its L2 (row-major order shared 2 A panels but 16+ W panels; 8 panels:
+  // qkv alone 5 % faster, the encoder pass unchanged, profiles/r05t_g256_gm/)
+  constexpr int GM = 4;
   const int gsz = GM * tilesN;
   const int grp = bid / gsz, gr = bid - grp * gsz;
   const int gm = min(GM, tilesM - grp * GM);
@@ -766,10 +686,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-#if WMX_G256_BK != 64
-  const int nk = K >> 5;
-#endif
-  constexpr int NS = g256_slots<KIND>();  // ring slots: NS - 1 slices in flight ahead of the one being read
   // this thread's epilogue column quad (n0 + 4 (tid & 63)) of the bias, loaded now so its latency hides behind
   // the main loop (the epilogue's column quads are the same in all four rounds)
   // (direct epilogue kinds: the lane's column quad after the in-quad transpose, wn 64 + 16 (fr & 3) + 4 (fr >> 2))
@@ -778,23 +694,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   // into LDS past the ring, and c1's column quad is loaded with the bias
   constexpr bool kLnf = KIND == EPI_LNF_STORE16 || KIND == EPI_LNF_GELU16;
   constexpr bool kGelu = KIND == EPI_GELU16 || KIND == EPI_LNF_GELU16;
-  constexpr bool kDirect = kLnf || (WMX_G256_DIRECT && (KIND == EPI_STORE16 || KIND == EPI_GELU16));
-  constexpr bool kSwap = g256_swap<KIND>();
-  // every kind on the 64-deep ring computes C^T fragments (WMX_G256_SWAP = 2; 1: the direct-epilogue kinds only):
-  // the LDS-image epilogues then write a lane's 4 consecutive columns with one ds_write_b128 instead of 4 b32
-  constexpr bool kSwapAll = kSwap || (WMX_G256_SWAP == 2 && WMX_G256_BK == 64);
+  constexpr bool kDirect = kLnf || KIND == EPI_STORE16 || KIND == EPI_GELU16;
   const int bcol = kDirect ? (wave & 3) * 64 + 16 * (lane & 3) + 4 * ((lane >> 2) & 3) : 4 * (tid & 63);
   float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f), c14 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (kSwap) {
-    // the tile's 256 bias (c2) and c1 columns go to LDS by DMA ahead of the ring (wave 7: bias, wave 6: c1; one
-    // 1 KiB piece each, columns clamped to N - 4), covered by the main loop's first counted wait
-    if (wave >= 6 && (wave == 7 || kLnf) && e.bias) {
-      const float* src = wave == 7 ? e.bias : e.c1;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + min(n0 + 4 * lane, N - 4)),
-                                       (__attribute__((address_space(3))) void*)(smem + kG256Bias + (7 - wave) * 1024),
-                                       16, 0, 0);
-    }
-  }
   if constexpr (kLnf) {
     // the tile's raw statistics go to LDS by DMA ahead of the ring's first slices (wave g < lng: group g's 256 rows,
     // two 1 KiB pieces; rows past M clamped, never stored), so the counted vmcnt of the main loop covers them and no
@@ -808,16 +710,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
             (__attribute__((address_space(3))) void*)(smem + kG256StatRaw + (wave * 256 + 128 * pc) * 8), 16, 0, 0);
       }
     }
-    if constexpr (!kSwap) {
-      const int bc = min(n0 + bcol, N - 4);
-      bias4 = *reinterpret_cast<const float4*>(e.bias + bc);
-      c14 = *reinterpret_cast<const float4*>(e.c1 + bc);
-    }
-  } else if (!kSwap && KIND >= 0 && e.bias && n0 + bcol < N) {
+    const int bc = min(n0 + bcol, N - 4);
+    bias4 = *reinterpret_cast<const float4*>(e.bias + bc);
+    c14 = *reinterpret_cast<const float4*>(e.c1 + bc);
+  } else if (KIND >= 0 && e.bias && n0 + bcol < N) {
     bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + bcol);
   }
 
-#if WMX_G256_BK == 64
   // Half-tile ring (the geometry of cdna_hip_programming.md §5's 256² template): K-tiles of 64 (128-B rows = whole
   // cache lines, where the 32-deep slices below fetch every line in two halves one slice apart) in two 64 KiB buffers
   // (t & 1) of four 16 KiB units, each 128 rows x 128 B:
@@ -889,8 +788,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
-          acc[4 * g + ii][2 * h + jj] = kSwapAll ? WMX_G256_MFMA(bfr[jj][s], af[ii][s], acc[4 * g + ii][2 * h + jj])
-                                                 : WMX_G256_MFMA(af[ii][s], bfr[jj][s], acc[4 * g + ii][2 * h + jj]);
+          acc[4 * g + ii][2 * h + jj] = WMX_G256_MFMA(af[ii][s], bfr[jj][s], acc[4 * g + ii][2 * h + jj]);
   };
   // prologue: K-tile 0 whole, then units 0, 2, 3 of K-tile 1 (its unit 1 goes out in phase 0 of K-tile 0)
 #pragma unroll
@@ -906,33 +804,24 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
-#if WMX_G256_PRIO == 1
+  // static priority 1 for the lagging half (MI355X_MICROARCH.md "two waves per SIMD" item 4; s_setprio around every
+  // segment measured 1.0-1.4 % slower per encoder pass, profiles/r03zs_static_prio/)
   if (lagging) __builtin_amdgcn_s_setprio(1);
-#endif
 #define WMX_G256_SEG(QG, QH)                                 \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         \
   __builtin_amdgcn_sched_barrier(0);                         \
   __builtin_amdgcn_s_barrier();                              \
   WMX_G256_PIN;                                              \
-  WMX_G256_PRIO_ON;                                          \
   quadrant(QG, QH);                                          \
-  WMX_G256_PRIO_OFF;                                         \
   __builtin_amdgcn_sched_barrier(0);                         \
   __builtin_amdgcn_s_barrier();
   for (int t = 0; t < nk; ++t) {
     const char* U = smem + (t & 1) * 65536;
     read_a(U);  // phase 0: units 0 and 1
     read_b(U + 16384);
-#if WMX_G256_LATE1 == 0
     if (t + 1 < nk) issue_unit(t + 1, 1);
-#endif
     WMX_G256_SEG(0, 0)
     read_b(U + 2 * 16384);  // phase 1: unit 2
-#if WMX_G256_LATE1
-    // unit 1 of K-tile t + 1 issued here instead of in phase 0 (the 12-read segment), ahead of unit 0 of t + 2 so
-    // the phase-3 vmcnt(6) still completes it
-    if (t + 1 < nk) issue_unit(t + 1, 1);
-#endif
     if (t + 2 < nk) issue_unit(t + 2, 0);
     WMX_G256_SEG(0, 1)
     read_a(U + 3 * 16384);  // phase 2: unit 3
@@ -948,141 +837,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     WMX_G256_SEG(1, 0)
   }
 #undef WMX_G256_SEG
-#else
-  // staging: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 are A rows, 16..31 W rows.
-  // Wave w issues pieces w, w + 8, w + 16, w + 24; lane l covers row l >> 2, 16-B column (l & 3).
-  const int srow = lane >> 2;
-  const int scol = ((lane & 3) ^ ((-(srow >> 2)) & 3)) * 8;  // source k offset of this lane's swizzled piece
-  const uint16_t* src[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int pc = wave + 8 * j;
-    if (pc < 16) {
-      src[j] = A + (long)min(m0 + pc * 16 + srow, M - 1) * lda + scol;
-    } else {
-      src[j] = W + (long)min(n0 + (pc - 16) * 16 + srow, N - 1) * ldw + scol;
-    }
-  }
-  // half h of slice kt: pieces 2h, 2h + 1 of this wave (h = 0: A rows, h = 1: W rows)
-  auto issue_half = [&](int kt, int h) {
-#if WMX_G256_MODE == 2
-    return;
-#endif
-    char* slot = smem + (kt % NS) * kG256Slot;
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = 2 * h + jj;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + kt * 32),
-                                       (__attribute__((address_space(3))) void*)(slot + (wave + 8 * j) * 1024), 16, 0,
-                                       0);
-    }
-  };
-  auto issue = [&](int kt) {
-    issue_half(kt, 0);
-    issue_half(kt, 1);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  const int piece = (fq ^ ((-(fr >> 2)) & 3)) << 4;
-  const int aoff = (wm * 128 + fr) * 64 + piece;
-  const int boff = BM * 64 + (wn * 64 + fr) * 64 + piece;
-
-  // Ping-pong schedule (cdna_hip_programming.md §5 256² template, T3+T4+T5): every 32-deep slice is two phases;
-  // a phase is [memory segment] s_barrier [16-MFMA segment] s_barrier.  Waves 4..7 (wave row 1) run one barrier
-  // behind waves 0..3, so on every SIMD one wave computes while its partner reads LDS / issues DMA.
-  //   phase A of slice t: ds_read B frags 0..3 + A frags 0..3; issue the A half of slice t + 3 into slot (t-1)&3
-  //                       (every memory segment retires its ds_reads with lgkmcnt(0) BEFORE its barrier, so the
-  //                       lagging half's last reads of slice t-1 are done before the leading half restages it)
-  //   phase B of slice t: wait (counted vmcnt) for slice t + 1; ds_read A frags 4..7; issue the W half of t + 3
-  // The wait in phase B of slice t precedes, by at least one barrier, every wave's first read of slice t + 1.
-#pragma unroll
-  for (int q = 0; q < NS - 1; ++q)
-    if (q < nk) issue(q);
-  vmcnt_even(4 * (min(nk, NS - 1) - 1));  // slice 0 landed (every younger slice may still fly)
-  __builtin_amdgcn_s_barrier();
-  const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
-  if (lagging) __builtin_amdgcn_s_barrier();
-#if WMX_G256_PRIO == 1
-  if (lagging) __builtin_amdgcn_s_setprio(1);  // static priority for the lagging half (MI355X_MICROARCH.md item 4)
-#endif
-#if WMX_G256_PHASES == 1
-  // one phase per slice: [12 ds_reads (A 0..7, B 0..3) + the 4 DMAs of slice t + 3 + counted wait for t + 1]
-  // s_barrier [32 MFMAs] s_barrier; waves 4..7 one barrier behind, as in the two-phase form
-  u16x8 af[8], bfr[4];
-  static_assert(NS == 4, "one-phase loop: 4 slots");
-  for (int t = 0; t < nk; ++t) {
-    const char* S = smem + (t & 3) * kG256Slot;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const u16x8*>(S + boff + j * 1024);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + i * 1024);
-    if (t + 3 < nk) issue(t + 3);
-    if (t + 3 < nk)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (t + 2 < nk)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    WMX_G256_PRIO_ON;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
-    WMX_G256_PRIO_OFF;
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-  }
-#else
-  u16x8 af[4], bfr[4];
-  for (int t = 0; t < nk; ++t) {
-    const char* S = smem + (t % NS) * kG256Slot;
-    // ---- phase A ----
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const u16x8*>(S + boff + j * 1024);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + i * 1024);
-    if (t + NS - 1 < nk) issue_half(t + NS - 1, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    WMX_G256_PRIO_ON;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i][j]);
-    WMX_G256_PRIO_OFF;
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // ---- phase B ----
-    // slice t + 1 is complete once only slices t + 2 .. t + NS - 2 (4 DMAs each) and the first half of t + NS - 1 (2)
-    // may be outstanding
-    vmcnt_even(4 * max(0, min(nk - 1, t + NS - 2) - (t + 1)) + (t + NS - 1 < nk ? 2 : 0));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u16x8*>(S + aoff + (i + 4) * 1024);
-    if (t + NS - 1 < nk) issue_half(t + NS - 1, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    WMX_G256_PRIO_ON;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i + 4][j] = WMX_G256_MFMA(af[i], bfr[j], acc[i + 4][j]);
-    WMX_G256_PRIO_OFF;
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-  }
-#endif
-#endif  // WMX_G256_BK
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
   if constexpr (kLnf) {  // Chan merge of the equal-count (256-column) groups of each of the tile's rows
@@ -1102,67 +856,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     }
     __syncthreads();
   }
-#ifdef WMX_G256_STAMPS
-  const unsigned long long st1 = __builtin_amdgcn_s_memtime();
-#endif
-
-#if WMX_G256_MODE == 3  // ablation: main loop only (keeps the accumulators live through an untaken store)
-  {
-    float sacc = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) sacc += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-    if (sacc == 1234.5f) reinterpret_cast<float*>(e.out)[tid] = sacc;
-    continue;
-  }
-#endif
-  if constexpr (kSwap) {
-    // C^T fragments: lane (fr, fq) holds C[16 i + fr][16 j + 4 fq .. + 3] of the wave tile, four consecutive
-    // columns of one row: bias (c2) and c1 from the LDS stage, (mean, rstd) of the row from the merged statistics,
-    // one 8-byte store per (i, j), no transpose
-    const float* bl = reinterpret_cast<const float*>(smem + kG256Bias);
-    const int cb = wn * 64 + 4 * fq;
-    float4 b4[4], c4[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      b4[j] = e.bias ? *reinterpret_cast<const float4*>(bl + cb + 16 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (kLnf) c4[j] = *reinterpret_cast<const float4*>(bl + 256 + cb + 16 * j);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rt = wm * 128 + 16 * i + fr, m = m0 + rt;
-      float2 ls = make_float2(0.f, 1.f);
-      if constexpr (kLnf) ls = reinterpret_cast<const float2*>(smem + kG256StatRow)[rt];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 v = acc[i][j];
-        float4 o;
-        if constexpr (kLnf)
-          o = make_float4(ls.y * (v[0] - ls.x * c4[j].x) + b4[j].x, ls.y * (v[1] - ls.x * c4[j].y) + b4[j].y,
-                          ls.y * (v[2] - ls.x * c4[j].z) + b4[j].z, ls.y * (v[3] - ls.x * c4[j].w) + b4[j].w);
-        else
-          o = make_float4(v[0] + b4[j].x, v[1] + b4[j].y, v[2] + b4[j].z, v[3] + b4[j].w);
-        if (kGelu) o = gelu_erf4(o);
-        const int n = n0 + cb + 16 * j;
-        if (m < M && n < N) {
-          const u16x4 hv = {from_f32<T>(o.x), from_f32<T>(o.y), from_f32<T>(o.z), from_f32<T>(o.w)};
-          *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = hv;
-        }
-      }
-    }
-#ifdef WMX_G256_STAMPS
-    if (tid == 0 && tile < kG256Stamps) {
-      g256_stamps[tile][0] = st0;
-      g256_stamps[tile][1] = st1;
-      g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
-      g256_stamps[tile][3] = rt0;
-      g256_stamps[tile][4] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-    __syncthreads();  // the next tile's DMA must not overwrite the ring or the bias stage before every wave left
-    continue;
-  } else if constexpr (kDirect) {
+  if constexpr (kDirect) {
     // LDS-free epilogue: for every (fragment row i, register r) the 16 lanes of a row group hold columns
     // 16 j + fr (j = 0..3) of one output row; a 4 x 4 transpose inside each lane quad (lane-dependent register
     // rotation, three DPP quad rotations, rotation back) leaves lane (fr) with the 4 consecutive columns
@@ -1223,15 +917,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
         }
       }
     }
-#ifdef WMX_G256_STAMPS
-    if (tid == 0 && tile < kG256Stamps) {
-      g256_stamps[tile][0] = st0;
-      g256_stamps[tile][1] = st1;
-      g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
-      g256_stamps[tile][3] = rt0;
-      g256_stamps[tile][4] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
     __syncthreads();  // the next tile's DMA must not overwrite the ring before every wave left this tile
     continue;
   }
@@ -1251,12 +936,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
         const int i = (rd & 1) * 4 + ii;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if constexpr (kSwapAll) {  // C^T fragment: 4 consecutive columns of row ii 16 + fr, one ds_write_b128
-            *reinterpret_cast<f32x4*>(img + (ii * 16 + fr) * LDT + wn * 64 + j * 16 + 4 * fq) = acc[i][j];
-          } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) img[(ii * 16 + fq * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
-          }
+          for (int r = 0; r < 4; ++r) img[(ii * 16 + fq * 4 + r) * LDT + wn * 64 + j * 16 + fr] = acc[i][j][r];
         }
       }
     }
@@ -1267,15 +948,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const uint16_t* __restr
     }
     __syncthreads();
   }
-#ifdef WMX_G256_STAMPS  // diagnostic build only (tools/mb_gemm256 -DWMX_G256_STAMPS): per-tile phase clocks
-  if (tid == 0 && tile < kG256Stamps) {
-    g256_stamps[tile][0] = st0;
-    g256_stamps[tile][1] = st1;
-    g256_stamps[tile][2] = __builtin_amdgcn_s_memtime();
-    g256_stamps[tile][3] = rt0;
-    g256_stamps[tile][4] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
   }  // tile loop
 }
 
@@ -1388,9 +1060,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
-#if WMX_G256_PRIO == 1
   if (lagging) __builtin_amdgcn_s_setprio(1);  // static priority for the lagging half (as gemm256)
-#endif
   i32x8 af[2], bfr[4];
   int sa[2], sb[4];
   for (int t = 0; t < nk; ++t) {
@@ -1414,14 +1084,12 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sa[i], 0,
                                                                      sb[j]);
-    WMX_G256_PRIO_OFF;
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     // ---- phase B: A fragments 2, 3; W half of slice t + 2 ----
@@ -1440,14 +1108,12 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
-    WMX_G256_PRIO_ON;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i + 2][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i + 2][j], 0, 0, 0, sa[i],
                                                                          0, sb[j]);
-    WMX_G256_PRIO_OFF;
     if (!lagging) {  // the same barrier, seen from the leading half
       if (more)
         asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
@@ -1490,34 +1156,8 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_kernel(const uint8_t* __restr
 // 16..31 (g = l >> 5), i.e. 16-B pieces g and 2 + g of its 64-B row; its scale operand is the byte of (row l & 31,
 // 32-k block g) (tools/mx8_check32.hip measures both maps).  Epilogues through the 64 x 256 fp32 LDS image.
 // ------------------------------------------------------------------------------------------------
-#ifndef WMX_MX8_BK
-#define WMX_MX8_BK 128  // 128: the half-tile ring of whole 128-B lines; 64: 64-deep slices (half lines)
-#endif
-constexpr int kMx8bSlot = 512 * 64 + 512 * 4;  // 256 A + 256 W rows x 64 B, + the scale dword of each row
-constexpr int kMx8bNS = 4;
-constexpr int kMx8bLds = WMX_MX8_BK == 128 ? 4 * 32768 + 2 * 2048 : kMx8bNS * kMx8bSlot;  // 132 / 136 KiB
+constexpr int kMx8bLds = 4 * 32768 + 2 * 2048;  // 132 KiB: two 64 KiB unit buffers + two 2 KiB scale buffers
 static_assert(kMx8bLds <= 163840 && 64 * (256 + 4) * 4 <= kMx8bLds, "gemm_mx8_256 LDS");
-// s_waitcnt vmcnt(n), n in 0..15 (uniform)
-__device__ inline void vmcnt_upto15(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-  }
-}
 
 template <DT T, int KIND>
 __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __restrict__ A, long lda,
@@ -1525,7 +1165,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
                                                               const uint8_t* __restrict__ W, long ldw,
                                                               const uint8_t* __restrict__ WS, long ldws, int M, int N,
                                                               int K, Epi e) {
-  constexpr int BM = 256, BN = 256, NS = kMx8bNS;
+  constexpr int BM = 256, BN = 256;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesN = (N + BN - 1) / BN;
   const int tilesM = (M + BM - 1) / BM;
@@ -1544,16 +1184,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-#if WMX_MX8_BK != 128
-  const int nk = K >> 6;
-#endif
-  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#if WMX_MX8_BK != 128  // (the 128-deep ring loads it after the main loop: no VGPRs to spare inside)
-  if (e.bias && n0 + 4 * (tid & 63) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (tid & 63));
-#endif
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);  // (loaded after the main loop: no VGPRs to spare inside)
 
-#if WMX_MX8_BK == 128
-  // 128-deep half-tile ring (as gemm256's 64-deep one, WMX_G256_BK): a K-tile is 128 e4m3 = one 128-B line per row,
+  // 128-deep half-tile ring (as gemm256's 64-deep one): a K-tile is 128 e4m3 = one 128-B line per row,
   // four 16 KiB units of 128 rows in two buffers (unit 0 = A rows m0 + 128 wm + [0, 64), 1 = W rows n0 + 64 wn +
   // [0, 32), 2 = W rows n0 + 64 wn + [32, 64), 3 = A rows m0 + 128 wm + [64, 128)) plus the K-tile's scale dword of
   // every row (4 e8m0 bytes) in a 2 KiB buffer per K-tile, staged with unit 1.  Phase p: one 64 x 32 quadrant of the
@@ -1660,17 +1293,13 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
   __builtin_amdgcn_s_barrier();
   const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
-#if WMX_G256_PRIO == 1
   if (lagging) __builtin_amdgcn_s_setprio(1);
-#endif
 #define WMX_MX8_SEG(QG, QH)                          \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
   __builtin_amdgcn_sched_barrier(0);                 \
   __builtin_amdgcn_s_barrier();                      \
   WMX_G256_PIN;                                      \
-  WMX_G256_PRIO_ON;                                  \
   quadrant(QG, QH);                                  \
-  WMX_G256_PRIO_OFF;                                 \
   __builtin_amdgcn_sched_barrier(0);                 \
   __builtin_amdgcn_s_barrier();
   // one K-tile; I1 / I2: K-tile t + 1 / t + 2 exists.  The three forms are separate straight-line bodies: a
@@ -1713,126 +1342,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
 #pragma unroll
     for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[i][j]));
 #undef WMX_MX8_SEG
-#else
-  // staging as gemm256: a slot is 32 pieces of 1 KiB (16 rows x 64 B); pieces 0..15 A rows, 16..31 W rows; wave w
-  // issues pieces w, w + 8 (A) and w + 16, w + 24 (W); lane l: row l >> 2, 16-B column (l & 3) swizzled at the source
-  const int srow = lane >> 2;
-  const int scol = ((lane & 3) ^ ((-(srow >> 2)) & 3)) * 16;
-  const uint8_t* src[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int pc = wave + 8 * j;
-    src[j] = pc < 16 ? A + (long)min(m0 + pc * 16 + srow, M - 1) * lda + scol
-                     : W + (long)min(n0 + (pc - 16) * 16 + srow, N - 1) * ldw + scol;
-  }
-  // scales: wave w < 4 stages A rows 64 w + lane, wave w >= 4 W rows 64 (w - 4) + lane: the dword (kt / 2) of the row's
-  // e8m0 bytes, which holds slice kt's two 32-k blocks at bytes 2 (kt & 1), + 1 (rows are 4-B aligned: K % 128 == 0)
-  const uint8_t* ssrc = wave < 4 ? AS + (long)min(m0 + 64 * wave + lane, M - 1) * ldas
-                                 : WS + (long)min(n0 + 64 * (wave - 4) + lane, N - 1) * ldws;
-  const int sdst = 512 * 64 + wave * 256;
-  auto issue_half = [&](int kt, int h) {
-    char* slot = smem + (kt % NS) * kMx8bSlot;
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = 2 * h + jj;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + kt * 64),
-                                       (__attribute__((address_space(3))) void*)(slot + (wave + 8 * j) * 1024), 16, 0,
-                                       0);
-    }
-    if (h == 0)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ssrc + (kt >> 1) * 4),
-                                       (__attribute__((address_space(3))) void*)(slot + sdst), 4, 0, 0);
-  };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-
-  const int fr = lane & 31, g = lane >> 5;
-  // 16-B pieces g and 2 + g of the lane's row, at their swizzled LDS positions (p ^ sw(row), sw = (-(row >> 2)) & 3;
-  // every fragment row offset below is a multiple of 32, so sw depends on fr only)
-  const int sw = (-(fr >> 2)) & 3;
-  const int p0 = (g ^ sw) << 4, p1 = ((2 + g) ^ sw) << 4;
-  const int arow = wm * 128 + fr, brow = 256 + wn * 64 + fr;  // brow: W rows follow the 256 A rows in the slot
-  auto frag = [&](const char* S, int row) {
-    const i32x4 lo = *reinterpret_cast<const i32x4*>(S + row * 64 + p0);
-    const i32x4 hi = *reinterpret_cast<const i32x4*>(S + row * 64 + p1);
-    return i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  auto scale = [&](const char* S, int row, int kt) {
-    return (int)*reinterpret_cast<const uint8_t*>(S + 512 * 64 + row * 4 + 2 * (kt & 1) + g);
-  };
-
-#pragma unroll
-  for (int q = 0; q < NS - 1; ++q)
-    if (q < nk) {
-      issue_half(q, 0);
-      issue_half(q, 1);
-    }
-  vmcnt_upto15(5 * (min(nk, NS - 1) - 1));  // slice 0 landed
-  __builtin_amdgcn_s_barrier();
-  const bool lagging = __builtin_amdgcn_readfirstlane(wave) >= 4;
-  if (lagging) __builtin_amdgcn_s_barrier();
-#if WMX_G256_PRIO == 1
-  if (lagging) __builtin_amdgcn_s_setprio(1);  // static priority for the lagging half (as gemm256)
-#endif
-  i32x8 af[2], bfr[2];
-  int sa[2], sb[2];
-  for (int t = 0; t < nk; ++t) {
-    const char* S = smem + (t % NS) * kMx8bSlot;
-    // ---- phase A: B blocks 0, 1 and A blocks 0, 1; the A half (+ scales) of slice t + NS - 1 ----
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bfr[j] = frag(S, brow + 32 * j);
-      sb[j] = scale(S, brow + 32 * j, t);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      af[i] = frag(S, arow + 32 * i);
-      sa[i] = scale(S, arow + 32 * i, t);
-    }
-    if (t + NS - 1 < nk) issue_half(t + NS - 1, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // retire this segment's reads before the barrier (WAR)
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    WMX_G256_PRIO_ON;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sa[i], 0, sb[j]);
-    WMX_G256_PRIO_OFF;
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // ---- phase B: slice t + 1 complete once only slices t + 2 .. t + NS - 2 (5 DMAs each) and the A half of
-    // t + NS - 1 (3) may be outstanding; A blocks 2, 3; the W half of t + NS - 1 ----
-    vmcnt_upto15(5 * max(0, min(nk - 1, t + NS - 2) - (t + 1)) + (t + NS - 1 < nk ? 3 : 0));
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      af[i] = frag(S, arow + 64 + 32 * i);
-      sa[i] = scale(S, arow + 64 + 32 * i, t);
-    }
-    if (t + NS - 1 < nk) issue_half(t + NS - 1, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    WMX_G256_PRIO_ON;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i + 2][j] =
-            __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[i], bfr[j], acc[i + 2][j], 0, 0, 0, sa[i], 0, sb[j]);
-    WMX_G256_PRIO_OFF;
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-  }
-#endif  // WMX_MX8_BK
-#if WMX_MX8_BK == 128
   if (e.bias && n0 + 4 * (tid & 63) < N) bias4 = *reinterpret_cast<const float4*>(e.bias + n0 + 4 * (tid & 63));
-#endif
   if (!lagging) __builtin_amdgcn_s_barrier();
   __syncthreads();
 
@@ -1859,7 +1369,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
     __syncthreads();
     if constexpr (KIND == EPI_GELU_MX8)
       epi_gelu_mx8_blocks<T>(e, img, LDT, m0 + rd * 64, n0, M, tid);
-    else if constexpr (KIND == EPI_RESID32 && WMX_MX8_BK == 128)  // (8 rows at once spilled beside the accumulators)
+    else if constexpr (KIND == EPI_RESID32)  // (8 rows at once spilled beside the accumulators)
       epi_rows64<T, EPI_RESID32, 4>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4);
     else
       epi_image64<T, KIND>(e, img, LDT, m0 + rd * 64, n0, M, N, tid, &bias4, kPre ? &pre : nullptr);
@@ -1873,10 +1383,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_256_kernel(const uint8_t* __r
 
 static int g256_grid(int tiles);
 
-// the 256 x 256 / 32x32x64 form for the encoder shapes (WMX_MX8_256=0: the 256 x 128 / 16x16x128 form everywhere)
+// the 256 x 256 / 32x32x64 form for the encoder shapes (the 256 x 128 / 16x16x128 form for the others)
 static bool mx8_256_ok(const Mx8Call& g) {
-  static const bool off = getenv("WMX_MX8_256") && atoi(getenv("WMX_MX8_256")) == 0;
-  return !off && g.M >= 4096 && g.N % 256 == 0 && g.K % 64 == 0 && g.ldas % 2 == 0 && g.ldws % 2 == 0 &&
+  return g.M >= 4096 && g.N % 256 == 0 && g.K % 64 == 0 && g.ldas % 2 == 0 && g.ldws % 2 == 0 &&
          (g.epi.kind == EPI_STORE16 || g.epi.kind == EPI_RESID32 || g.epi.kind == EPI_GELU_MX8);
 }
 
@@ -2071,114 +1580,6 @@ static void launch_skinny(const GemmCall& g, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// RedTail: split-K reduction + residual + LayerNorm inside the producing packed GEMM launch (the decode step's
-// out-projections and fc2).  The in-launch merge of cdna_hip_programming.md Guideline 16 in its sc1 form, twice:
-//   1. every workgroup drains its write-through partial stores and takes a ticket on its column group's counter;
-//      the one drawing S-1 sums the S slices in slice order, x = (x + bias) + sum (same order as
-//      reduce_ln4_kernel), stores x write-through and re-arms the counter;
-//   2. those reducers take a ticket on one launch counter; the last normalises every row, one wave per row
-//      group (4 rows x 5 column quads per lane in flight, wave-only reductions), and re-arms it.
-// Requires N % 4 == 0 and N <= 1280 (packed_tail_ok).
-// ------------------------------------------------------------------------------------------------
-constexpr int kTailQpl = 5, kTailRows = 4;
-typedef unsigned int tail_u32x4 __attribute__((ext_vector_type(4)));
-// 16-byte write-through (sc1, aux 16) store / sc1 load through a buffer resource on a wave-uniform base
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tail_rsrc(const float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ void tail_st4(__amdgpu_buffer_rsrc_t r, long idx, float4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tail_u32x4, v), r, (int)(idx * 4), 0, 16);
-}
-__device__ __forceinline__ float4 tail_ld4(__amdgpu_buffer_rsrc_t r, long idx) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
-}
-template <DT T, int MT, int NCT, int NW>
-__device__ __forceinline__ void packed_red_tail(const RedTail& rt, const float* part, int M, int N, int S, int m0,
-                                                int t0) {
-  constexpr int NT = 64 * NW, C4 = 4 * NCT;
-  __shared__ int flag;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int cg = blockIdx.z * gridDim.x + blockIdx.x;
-  if (tid == 0) flag = __hip_atomic_fetch_add(rt.cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
-  __syncthreads();
-  if (!flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const auto pr = tail_rsrc(part), xr = tail_rsrc(rt.x);
-  for (int idx = tid; idx < MT * 16 * C4; idx += NT) {
-    const int row = idx / C4, c = (idx - row * C4) * 4;
-    const int m = m0 + row, n = t0 * 16 + c;
-    if (m >= M || n >= N) continue;
-    float4 t[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      t[s] = s < S ? tail_ld4(pr, ((long)s * M + m) * N + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 xv = *reinterpret_cast<const float4*>(rt.x + (long)m * N + n);
-    const float4 bv = rt.bias ? *reinterpret_cast<const float4*>(rt.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) p = make_float4(p.x + t[s].x, p.y + t[s].y, p.z + t[s].z, p.w + t[s].w);
-    tail_st4(xr, (long)m * N + n,
-             make_float4((xv.x + bv.x) + p.x, (xv.y + bv.y) + p.y, (xv.z + bv.z) + p.z, (xv.w + bv.w) + p.w));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int ntask = gridDim.x * gridDim.z;
-  if (tid == 0) {
-    __hip_atomic_store(rt.cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = __hip_atomic_fetch_add(rt.cnt + ntask, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntask - 1;
-  }
-  __syncthreads();
-  if (!flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const int n4 = N >> 2;
-  for (int r0 = wave * kTailRows; r0 < M; r0 += NW * kTailRows) {
-    float4 v[kTailRows][kTailQpl];
-#pragma unroll
-    for (int r = 0; r < kTailRows; ++r)
-#pragma unroll
-      for (int j = 0; j < kTailQpl; ++j) {
-        const int q = lane + 64 * j, m = r0 + r;
-        const bool ok = m < M && q < n4;
-        v[r][j] = ok ? tail_ld4(xr, (long)m * N + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-    for (int r = 0; r < kTailRows; ++r) {
-      const int m = r0 + r;
-      if (m >= M) break;  // wave-uniform
-      float sum = 0.f;
-#pragma unroll
-      for (int j = 0; j < kTailQpl; ++j) sum += (v[r][j].x + v[r][j].y) + (v[r][j].z + v[r][j].w);
-      const float mean = wave_sum(sum) / N;
-      float sq = 0.f;
-#pragma unroll
-      for (int j = 0; j < kTailQpl; ++j) {
-        if (lane + 64 * j < n4) {
-          const float4 d = make_float4(v[r][j].x - mean, v[r][j].y - mean, v[r][j].z - mean, v[r][j].w - mean);
-          sq += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-        }
-      }
-      const float rstd = 1.0f / sqrtf(wave_sum(sq) / N + 1e-5f);
-#pragma unroll
-      for (int j = 0; j < kTailQpl; ++j) {
-        const int q = lane + 64 * j;
-        if (q < n4) {
-          const float4 gg = *reinterpret_cast<const float4*>(rt.g + 4 * q);
-          const float4 bb = *reinterpret_cast<const float4*>(rt.b + 4 * q);
-          const u16x4 h = {from_f32<T>((v[r][j].x - mean) * rstd * gg.x + bb.x),
-                           from_f32<T>((v[r][j].y - mean) * rstd * gg.y + bb.y),
-                           from_f32<T>((v[r][j].z - mean) * rstd * gg.z + bb.z),
-                           from_f32<T>((v[r][j].w - mean) * rstd * gg.w + bb.w)};
-          *reinterpret_cast<u16x4*>(rt.out + (long)m * N + 4 * q) = h;
-        }
-      }
-    }
-  }
-  if (tid == 0) __hip_atomic_store(rt.cnt + ntask, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ------------------------------------------------------------------------------------------------
 // decode GEMM on packed weights (skinny M): workgroup = NCT 16-column tiles x one K slice x one 16*MT row chunk;
 // its 4 waves split the slice's k-steps, every wave issues KU k-steps of loads (NCT contiguous 1 KiB weight
 // fragments + MT activation fragments) before their MFMAs, partial tiles are summed through LDS.
@@ -2190,11 +1591,7 @@ __device__ __forceinline__ void packed_red_tail(const RedTail& rt, const float* 
 // is straight-line code.  The unsplit residual producers (MT + NCT <= 3, fc2: 10 k-steps per wave) take 5 per batch.
 template <int MT, int NCT>
 constexpr int packed_ku() {
-#ifdef WMX_PACKED_GUARDED  // diagnostic build of round 2's faulting form: per-step guarded loads
-  return (MT + NCT) <= 3 ? 4 : (MT + NCT) <= 8 ? 2 : 1;
-#else
   return (MT + NCT) <= 3 ? 5 : (MT + NCT) <= 8 ? 2 : 1;
-#endif
 }
 // 8-bit weights: a k-step is 64 deep (one 16-byte weight piece + two A fragments per 16-row tile); the waves per
 // workgroup come from the 32-deep step count as for 16-bit weights (packed_nw), so a wave holds 1-2 of these wider
@@ -2295,33 +1692,24 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
   }
 }
 
-#ifndef WMX_PART_ST
-#define WMX_PART_ST 0  // split-K partial stores: 0 plain (default), 1 non-temporal, 2 write-through sc1 (A/B builds)
-#endif
 // Epilogue class, a template parameter so each launch carries only the code it runs (these launches are a few
 // microseconds long and start on a cold instruction cache: a generic epilogue switch in a split-K launch measured
 // +0.6 us per launch): kPackedPart split-K raw partials (S > 1); kPackedGelu S == 1 bias + GELU -> 16-bit
-// (decode fc1; bias loaded beside the first k-steps); kPackedGeneric every other S == 1 epilogue; kPackedTail
-// partials + the in-launch reduce / LayerNorm tail (RedTail)
-enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2, kPackedTail = 3 };
+// (decode fc1; bias loaded beside the first k-steps); kPackedGeneric every other S == 1 epilogue
+enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2 };
 
 // W8: the weights are e4m3 bytes in the packed8_index layout with per-row scales wsc (a k-step is 64 deep: the
 // same 16-byte lane load as a bf16 k-step, widened in registers into the B fragments of two MFMAs; the row scale
 // multiplies the reduced fp32 tile before any epilogue or partial store)
-// AREC: A is the merge of a decode cross attention's two key-chunk records (PackedCall::arec): the lane loads both
-// chunks' 8 fp32 outputs and (max, sum) of its row and head in the batch, and merges them after the batch's loads
-// exactly as the cross attention's in-launch merge does (same operations, same order: bit-identical A)
-template <DT T, int MT, int NCT, int NW, int EPK, int W8 = 0, bool AREC = false>
+template <DT T, int MT, int NCT, int NW, int EPK, int W8 = 0>
 __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __restrict__ A, long lda,
                                                               const uint16_t* __restrict__ Wp, int M, int N, int K,
-                                                              int S, Epi e, float* __restrict__ part, RedTail rt,
+                                                              int S, Epi e, float* __restrict__ part,
                                                               unsigned long long* __restrict__ tprobe,
                                                               const int* __restrict__ pslot,
-                                                              const float* __restrict__ wsc,
-                                                              const float2* __restrict__ arec) {
+                                                              const float* __restrict__ wsc) {
   constexpr int KU = W8 ? packed_ku8<MT, NCT>() : packed_ku<MT, NCT>();
   constexpr int LDR = 16 * NCT + 1;
-  constexpr bool TAIL = EPK == kPackedTail;
   constexpr int NT = 64 * NW;
   __shared__ float red[NW][MT * 16][LDR];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2397,68 +1785,13 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   }
   for (int kk = ks0; !W8 && kk < ks1; kk += KU) {
     u16x8 b[KU][NCT], av[KU][MT];
-    [[maybe_unused]] f32x4 ro[AREC ? KU : 1][AREC ? MT : 1][4];
-    [[maybe_unused]] float2 rml[AREC ? KU : 1][AREC ? MT : 1][2];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
-#ifdef WMX_PACKED_GUARDED
-      if (kk + u >= ks1) continue;
-      int k = kk + u;
-      {  // diagnostic bounds check: report (and do not issue) any load outside the packed weights / the A rows
-        bool bad = k < 0 || k >= ksteps;
-#pragma unroll
-        for (int j = 0; j < NCT; ++j)
-          bad |= (wt[j] + ((long)k << 9) - Wp) + 8 > (long)ntiles * ksteps * 512 || (wt[j] + ((long)k << 9)) < Wp;
-#pragma unroll
-        for (int i = 0; i < MT; ++i) bad |= (ar[i] + k * 32 - A) + 8 > (long)(M - 1) * lda + K || (ar[i] + k * 32) < A;
-        if (bad) {
-          printf("WMX_PACKED_GUARDED OOB: blk (%d,%d,%d) wave %d lane %d kk %d u %d ks0 %d ks1 %d M %d N %d K %d S %d\n",
-                 blockIdx.x, blockIdx.y, blockIdx.z, wave, lane, kk, u, ks0, ks1, M, N, K, S);
-          k = ks0;
-        }
-      }
-#else
       const int k = min(kk + u, ks1 - 1);  // clamped: a duplicate load of the wave's last k-step, MFMA skipped
-#endif
 #pragma unroll
       for (int j = 0; j < NCT; ++j) b[u][j] = stream_load(reinterpret_cast<const u16x8*>(wt[j] + ((long)k << 9)));
-      if constexpr (AREC) {
-        const float* ro0 = reinterpret_cast<const float*>(A);
-        const int kc = k * 32 + 8 * fq, hd = kc >> 6;
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          const long row = min(m0 + i * 16 + fr, M - 1);
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const float* o = ro0 + ((long)c * M + row) * lda + kc;
-            ro[u][i][2 * c] = *reinterpret_cast<const f32x4*>(o);
-            ro[u][i][2 * c + 1] = *reinterpret_cast<const f32x4*>(o + 4);
-            rml[u][i][c] = arec[((long)c * M + row) * (lda >> 6) + hd];
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + k * 32);
-      }
-    }
-    if constexpr (AREC) {  // the cross attention's merge (wmx_attn.hip, KS = 2): max, weights, sums, o / l
-#pragma unroll
-      for (int u = 0; u < KU; ++u)
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          float Mx = -INFINITY;
-          Mx = fmaxf(Mx, rml[u][i][0].x);
-          Mx = fmaxf(Mx, rml[u][i][1].x);
-          const float s0 = rml[u][i][0].x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(rml[u][i][0].x - Mx);
-          const float s1 = rml[u][i][1].x == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(rml[u][i][1].x - Mx);
-          const float l = __builtin_fmaf(rml[u][i][1].y, s1, __builtin_fmaf(rml[u][i][0].y, s0, 0.f));
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const float o2 = __builtin_fmaf(ro[u][i][2 + (q >> 2)][q & 3], s1,
-                                            __builtin_fmaf(ro[u][i][q >> 2][q & 3], s0, 0.f));
-            av[u][i][q] = from_f32<T>(o2 / l);
-          }
-        }
+      for (int i = 0; i < MT; ++i) av[u][i] = *reinterpret_cast<const u16x8*>(ar[i] + k * 32);
     }
     // the whole batch is in flight before the first MFMA: without this fence the scheduler may interleave a
     // load behind an MFMA and wait for it with vmcnt(0), two round trips per batch instead of one (measured +1 us
@@ -2502,22 +1835,14 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
       v4[2] *= wsc4.z;
       v4[3] *= wsc4.w;
     }
-    if constexpr (TAIL) {  // write-through (sc1) so the last arriver on another XCD reads them without an L2 release
-      tail_st4(tail_rsrc(part), ((long)sp * M + m) * N + n, make_float4(v4[0], v4[1], v4[2], v4[3]));
-    } else if constexpr (EPK == kPackedGelu) {  // N and ldc multiples of 4 (host-checked)
+    if constexpr (EPK == kPackedGelu) {  // N and ldc multiples of 4 (host-checked)
       const u16x4 h = {from_f32<T>(gelu_erf(v4[0] + pbias.x)), from_f32<T>(gelu_erf(v4[1] + pbias.y)),
                        from_f32<T>(gelu_erf(v4[2] + pbias.z)), from_f32<T>(gelu_erf(v4[3] + pbias.w))};
       *reinterpret_cast<u16x4*>(reinterpret_cast<uint16_t*>(e.out) + (long)m * e.ldc + n) = h;
     } else if (EPK == kPackedPart || S > 1) {
       float* dst = part + ((long)sp * M + m) * N + n;
       if (n + 3 < N && (N & 3) == 0) {
-#if WMX_PART_ST == 2  // A/B build switch: write-through (sc1) partial stores, no dirty L2 lines at the boundary
-        tail_st4(tail_rsrc(part), ((long)sp * M + m) * N + n, make_float4(v4[0], v4[1], v4[2], v4[3]));
-#elif WMX_PART_ST == 1  // non-temporal partial stores
-        __builtin_nontemporal_store(f32x4{v4[0], v4[1], v4[2], v4[3]}, reinterpret_cast<f32x4*>(dst));
-#else
         *reinterpret_cast<float4*>(dst) = make_float4(v4[0], v4[1], v4[2], v4[3]);
-#endif
       } else {
         for (int q = 0; q < 4 && n + q < N; ++q) dst[q] = v4[q];
       }
@@ -2529,7 +1854,6 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
       }
     }
   }
-  if constexpr (TAIL) packed_red_tail<T, MT, NCT, NW>(rt, part, M, N, S, m0, t0);
   if (tprobe && tid == 0) probe_record(tprobe, *pslot, probe_t0);
 }
 
@@ -2541,20 +1865,6 @@ static int packed_mt(int M) {
 int packed_nct(int M, int N, int K) {
   const int mt = packed_mt(M);
   if (mt > 4) return 2;
-  // tuning override (WMX_PACKED_NCT="N:K:nct,..."): the column tiles per workgroup of one projection shape
-  static const std::vector<std::array<int, 3>> ov = [] {
-    std::vector<std::array<int, 3>> v;
-    const char* e = getenv("WMX_PACKED_NCT");
-    for (const char* q = e; q && *q;) {
-      std::array<int, 3> t{};
-      if (sscanf(q, "%d:%d:%d", &t[0], &t[1], &t[2]) == 3 && (t[2] == 1 || t[2] == 2 || t[2] == 4)) v.push_back(t);
-      q = strchr(q, ',');
-      if (q) ++q;
-    }
-    return v;
-  }();
-  for (const auto& t : ov)
-    if (t[0] == N && t[1] == K) return t[2];
   return (N >= 16384 || K >= 4096) ? 4 : 2;
 }
 
@@ -2566,12 +1876,8 @@ int packed_splits(int M, int N, int K, long cap_elems) {
   // workgroups a split aims for: 160 up to 24 rows (the bench's two groups of 4 windows x beam 5 decode in step, so
   // two launches of this size run at once; fewer slices = fewer partials for the consumers: 414.3-414.7x against
   // 410.5-410.8x with 480, profiles/r04_split_target/), 480 above (16 windows: 724.6 / 568.0x against 723.1 / 562.6x
-  // with 240); WMX_PACKED_TARGET overrides (tuning runs)
-  static const long target_env = [] {
-    const char* v = getenv("WMX_PACKED_TARGET");  // (<= 0 or unset: the row rule below)
-    return v ? std::max(0L, atol(v)) : 0L;
-  }();
-  const long target = target_env ? target_env : (M <= 24 ? 160L : 480L);
+  // with 240)
+  const long target = M <= 24 ? 160L : 480L;
   long S = (target + wgs - 1) / wgs;
   S = std::min<long>(S, std::max(1, (K / 32) / 4));
   S = std::min<long>(S, K / (2L * std::max(M, 1)));
@@ -2595,18 +1901,12 @@ constexpr int kPackedOneWgPerCu = 256;
 template <int MT, int NCT>
 static int packed_nw(int K, int S, long wgs = 1L << 30, bool w8 = false) {
   const int ksteps = K / 32, kps = (ksteps + S - 1) / S;
-  // k-steps per wave the wave count aims for (WMX_PACKED_PER overrides 4 for tuning runs: 2 = one load batch)
-  static const int per_t = [] {
-    const char* v = getenv("WMX_PACKED_PER");
-    return v ? std::max(1, atoi(v)) : 4;
-  }();
-  const int per4 = (kps + per_t - 1) / per_t;
-  static const bool only4 = getenv("WMX_PACKED_NW4") != nullptr;  // A/B switch for tuning runs
-  static const bool lds80 = getenv("WMX_PACKED_LDS80") != nullptr;  // A/B switch: the 80 KiB budget everywhere
-  const int budget = (!lds80 && !w8 && wgs <= kPackedOneWgPerCu) ? 163840 : 81920;
+  // k-steps per wave the wave count aims for: 4 (two dependent load batches; 2, 3 measured within noise, round 4)
+  const int per4 = (kps + 3) / 4;
+  const int budget = (!w8 && wgs <= kPackedOneWgPerCu) ? 163840 : 81920;
   const bool fit8 = packed_red_bytes<MT, NCT>(8) <= budget;
   const bool fit16 = packed_red_bytes<MT, NCT>(16) <= budget;
-  if (only4 || per4 <= 4 || !fit8) return 4;
+  if (per4 <= 4 || !fit8) return 4;
   if (per4 <= 8 || !fit16) return 8;
   return 16;
 }
@@ -2616,29 +1916,16 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int ntiles = (g.N + 15) / 16;
   dim3 grid((ntiles + NCT - 1) / NCT, g.S, (g.M + MT * 16 - 1) / (MT * 16));
   const int nw = packed_nw<MT, NCT>(g.K, g.S, (long)grid.x * grid.y * grid.z, W8 != 0);
-  const bool tail = g.tail.cnt != nullptr;
-  const int epk = tail ? kPackedTail
-                 : g.S > 1 ? kPackedPart
+  const int epk = g.S > 1 ? kPackedPart
                  : (g.epi.kind == EPI_GELU16 && g.epi.bias && g.N % 4 == 0 && g.epi.ldc % 4 == 0) ? kPackedGelu
                                                                                                  : kPackedGeneric;
 #define WMX_PACKED_EPK(NWV, EPKV)                                                                                  \
   hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, EPKV, W8>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W,  \
-                     g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot, g.wscale, nullptr)
+                     g.M, g.N, g.K, g.S, g.epi, g.part, g.tprobe, g.pslot, g.wscale)
 #define WMX_PACKED_LAUNCH(NWV)                                                                                     \
   do {                                                                                                             \
     switch (epk) {                                                                                                 \
-      case kPackedTail: WMX_PACKED_EPK(NWV, kPackedTail); break;                                                   \
-      case kPackedPart:                                                                                            \
-        if constexpr (W8 == 0 && NWV <= 8) { /* (16 waves: the merge's registers spill; host-checked) */          \
-          if (g.arec) {                                                                                            \
-            hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, kPackedPart, 0, true>), grid, dim3(64 * NWV), 0,  \
-                               st, g.A, g.lda, g.W, g.M, g.N, g.K, g.S, g.epi, g.part, g.tail, g.tprobe, g.pslot,     \
-                               g.wscale, g.arec);                                                                   \
-            break;                                                                                                 \
-          }                                                                                                        \
-        }                                                                                                          \
-        WMX_PACKED_EPK(NWV, kPackedPart);                                                                          \
-        break;                                                                                                     \
+      case kPackedPart: WMX_PACKED_EPK(NWV, kPackedPart); break;                                                   \
       case kPackedGelu: WMX_PACKED_EPK(NWV, kPackedGelu); break;                                                   \
       default: WMX_PACKED_EPK(NWV, kPackedGeneric); break;                                                         \
     }                                                                                                              \
@@ -2738,26 +2025,9 @@ static void launch_packed_nct(int nct, const PackedCall& g, hipStream_t st) {
   else launch_packed_mt<T, 2, W8>(g, st);
 }
 
-// the tail's reducers and its single normalising workgroup: S <= 8 slices, rows of <= 5 quads per lane, one
-// counter per column group plus one, at most 8 waves per workgroup
-bool packed_tail_ok(int M, int N, int K, int S) {
-  if (S < 2 || S > 8 || N % 4 != 0 || N > 256 * kTailQpl || K % 32 != 0 || M < 1) return false;
-  if ((long)S * M * N * 4 >= 0x7fffffffL) return false;  // 32-bit buffer offsets
-  const int mt = (std::min(M, 128) + 15) / 16;
-  const int mtc = mt <= 4 ? mt : (mt <= 6 ? 6 : 4);
-  const int nct = mt > 4 ? 2 : packed_nct(M, N, K);
-  const long groups = (long)((N + 16 * nct - 1) / (16 * nct)) * ((M + mtc * 16 - 1) / (mtc * 16));
-  if (groups + 1 > packed_tail_counters()) return false;
-  const int kps = (K / 32 + S - 1) / S, per4 = (kps + 3) / 4;
-  return per4 <= 8;
-}
-
 void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
   WMX_CHECK(g.M >= 1 && g.K % 32 == 0 && g.S >= 1, "packed gemm: shape");
   WMX_CHECK(g.S == 1 || g.part != nullptr, "packed gemm: partial buffer required for S > 1");
-  WMX_CHECK(g.tail.cnt == nullptr ||
-                (packed_tail_ok(g.M, g.N, g.K, g.S) && g.tail.x && g.tail.g && g.tail.b && g.tail.out),
-            "packed gemm: reduction tail shape");
   WMX_CHECK(g.nct == 0 || g.nct == 1 || g.nct == 2 || g.nct == 4, "packed gemm: column tiles per workgroup");
   WMX_CHECK((g.epi.kind != EPI_RESID_STATS && g.epi.kind != EPI_LNFOLD_GELU16) ||
                 (g.S == 1 && g.N % 16 == 0 && g.epi.stats && g.epi.ldc % 4 == 0 &&
@@ -2765,12 +2035,8 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
                                                   : (g.epi.out16 != nullptr && g.N <= 2048))),
             "packed gemm: folded-LayerNorm epilogue arguments");
   const bool w8 = g.wscale != nullptr;
-  WMX_CHECK(!g.arec || (!w8 && g.S > 1 && g.tail.cnt == nullptr && g.K % 64 == 0 && g.lda == g.K &&
-                        packed_plan(g.M, g.N, g.K, g.S, g.nct, false).NW <= 8),
-            "packed gemm: record-merge A needs 16-bit weights, split-K partials, lda == K and <= 8 waves");
-  WMX_CHECK(!w8 || (g.K % 64 == 0 && g.tail.cnt == nullptr && g.epi.kind != EPI_RESID_STATS &&
-                    g.epi.kind != EPI_LNFOLD_GELU16),
-            "packed gemm: 8-bit weights need K % 64 == 0 and no folded-LayerNorm / in-launch tail epilogue");
+  WMX_CHECK(!w8 || (g.K % 64 == 0 && g.epi.kind != EPI_RESID_STATS && g.epi.kind != EPI_LNFOLD_GELU16),
+            "packed gemm: 8-bit weights need K % 64 == 0 and no folded-LayerNorm epilogue");
   const int nct = g.nct ? g.nct : packed_nct(g.M, g.N, g.K);
   // (8-bit weights: e4m3 bytes (w8kind 1, the fp8 decode) or int8 bytes (w8kind 2, the CTranslate2 int8 grid))
   const int kind = w8 ? (g.w8kind == 2 ? 2 : 1) : 0;
@@ -2786,198 +2052,6 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
   WMX_HIP(hipGetLastError());
 }
 
-// ------------------------------------------------------------------------------------------------
-// Decode MLP in one launch: fc1 (+bias, GELU) -> fc2 split-K partials, the fc1 -> fc2 edge handed off inside the
-// launch (the persistent-layer engine's premise, MI355X_MICROARCH.md "engine-vs-launches" / "prefetch-credit",
-// tried on this one edge).  Workgroup b (1024 threads, one per CU):
-//   phase A  fc1 column tiles 2b, 2b+1 over the whole K = d (16 waves x up to 3 k-steps);
-//   phase B  fc2 column group cg = b % (d/64) (4 tiles) over K slice sp = b / (d/64) (d/2 wide, 8 slices).
-// The K slice sp of fc2 is exactly the fc1 output of workgroups [sp d/64, (sp+1) d/64), so each slice is one
-// group of d/64 producers and d/64 consumers.  Every workgroup issues its phase-B weight loads together with its
-// phase-A loads (the weights do not depend on the hand-off), stores GELU(fc1) write-through (sc1), drains, and
-// adds 1 to its slice's monotonic counter behind a workgroup barrier; one lane polls the counter with sc1 loads
-// until the slice's generation is complete, and every wave then reads the slice with sc1 loads (the hand-off of
-// MI355X_MICROARCH.md's sc1 table, first row).  Partials part[8][M][d] feed reduce_ln as in the split form.
-// ------------------------------------------------------------------------------------------------
-constexpr int kMlpNW = 16, kMlpS = 8, kMlpKA = 3, kMlpKB = 2;
-typedef unsigned int mlp_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t mlp_rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
-}
-
-template <DT T>
-__global__ __launch_bounds__(64 * kMlpNW) void mlp_fused_kernel(MlpCall c) {
-  constexpr int MT = 2, NA = 2, NB = 4, NW = kMlpNW;
-  constexpr int LDA_ = 16 * NA + 1, LDB_ = 16 * NB + 1;
-  constexpr int RED = (NW * MT * 16 * LDA_ > (NW / 2) * MT * 16 * LDB_) ? NW * MT * 16 * LDA_ : (NW / 2) * MT * 16 * LDB_;
-  __shared__ float red[RED];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const unsigned long long probe_t0 = (c.tprobe && tid == 0) ? probe_clock() : 0ull;
-  const int d = c.d, M = c.M;
-  const int ksA = d >> 5, ntA = (4 * d) >> 4;          // fc1: K = d, N = 4d
-  const int ksB = (4 * d) >> 5, ntB = d >> 4;          // fc2: K = 4d, N = d
-  const int cgn = d / (16 * NB), kpsB = ksB / kMlpS;   // fc2 column groups (= producers per slice), k-steps per slice
-  const int b = blockIdx.x, sp = b / cgn, cg = b - sp * cgn;
-  // ---- every load that does not depend on the hand-off: fc1 weights + rows, fc2 weights, fc1 bias ----
-  u16x8 wa[kMlpKA][NA], aa[kMlpKA][MT], wb[kMlpKB][NB];
-#pragma unroll
-  for (int j = 0; j < kMlpKA; ++j) {
-    const int k = min(wave + NW * j, ksA - 1);  // clamped; MFMAs of k-steps past the end are skipped
-#pragma unroll
-    for (int t = 0; t < NA; ++t)
-      wa[j][t] = stream_load(reinterpret_cast<const u16x8*>(c.W1 + packed_w_elem(NA * b + t, ntA, ksA, k, lane)));
-#pragma unroll
-    for (int i = 0; i < MT; ++i) aa[j][i] = *reinterpret_cast<const u16x8*>(c.A + packed_a_elem(i * 16 + fr, M, c.lda, k, lane));
-  }
-#pragma unroll
-  for (int j = 0; j < kMlpKB; ++j) {
-    const int k = sp * kpsB + min(wave + NW * j, kpsB - 1);
-#pragma unroll
-    for (int t = 0; t < NB; ++t)
-      wb[j][t] = stream_load(reinterpret_cast<const u16x8*>(c.W2 + packed_w_elem(NB * cg + t, ntB, ksB, k, lane)));
-  }
-  const int qa = tid & (4 * NA - 1);  // phase-A epilogue: the thread's column quad
-  const float4 pbias = *reinterpret_cast<const float4*>(c.b1 + 32 * b + 4 * qa);
-  __builtin_amdgcn_sched_barrier(0);
-  // ---- phase A: fc1 ----
-  {
-    f32x4 acc[MT][NA];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int t = 0; t < NA; ++t) acc[i][t] = f32x4{0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < kMlpKA; ++j)
-      if (wave + NW * j < ksA)
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int t = 0; t < NA; ++t) acc[i][t] = mfma16<T>(aa[j][i], wa[j][t], acc[i][t]);
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int t = 0; t < NA; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[(wave * MT * 16 + i * 16 + fq * 4 + r) * LDA_ + t * 16 + fr] = acc[i][t][r];
-  }
-  __syncthreads();
-  const auto hr = mlp_rsrc(c.h);
-  if (tid < MT * 16 * 4 * NA) {
-    const int row = tid / (4 * NA), col = 4 * qa;
-    float v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float s = red[row * LDA_ + col + q];
-#pragma unroll
-      for (int w = 1; w < NW; ++w) s += red[(w * MT * 16 + row) * LDA_ + col + q];
-      v[q] = s;
-    }
-    if (row < M) {
-      const u16x4 h = {from_f32<T>(gelu_erf(v[0] + pbias.x)), from_f32<T>(gelu_erf(v[1] + pbias.y)),
-                       from_f32<T>(gelu_erf(v[2] + pbias.z)), from_f32<T>(gelu_erf(v[3] + pbias.w))};
-      const int off = (row * 4 * d + 32 * b + col) * 2;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(mlp_u32x2, h), hr, off, 0, 16);  // sc1
-    }
-  }
-  // ---- hand-off: drain, barrier, one arrival per workgroup; one lane polls the slice's generation ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(c.cnt) + sp, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = (old / cgn + 1) * cgn;
-    int spins = 0;
-    while ((int)(__hip_atomic_load(reinterpret_cast<unsigned*>(c.cnt) + sp, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-      if (++spins > (1 << 22)) {  // a producer never arrived: flag it and finish (wrong output, no hang)
-        __hip_atomic_store(c.cnt + kMlpS, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-  // ---- phase B: fc2 over the slice, h read write-through (sc1) ----
-  u16x8 ha[kMlpKB][MT];
-#pragma unroll
-  for (int j = 0; j < kMlpKB; ++j) {
-    const int k = sp * kpsB + min(wave + NW * j, kpsB - 1);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int off = (int)packed_a_elem(i * 16 + fr, M, 4L * d, k, lane) * 2;
-      ha[j][i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(hr, off, 0, 16));
-    }
-  }
-  // k-steps past the slice's end: zero weight operand, MFMA unconditional (a guarded MFMA let the compiler sink
-  // the sc1 loads into the guard, one round trip per k-step)
-#pragma unroll
-  for (int j = 0; j < kMlpKB; ++j) {
-    const bool ok = wave + NW * j < kpsB;
-#pragma unroll
-    for (int t = 0; t < NB; ++t) wb[j][t] = ok ? wb[j][t] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  f32x4 acc[MT][NB];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int t = 0; t < NB; ++t) acc[i][t] = f32x4{0, 0, 0, 0};
-#pragma unroll
-  for (int j = 0; j < kMlpKB; ++j)
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int t = 0; t < NB; ++t) acc[i][t] = mfma16<T>(ha[j][i], wb[j][t], acc[i][t]);
-  // two-step cross-wave sum: waves 8..15 store, waves 0..7 add theirs, then 8 slots per output
-  constexpr int NH = NW / 2;
-  if (wave >= NH) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int t = 0; t < NB; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          red[((wave - NH) * MT * 16 + i * 16 + fq * 4 + r) * LDB_ + t * 16 + fr] = acc[i][t][r];
-  }
-  __syncthreads();
-  if (wave < NH) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int t = 0; t < NB; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[(wave * MT * 16 + i * 16 + fq * 4 + r) * LDB_ + t * 16 + fr] += acc[i][t][r];
-  }
-  __syncthreads();
-  if (tid < MT * 16 * 4 * NB) {
-    const int row = tid / (4 * NB), col = 4 * (tid & (4 * NB - 1));
-    if (row < M) {
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float s = red[row * LDB_ + col + q];
-#pragma unroll
-        for (int w = 1; w < NH; ++w) s += red[(w * MT * 16 + row) * LDB_ + col + q];
-        v[q] = s;
-      }
-      *reinterpret_cast<float4*>(c.part + ((long)sp * M + row) * d + NB * 16 * cg + col) = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  }
-  if (c.tprobe && tid == 0) probe_record(c.tprobe, *c.pslot, probe_t0);
-}
-
-bool mlp_fused_ok(int M, int d) { return M >= 1 && M <= 32 && d % 64 == 0 && d >= 256 && d <= 1536; }
-
-void launch_mlp_fused(DT dt, const MlpCall& c, hipStream_t st) {
-  WMX_CHECK(mlp_fused_ok(c.M, c.d) && c.A && c.W1 && c.b1 && c.W2 && c.h && c.part && c.cnt && c.lda >= c.d,
-            "fused mlp: shape / arguments");
-  const dim3 grid(c.d / 8);  // fc1 column groups of 32 = (d / 64 fc2 column groups) x 8 K slices
-  if (dt == DT::BF16)
-    hipLaunchKernelGGL(mlp_fused_kernel<DT::BF16>, grid, dim3(64 * kMlpNW), 0, st, c);
-  else
-    hipLaunchKernelGGL(mlp_fused_kernel<DT::F16>, grid, dim3(64 * kMlpNW), 0, st, c);
-  WMX_HIP(hipGetLastError());
-}
 
 template <DT T, int BM, int BN, int WM, int WN>
 static void launch_cfg(const GemmCall& g, hipStream_t st) {
@@ -3029,8 +2103,7 @@ static int g256_grid(int tiles) {
       n = 256;
     return std::max(8, n / 8 * 8);
   }();
-  static const bool one_tile = getenv("WMX_G256_NONPERSIST") != nullptr;  // A/B switch: one tile per workgroup
-  return one_tile ? tiles : std::min(tiles, cus);
+  return std::min(tiles, cus);
 }
 
 template <DT T>
@@ -3067,6 +2140,8 @@ static void launch_t(const GemmCall& g, hipStream_t st) {
   }
   if (g.tile == TILE_256) {
     WMX_CHECK(g.K % WMX_G256_BK == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0, "gemm256: K / leading dimensions");
+    // the ring's per-lane element offsets are 32-bit (m lda + chunk, n ldw + chunk; the K-tile offset is added as long)
+    WMX_CHECK(g256_offsets_fit(g.M, g.N, g.lda, g.ldw), "gemm256: M x lda or N x ldw exceeds 32-bit element offsets");
     WMX_CHECK(g.epi.kind != EPI_CROSSKV || (g.epi.d % 256 == 0 && g.epi.xt % 4 == 0), "gemm256: cross K/V shape");
     const bool lns = g.epi.kind == EPI_RESID32_LNS || g.epi.kind == EPI_GELU_POS32_LNS;
     const bool lnf = g.epi.kind == EPI_LNF_STORE16 || g.epi.kind == EPI_LNF_GELU16;

@@ -89,6 +89,10 @@ __host__ __device__ inline long crossv8_off(int t, int c) {
 enum GemmTile { TILE_128x128 = 0, TILE_64x64 = 1, TILE_32x64 = 2, TILE_SKINNY = 3, TILE_256 = 4 };
 // K depth of one staged slice of the 256 x 256 GEMM (gemm256_kernel): 64 = the half-tile ring of whole 128-B lines
 // (default, K % 64 == 0), 32 = the 32-deep slice ring (every 128-B line fetched in two halves one slice apart)
+// gemm256's ring addresses a lane's rows with 32-bit element offsets (row * ld + chunk): every row base must fit
+inline bool g256_offsets_fit(long M, long N, long lda, long ldw) {
+  return (M - 1) * lda + 64 < (1L << 32) && (N - 1) * ldw + 64 < (1L << 32);
+}
 #ifndef WMX_G256_BK
 #define WMX_G256_BK 64
 #endif
@@ -153,8 +157,8 @@ __host__ __device__ inline long packed8_index(long n, long k, long K) {
 // (N padded entries 0), and optionally rm = the dequantized row-major [N][K] 16-bit copy (many-row passes)
 // the CTranslate2 int8 grid (model dtype I8): per-row CT2 scales (derived: 127 / max|row|, or given), int8 bytes in the
 // packed8_index layout, the GEMM's row multipliers 1 / scale, and the row-major dequantized copy (rm, optional)
-void launch_i8_quantize(DT dt, const uint16_t* src, int N, int K, float* ct2s, bool derive, uint8_t* q8, float* mult,
-                        uint16_t* rm, hipStream_t st);
+void launch_i8_quantize(DT dt, const uint16_t* src, int N, int K, float* ct2s, uint8_t* q8, float* mult, uint16_t* rm,
+                        hipStream_t st);
 void launch_w8_quantize(DT dt, const uint16_t* src, int N, int K, uint8_t* q8, float* scale, uint16_t* rm,
                         hipStream_t st);
 // fp8 cross K / V^T images: per (layer, kv, window, head) image one power-of-two scale (mx8_exp of the image's
@@ -167,17 +171,6 @@ void launch_crosskv_quant(const uint16_t* src, uint8_t* dst, float* scale, int L
 
 // C[M][N] = A[M][K] . Wp^T.  S == 1: epilogue applied in-kernel.  S > 1: K is split over S workgroup slices and
 // each writes raw fp32 partials part[s][M][N] (no bias); the consumer sums them in slice order (deterministic).
-// in-launch split-K reduction + residual + LayerNorm of a partial-output packed GEMM (decode step): the last
-// of a column group's S slices sums them into x (x += bias + sum_s part[s]); the last column group normalises
-// every row into out (LN(x) * g + b).  cnt: >= packed_tail_counters() zeroed ints, re-armed by the kernel.
-struct RedTail {
-  const float* bias = nullptr;
-  float* x = nullptr;
-  const float* g = nullptr;
-  const float* b = nullptr;
-  uint16_t* out = nullptr;
-  int* cnt = nullptr;
-};
 struct PackedCall {
   const uint16_t* A;
   long lda;
@@ -187,12 +180,7 @@ struct PackedCall {
   Epi epi;
   const float* wscale = nullptr;  // 8-bit weights: per-row scales (result = scale[n] * acc, before the epilogue)
   int w8kind = 1;                 // with wscale: 1 e4m3 bytes (fp8 decode), 2 int8 bytes (CTranslate2 int8 grid)
-  // A = the merge of a decode cross attention's two key-chunk records (DecAttnArgs::rec_o / rec_ml): A points at
-  // rec_o (fp32 [2][M][K], lda = K) and arec at rec_ml ([2][M][K / 64]); the lane's 8 k-values of a row are merged
-  // exactly as the cross attention's own merge does and rounded to 16 bits (16-bit weights, split-K partials only)
-  const float2* arec = nullptr;
   float* part = nullptr;
-  RedTail tail;  // tail.cnt != nullptr (with S > 1): reduce + LayerNorm in the same launch
   // in-situ probe: [slot][workgroup][start, end] wall-clock ticks (probe_record) at slot *pslot, or null
   unsigned long long* tprobe = nullptr;
   const int* pslot = nullptr;
@@ -205,25 +193,6 @@ struct PackedPlan {
   int MT, NCT, NW, KU, gx, gz;
 };
 PackedPlan packed_plan(int M, int N, int K, int S, int nct = 0, bool w8 = false);
-// decode MLP in one launch (fc1 + bias + GELU -> fc2 split-K partials, the edge handed off in-launch):
-// part[8][M][d] raw fc2 partials (no bias) for reduce_ln, h [M][4d] the GELU(fc1) rows (write-through),
-// cnt: kMlpCounters zeroed ints per context (8 monotonic slice counters + an error word set on a poll timeout)
-struct MlpCall {
-  const uint16_t* A = nullptr;  // LN(x) rows, 16-bit
-  long lda = 0;
-  const uint16_t* W1 = nullptr;  // packed fc1 [4d][d]
-  const float* b1 = nullptr;
-  const uint16_t* W2 = nullptr;  // packed fc2 [d][4d]
-  uint16_t* h = nullptr;
-  float* part = nullptr;
-  int* cnt = nullptr;
-  int M = 0, d = 0;
-  unsigned long long* tprobe = nullptr;
-  const int* pslot = nullptr;
-};
-constexpr int kMlpCounters = 16, kMlpSlices = 8;
-bool mlp_fused_ok(int M, int d);
-void launch_mlp_fused(DT dt, const MlpCall& c, hipStream_t st);
 // the element offsets a packed-GEMM lane reads, shared by gemm_packed_kernel and the host-side extent check
 // (packed_extent): k-step range of one wave, the B fragment of column tile t (clamped to the last tile) and the A
 // fragment of row `row` (clamped to the last row)
@@ -247,9 +216,6 @@ struct PackedExtent {
   long w_end, a_end, part_end, stray_ksteps;
 };
 PackedExtent packed_extent(int M, int N, int K, int S, long lda, int nct = 0, bool w8 = false);
-// whether a partial-output launch of this shape can carry the RedTail; counters the tail needs
-bool packed_tail_ok(int M, int N, int K, int S);
-constexpr int packed_tail_counters() { return 4096; }
 int packed_nct(int M, int N, int K);
 // split count for a partial-output launch (<= cap_elems / (M*N) partial slices)
 int packed_splits(int M, int N, int K, long cap_elems);
@@ -290,8 +256,6 @@ void launch_unpack_packed(const uint16_t* packed, uint16_t* rowmajor, int N, int
 void launch_embed_ln(DT dt, const uint16_t* tok_emb, const uint16_t* pos_emb, const int* hist, long hist_ld, int R,
                      const int* pad, const int* slot0, const float* g, const float* b, int d, float* x, uint16_t* out,
                      hipStream_t st, int V, float2* stats = nullptr, long stats_ld = 0);
-// one wave idles on the stream for `ticks` device wall-clock ticks (a phase offset between context groups)
-void launch_spin(unsigned long long ticks, hipStream_t st);
 // LayerNorm (g, b) folded into the projection W (+ bias): packed Wp = W diag(g), c1 = Wp 1, c2 = bias + W b
 // (rowmajor: Wp is written row-major [N][K] instead of packed: the encoder's gemm256 operand)
 void launch_fold_ln(DT dt, const uint16_t* Wrm, const float* g, const float* b, const float* bias, int N, int K,
@@ -346,19 +310,7 @@ struct DecAttnArgs {
   int Tk;
   int rows_per_win;    // rows sharing one encoder window (beam)
   int* xcnt = nullptr; // key-chunked launches: one arrival counter per (window, head), zero between launches
-  int xcd_remap = 0;   // cross attention: place the workgroups of one head on one or two XCDs (launch_cross_t)
   unsigned long long* tprobe = nullptr;  // [slot][workgroup][start, end] wall-clock ticks (probe_record), or null
-  // diagnostic phase stamps of the decode cross attention (WMX_PHASE_PROBE with the in-situ probe): [slot][workgroup]
-  // [kPhaseStamps] wall-clock ticks at the kernel's phase boundaries (wave 0), the last two words its XCC_ID / HW_ID
-  unsigned long long* pphase = nullptr;
-  // decode cross attention with the fused query projection: every wave's query-projection loads are issued before any
-  // wave's K loads (a workgroup barrier between the two batches), so no projection load queues behind K streams
-  int issue_bar = 0;
-  // decode cross attention, 2 key chunks (KS == 2): the chunks' records go to the consumer instead of an in-launch
-  // merge -- rec_o [2][R][d] fp32 (each chunk's unnormalised output), rec_ml [2][R][H] (max, sum) -- and the cross
-  // out-projection merges them in its A loads (PackedCall::arec); no arrival ticket, no last-arriver merge
-  float* rec_o = nullptr;
-  float2* rec_ml = nullptr;
   // decode step fed by split-K partials (qS > 0): q = bias + sum_s qpart[s*qpart_stride + m*qpart_ld + col]
   // (self attention: columns [0,d) q, [d,2d) k, [2d,3d) v; k and v are also written to the cache at slot0)
   const float* qpart = nullptr;
@@ -388,7 +340,6 @@ void launch_self_attn(DT dt, const DecAttnArgs& a, hipStream_t st);
 // ws: cross_attn_ws_floats(H, nwin, nq_max) floats for the key-chunk records (decode steps), a.xcnt: nwin*H
 // zero-initialised ints (the merging workgroup re-arms its counter)
 size_t cross_attn_ws_floats(int H, int nwin, int nq_max);
-int cross_attn_key_chunks(const DecAttnArgs& a);
 void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st);
 // raw cross-attention scores of selected heads (alignment): out [nh][R*Tn][Tk] f32
 void launch_cross_scores(DT dt, const DecAttnArgs& a, const int* heads_layer_local, int nh, float* out, hipStream_t st);

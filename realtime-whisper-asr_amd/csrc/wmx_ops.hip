@@ -322,20 +322,24 @@ void launch_w8_quantize(DT dt, const uint16_t* src, int N, int K, uint8_t* q8, f
 
 // ---------------- the CTranslate2 int8 grid (model dtype I8) ----------------
 // One wave per weight row n of a packed 16-bit [N][K] matrix: the CT2 row scale s = 127 / max|w| (1 for an all-zero
-// row; CTranslate2's int8 quantization, oracle/whisper_np.py int8_rows) written to ct2s[n] when `derive`, else read
+// row; CTranslate2's int8 quantization, oracle/whisper_np.py int8_rows) written to ct2s[n] where ct2s[n] is 0 (not
+// given), else ct2s[n] read as given (a CT2 int8 checkpoint's own weight_scale).  The given / derived state is the
+// scale array itself, which lives in the broadcast parameter region: a rank that receives the arena keeps the
+// sender's scales bit for bit.
 // from it (a CT2 int8 checkpoint's own weight_scale); q = rint(w s) clamped to [-127, 127] as int8 bytes in the
 // packed8_index layout, the GEMM's row multiplier 1 / s, and the row-major copy q / s rounded to 16 bits.  With the
 // 16-bit weight w = round16(q_ckpt / s_ckpt) and the checkpoint's scale, |q_ckpt| <= 127 makes rint(w s) = q_ckpt
 // exactly (the relative rounding of w is <= 2^-9, so |w s - q_ckpt| <= 127 / 512 < 1/2).
 template <DT T>
 __global__ __launch_bounds__(256) void i8_quantize_kernel(const uint16_t* __restrict__ src, int N, int Np, int K,
-                                                          float* __restrict__ ct2s, int derive, uint8_t* __restrict__ q8,
+                                                          float* __restrict__ ct2s, uint8_t* __restrict__ q8,
                                                           float* __restrict__ mult, uint16_t* __restrict__ rm) {
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (n >= Np) return;  // (wave-uniform)
   float s = 1.f;
   if (n < N) {
-    if (derive) {
+    s = ct2s[n];
+    if (!(s > 0.f)) {  // (wave-uniform) not given: CT2's rule
       float am = 0.f;
       for (int k = 8 * lane; k < K; k += 512) {
         const u16x8 h = *reinterpret_cast<const u16x8*>(src + packed_index(n, k, K));
@@ -345,8 +349,6 @@ __global__ __launch_bounds__(256) void i8_quantize_kernel(const uint16_t* __rest
       am = wave_max(am);
       s = am > 0.f ? 127.f / am : 1.f;
       if (lane == 0) ct2s[n] = s;
-    } else {
-      s = ct2s[n];
     }
   }
   for (int k = 8 * lane; k < K; k += 512) {
@@ -367,16 +369,16 @@ __global__ __launch_bounds__(256) void i8_quantize_kernel(const uint16_t* __rest
   if (lane == 0) mult[n] = n < N ? 1.f / s : 0.f;
 }
 
-void launch_i8_quantize(DT dt, const uint16_t* src, int N, int K, float* ct2s, bool derive, uint8_t* q8, float* mult,
-                        uint16_t* rm, hipStream_t st) {
+void launch_i8_quantize(DT dt, const uint16_t* src, int N, int K, float* ct2s, uint8_t* q8, float* mult, uint16_t* rm,
+                        hipStream_t st) {
   WMX_CHECK(K % 64 == 0 && N >= 1, "int8 quantize: K must be a multiple of 64");
   const int Np = (N + 15) / 16 * 16;
   if (dt == DT::BF16)
     hipLaunchKernelGGL(i8_quantize_kernel<DT::BF16>, dim3(cdiv(Np, 4)), dim3(256), 0, st, src, N, Np, K, ct2s,
-                       derive ? 1 : 0, q8, mult, rm);
+                       q8, mult, rm);
   else
     hipLaunchKernelGGL(i8_quantize_kernel<DT::F16>, dim3(cdiv(Np, 4)), dim3(256), 0, st, src, N, Np, K, ct2s,
-                       derive ? 1 : 0, q8, mult, rm);
+                       q8, mult, rm);
   WMX_HIP(hipGetLastError());
 }
 
@@ -836,8 +838,7 @@ void launch_reduce_ln(DT dt, const float* part, int S, const float* bias, float*
                       const int* pslot) {
   WMX_CHECK(d <= 2 * kRedThreads && S >= 1 && S <= kRedMaxS, "reduce_ln: width / split count");
   const long pstride = (long)rows * d;
-  static const bool legacy = getenv("WMX_REDLN_LEGACY") != nullptr;  // A/B switch for tuning runs
-  if (!legacy && d % 4 == 0 && d <= 4096) {
+  if (d % 4 == 0 && d <= 4096) {
     const int nt = ((d / 4 + 63) / 64) * 64;
     if (dt == DT::BF16)
       hipLaunchKernelGGL(reduce_ln4_kernel<DT::BF16>, dim3(rows), dim3(nt), 0, st, part, S, pstride, bias, x, g, b,
@@ -865,17 +866,6 @@ __device__ inline float prng_u(uint64_t key, uint64_t i) {
   z = z ^ (z >> 31);
   const float k = (float)(uint32_t)(z >> 40);
   return __fsub_rn(__fmul_rn(k, 1.1920928955078125e-7f), 1.0f);
-}
-
-// ---------------- stream phase offset: one wave idles for `ticks` device wall-clock ticks ----------------
-__global__ void spin_kernel(unsigned long long ticks) {
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
-}
-
-void launch_spin(unsigned long long ticks, hipStream_t st) {
-  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, ticks);
-  WMX_HIP(hipGetLastError());
 }
 
 template <DT T>

@@ -26,7 +26,7 @@
 #include <unistd.h>
 #include <vector>
 
-#include "../../include/wmx.h"
+#include "../../include/wmx_diag.h"  // (includes wmx.h)
 #include "wmx_common.h"
 #include "wmx_decode.h"
 #include "wmx_kernels.h"
@@ -164,7 +164,6 @@ struct Model {
   bool i8 = false;
   bool kv8 = false;  // the fp8 cross K / V images (the MX8 model's fp8 decode)
   float* i8stok = nullptr;  // CT2 scales of the token embedding (the logits projection)
-  std::set<std::string> i8_given;  // weights whose CT2 scales were set (wmx_model_set_row_scales), not derived
   std::map<std::string, std::pair<float*, long>> i8_scale_dst;  // weight name -> (its scale rows, row count)
   size_t param_bytes = 0;  // the arena's parameter region [0, param_bytes): what a weight broadcast must carry
   char* arena = nullptr;
@@ -304,7 +303,7 @@ static void build_model(Model& m) {
     P.add(&L.c2fc1, 4 * da);
   }
   for (auto& L : m.dec) {
-    if (!m.fold && !m.mixed) break;  // the folded copies exist only for the folded / mixed steps
+    if (!m.mixed) break;  // the folded copies exist only for the mixed step
     P.add(&L.fqkv, (size_t)3 * dt * dt);
     P.add(&L.fcq, (size_t)dt * dt);
     P.add(&L.ffc1, (size_t)4 * dt * dt);
@@ -513,7 +512,7 @@ static void prepare_fold(Model& m) {
     }
     WMX_HIP(hipStreamSynchronize(m.st));
   }
-  if (!m.fold && !m.mixed) return;
+  if (!m.mixed) return;
   const int dt = m.d.n_text_state;
   for (auto& L : m.dec) {
     launch_fold_ln(m.dt, L.rqkv, L.ln1g, L.ln1b, L.bqkv, 3 * dt, dt, L.fqkv, L.c1qkv, L.c2qkv, m.st);
@@ -541,25 +540,20 @@ static void prepare_mx8(Model& m) {
 static void prepare_w8(Model& m) {
   if (!m.w8) return;
   const int dt = m.d.n_text_state;
-  if (m.i8) {  // the CTranslate2 int8 grid: int8 bytes with CT2's row scales (given, or derived by CT2's rule)
-    auto given = [&](const std::string& nm) { return m.i8_given.count(nm) > 0; };
-    for (int i = 0; i < (int)m.dec.size(); ++i) {
-      DecLayer& L = m.dec[i];
-      const std::string p = "decoder.layers." + std::to_string(i);
-      // (the fused q | k | v rows: derived only when none of the three was given; a checkpoint gives all three)
-      const bool gqkv = given(p + ".self_attn.q_proj.weight") && given(p + ".self_attn.k_proj.weight") &&
-                        given(p + ".self_attn.v_proj.weight");
-      launch_i8_quantize(m.dt, L.wqkv, 3 * dt, dt, L.i8sqkv, !gqkv, L.q8qkv, L.s8qkv, L.rqkv, m.st);
-      launch_i8_quantize(m.dt, L.wo, dt, dt, L.i8so, !given(p + ".self_attn.out_proj.weight"), L.q8o, L.s8o, L.ro, m.st);
-      launch_i8_quantize(m.dt, L.wcq, dt, dt, L.i8scq, !given(p + ".encoder_attn.q_proj.weight"), L.q8cq, L.s8cq, L.rcq,
-                         m.st);
-      launch_i8_quantize(m.dt, L.wco, dt, dt, L.i8sco, !given(p + ".encoder_attn.out_proj.weight"), L.q8co, L.s8co,
-                         L.rco, m.st);
-      launch_i8_quantize(m.dt, L.wfc1, 4 * dt, dt, L.i8sfc1, !given(p + ".fc1.weight"), L.q8fc1, L.s8fc1, L.rfc1, m.st);
-      launch_i8_quantize(m.dt, L.wfc2, dt, 4 * dt, L.i8sfc2, !given(p + ".fc2.weight"), L.q8fc2, L.s8fc2, L.rfc2, m.st);
+  if (m.i8) {
+    // the CTranslate2 int8 grid: int8 bytes with CT2's row scales.  A row's scale is given (a CT2 checkpoint's
+    // weight_scale, wmx_model_set_row_scales) when its entry is > 0, else derived by CT2's rule and stored; a weight
+    // set after its scales zeroes them (wmx_model_set_tensor).  The state is the scale array itself, in the
+    // broadcast parameter region, so every rank of a weight broadcast derives nothing the sender did not.
+    for (DecLayer& L : m.dec) {
+      launch_i8_quantize(m.dt, L.wqkv, 3 * dt, dt, L.i8sqkv, L.q8qkv, L.s8qkv, L.rqkv, m.st);
+      launch_i8_quantize(m.dt, L.wo, dt, dt, L.i8so, L.q8o, L.s8o, L.ro, m.st);
+      launch_i8_quantize(m.dt, L.wcq, dt, dt, L.i8scq, L.q8cq, L.s8cq, L.rcq, m.st);
+      launch_i8_quantize(m.dt, L.wco, dt, dt, L.i8sco, L.q8co, L.s8co, L.rco, m.st);
+      launch_i8_quantize(m.dt, L.wfc1, 4 * dt, dt, L.i8sfc1, L.q8fc1, L.s8fc1, L.rfc1, m.st);
+      launch_i8_quantize(m.dt, L.wfc2, dt, 4 * dt, L.i8sfc2, L.q8fc2, L.s8fc2, L.rfc2, m.st);
     }
-    launch_i8_quantize(m.dt, m.tok_emb, m.d.n_vocab, dt, m.i8stok, !given("decoder.embed_tokens.weight"), m.tok8,
-                       m.tok8s, nullptr, m.st);
+    launch_i8_quantize(m.dt, m.tok_emb, m.d.n_vocab, dt, m.i8stok, m.tok8, m.tok8s, nullptr, m.st);
     WMX_HIP(hipStreamSynchronize(m.st));
     return;
   }
@@ -710,8 +704,6 @@ struct Ctx {
   float* sel_ws = nullptr;
   float* xa_ws = nullptr;
   int* xa_cnt = nullptr;
-  int* red_cnt = nullptr;  // RedTail arrival counters (packed GEMM with in-launch reduce + LayerNorm)
-  int* mlp_cnt = nullptr;  // fused-MLP slice counters + error word (launch_mlp_fused)
   int* nf_err = nullptr;   // non-finite decode guard (RuleOpts::err): 0, or 1 + row + 1024 * slot of the first hit
   uint32_t* mask = nullptr;
   // alignment
@@ -743,19 +735,13 @@ struct Ctx {
   int probe_kernel = -1, probe_layer = 0;
   unsigned long long* probe_buf = nullptr;
   unsigned long long* cur_probe = nullptr;
-  // diagnostic phase stamps of the probed layer's cross attention ([T][kProbeWG][kPhaseStamps]; WMX_PHASE_PROBE=1 at
-  // wmx_ctx_set_probe, read by wmx_ctx_probe_phases), or null
-  unsigned long long* phase_buf = nullptr;
 
   double probe_bytes[kProbeLaunches] = {0}, wall_khz = 0;
   int probe_slots[2] = {0, 0};  // [first, last) decode slot probed by the last transcribe
-  double start_delay_us = 0;    // wmx_ctx_set_phase_offset: idle time before the decode loop (group phase offset)
   std::shared_ptr<struct Lockstep> lockstep;  // wmx_ctx_set_lockstep: the decode loops of the group start together
   bool lockstep_ok = false;                   // the last call's barrier saw every member
   long lockstep_timeouts = 0;                 // chunk barriers that timed out (this member then left the barrier)
   bool xq_fused = true;         // decode step: cross-q projection inside the cross attention (WMX_XQ_FUSED=0: off)
-  bool mlp_fused = false;       // decode step: fc1 -> fc2 in one launch, in-launch hand-off (WMX_MLP_FUSED=1)
-  bool xa_recsplit = false;     // decode step: cross-attention records merged by the cross out-projection (env at creation)
   float stage_ms[7] = {0};
   int last_steps = 0;
   // parity recorder (wmx_ctx_record): [cap][R][V] raw logits + [cap][R][2] selections of the last transcribe
@@ -876,8 +862,6 @@ static void alloc_ctx(Ctx& c) {
   // key-chunk records: chunked launches have <= 16 queries per window (more use one chunk, no records)
   P.add(&c.xa_ws, cross_attn_ws_floats(d.n_text_head, B, 16));
   P.add(&c.xa_cnt, (size_t)B * d.n_text_head);
-  P.add(&c.red_cnt, (size_t)packed_tail_counters());
-  P.add(&c.mlp_cnt, (size_t)kMlpCounters);
   P.add(&c.nf_err, 4);
   P.add(&c.probe_buf, (size_t)kProbeLaunches * T * kProbeWG * 2);
   P.add(&c.mask, (V + 31) / 32);
@@ -940,8 +924,7 @@ static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ld
     launch_gemm(c.dt, g, c.st);
     return;
   }
-  static const bool no_g256 = getenv("WMX_NO_G256") != nullptr;  // A/B switch for tuning runs
-  if (!no_g256 && M >= 4096 && K % WMX_G256_BK == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
+  if (M >= 4096 && K % WMX_G256_BK == 0 && lda % 8 == 0 && ldw % 8 == 0 && g256_offsets_fit(M, N, lda, ldw) &&
       (e.kind != EPI_CROSSKV || e.d % 256 == 0) && e.kind != EPI_QKV_CACHE) {
     // encoder / conv front end / cross-K/V: 256x256 ping-pong tile, every tile on its own CU
     g.tile = TILE_256;
@@ -949,12 +932,8 @@ static void gemm(Ctx& c, const uint16_t* A, long lda, const uint16_t* W, long ld
     return;
   }
   // rows from which the 128x128 tile is used (the word-alignment forward, ~900 rows per context group: align stage
-  // 15.7-16.3 vs 16.9-18.8 ms with 64x64 tiles, profiles/r03r_align_m128_ab.txt); WMX_GEMM_M128 overrides
-  static const int m128 = [] {
-    const char* v = getenv("WMX_GEMM_M128");
-    return v ? atoi(v) : 512;
-  }();
-  if (M >= m128) {
+  // 15.7-16.3 vs 16.9-18.8 ms with 64x64 tiles, profiles/r03r_align_m128_ab.txt)
+  if (M >= 512) {
     g.tile = TILE_128x128;
     bm = 128;
     bn = 128;
@@ -1004,8 +983,7 @@ static void set_w(PackedCall& g, const uint16_t* Wp, W8 w8) {
 
 static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, const Epi& e,
                    const uint16_t* Wrm = nullptr, W8 w8 = {}) {
-  static const bool packed_only = getenv("WMX_PREFILL_PACKED") != nullptr;  // A/B switch for tuning runs
-  if (Wrm && M > 256 && !packed_only) {  // (fp8 decode: Wrm holds the dequantized 8-bit weights)
+  if (Wrm && M > 256) {  // (fp8 decode: Wrm holds the dequantized 8-bit weights)
     gemm(c, A, lda, Wrm, K, M, N, K, e);
     return;
   }
@@ -1024,11 +1002,9 @@ static void gemm_p(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int 
 }
 
 // decoder projection on packed weights, split-K raw partials into c.part; returns the split count
-static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, W8 w8 = {},
-                       const float2* arec = nullptr) {
+static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K, W8 w8 = {}) {
   PackedCall g;
   g.A = A;
-  g.arec = arec;
   g.lda = lda;
   set_w(g, Wp, w8);
   g.M = M;
@@ -1046,39 +1022,15 @@ static int gemm_p_part(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, 
   return g.S;
 }
 
-// decoder projection whose split-K partials feed x += bias + sum; out16 = LN(x) (reduce_ln): one packed launch
-// carrying the reduction and the LayerNorm when the shape allows (RedTail), else the GEMM and reduce_ln
+// decoder projection whose split-K partials feed x += bias + sum; out16 = LN(x): the GEMM, then reduce_ln
+// (an in-launch reduce + LayerNorm tail measured slower than the kernel boundary, 798 vs 587 ms per call, and was
+// removed in round 6)
 static void gemm_p_redln(Ctx& c, const uint16_t* A, long lda, const uint16_t* Wp, int M, int N, int K,
                          const float* bias, const float* g, const float* b, unsigned long long* redprobe = nullptr,
-                         W8 w8 = {}, int ablate = 0, const float2* arec = nullptr) {
-  // opt-in (WMX_REDLN_FUSED): measured slower than the separate reduce_ln launch, 798 vs 587 ms per call on the
-  // default bench -- the in-launch chain (sc1 partial loads, write-through x, a second arrival, the single
-  // normalising workgroup's row loads) costs ~10 us more than the kernel boundary it removes
-  static const bool fused = getenv("WMX_REDLN_FUSED") != nullptr;
-  const int S = packed_splits(M, N, K, c.part_elems);
-  if (fused && !w8.q8 && !arec && packed_tail_ok(M, N, K, S)) {
-    PackedCall p;
-    p.A = A;
-    p.lda = lda;
-    p.W = Wp;
-    p.M = M;
-    p.N = N;
-    p.K = K;
-    p.S = S;
-    p.part = c.part;
-    p.tail.bias = bias;
-    p.tail.x = c.dx;
-    p.tail.g = g;
-    p.tail.b = b;
-    p.tail.out = c.dhb;
-    p.tail.cnt = c.red_cnt;
-    launch_gemm_packed(c.dt, p, c.st);
-    return;
-  }
-  // (ablate: timing-only WMX_ABLATE bits of dec_step_fast; 16 = leave out the GEMM, 4 = leave out reduce_ln)
-  const int S2 = (ablate & 16) ? S : gemm_p_part(c, A, lda, Wp, M, N, K, w8, arec);
+                         W8 w8 = {}) {
+  const int S = gemm_p_part(c, A, lda, Wp, M, N, K, w8);
   c.cur_probe = nullptr;
-  if (!(ablate & 4)) launch_reduce_ln(c.dt, c.part, S2, bias, c.dx, g, b, c.dhb, M, N, c.st, redprobe, c.slot);
+  launch_reduce_ln(c.dt, c.part, S, bias, c.dx, g, b, c.dhb, M, N, c.st, redprobe, c.slot);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1168,8 +1120,9 @@ static void encode_layers_mx8(Ctx& c, int B) {
 // to 16 bits before the mean is removed, which adds ~2^-9 |mean| / std relative error per projection input on top of
 // the unfolded form's LN-output rounding ("Encoder LayerNorm fold").
 static bool enc_fold_rows(const Ctx& c, long rows) {
-  static const bool no_g256 = getenv("WMX_NO_G256") != nullptr;
-  return c.m->enc_fold && c.est && rows >= 4096 && !no_g256;  // the gemm256 dispatch condition of gemm()
+  // the gemm256 dispatch condition of gemm() for every folded launch (the widest A: fc2's 4 d columns)
+  const long da = c.m->d.n_audio_state;
+  return c.m->enc_fold && c.est && rows >= 4096 && g256_offsets_fit(rows, 4 * da, 4 * da, 4 * da);
 }
 
 static Epi epi_lns(Ctx& c, int kind, const float* bias, long rows) {
@@ -1311,22 +1264,10 @@ struct FwdArgs {
 
 // Decode step (Tn == 1): every projection runs on packed weights with split-K partials, and the reductions are
 // fused into the consumers -- q/k/v into self attention (which also writes the KV cache), cross q into cross
-// attention, out-proj / fc2 into reduce_ln (residual add + the next LayerNorm).  11 launches per layer.
+// attention, out-proj / fc2 into reduce_ln (residual add + the next LayerNorm).  10 launches per layer.
 // Leaves LN_final(x) of every row in c.dhb.
-// Timing-only ablation of the decode step (WMX_ABLATE, a bit mask read once; never set in a product or parity run):
-// the launches named by the set bits are left out of the step so that an A/B run measures what each kind of launch
-// costs on the critical path with the context groups running beside each other. 1 self attention, 2 cross
-// attention, 4 reduce_ln, 8 fc1 + fc2, 16 qkv / out / cross-out projections; 32 every layer's cross attention reads
-// layer 0's cross K / V images, 64 every layer streams layer 0's weights (the caches then hold them: what the HBM
-// stream of each costs). Results are wrong by construction.
-static int ablate_mask() {
-  static const int m = getenv("WMX_ABLATE") ? atoi(getenv("WMX_ABLATE")) : 0;
-  return m;
-}
-
 static void dec_step_fast(Ctx& c, const FwdArgs& f) {
   Model& m = *c.m;
-  const int ab = ablate_mask();
   const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
   const int R = f.rows;
   const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
@@ -1334,7 +1275,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
                   c.dx, c.dhb, c.st, m.d.n_vocab);
   const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
   for (int l = 0; l < Lt; ++l) {
-    DecLayer& L = m.dec[(ab & 64) ? 0 : l];
+    DecLayer& L = m.dec[l];
     const bool last = l + 1 == Lt;
     const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
     const bool prev = c.probe_kernel >= 0 && l + 1 == c.probe_layer;  // its last launch precedes the probed qkv
@@ -1342,7 +1283,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     auto pbuf = [&](int id) { return probed ? c.probe_buf + id * probe_stride : nullptr; };
     // self attention: QKV partials -> (reduce, cache write, attention) -> out-proj partials -> +x, LN2
     probe(kProbeQKV);
-    int S = (ab & 16) ? 2 : gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt, w8_of(m, L.q8qkv, L.s8qkv));
+    int S = gemm_p_part(c, c.dhb, dt, L.wqkv, R, 3 * dt, dt, w8_of(m, L.q8qkv, L.s8qkv));
     c.cur_probe = nullptr;
     DecAttnArgs a{};
     a.o = c.dao;
@@ -1363,9 +1304,9 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     a.qpart_ld = 3 * dt;
     a.qbias = L.bqkv;
     a.tprobe = pbuf(kProbeSelf);
-    if (!(ab & 1)) launch_self_attn(c.dt, a, c.st);
+    launch_self_attn(c.dt, a, c.st);
     probe(kProbeOut);
-    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut), w8_of(m, L.q8o, L.s8o), ab);
+    gemm_p_redln(c, c.dao, dt, L.wo, R, dt, dt, L.bo, L.ln2g, L.ln2b, pbuf(kProbeRedOut), w8_of(m, L.q8o, L.s8o));
     // cross attention: q partials -> (reduce, attention) -> out-proj partials -> +x, LN3; with c.xq_fused the
     // cross attention projects its own queries from LN2(x) (no cross-q launch)
     if (!c.xq_fused) {
@@ -1379,7 +1320,7 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     x.Tn = 1;
     x.H = H;
     x.d = dt;
-    set_cross_images(c, x, (ab & 32) ? 0 : l);
+    set_cross_images(c, x, l);
     x.Tk = 1500;
     x.rows_per_win = f.win_rows > 0 ? f.win_rows : c.K;
     x.qpart = c.part;
@@ -1396,62 +1337,25 @@ static void dec_step_fast(Ctx& c, const FwdArgs& f) {
     }
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
-    if (probed) {
-      x.tprobe = c.probe_buf + kProbeCross * probe_stride;
-      x.pphase = c.phase_buf;
-    }
-    // (WMX_XATTN_RECSPLIT, the 16-bit fused form with two key chunks: the chunks' records merged in the cross
-    // out-projection's A loads instead of by the last-arriving chunk: no ticket, no merge pass in the attention)
-    const float2* arec = nullptr;
-    if (c.xa_recsplit && c.xq_fused && !m.w8 && !m.fold && cross_attn_key_chunks(x) == 2 &&
-        packed_plan(R, dt, dt, packed_splits(R, dt, dt, c.part_elems), 0, false).NW <= 8) {
-      x.rec_o = c.xa_ws;
-      x.rec_ml = reinterpret_cast<float2*>(c.xa_ws + (size_t)2 * R * dt);
-      arec = x.rec_ml;
-    }
-    if (!(ab & 2)) launch_cross_attn(c.dt, x, c.xa_ws, c.st);
+    if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
+    launch_cross_attn(c.dt, x, c.xa_ws, c.st);
     probe(kProbeCrossOut);
-    gemm_p_redln(c, arec ? reinterpret_cast<const uint16_t*>(x.rec_o) : c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g,
-                 L.ln3b, pbuf(kProbeRedCrossOut), w8_of(m, L.q8co, L.s8co), ab, arec);
+    gemm_p_redln(c, c.dao, dt, L.wco, R, dt, dt, L.bco, L.ln3g, L.ln3b, pbuf(kProbeRedCrossOut),
+                 w8_of(m, L.q8co, L.s8co));
     // MLP: fc1 (+bias, GELU in-kernel) -> fc2 partials -> +x, next LN1 (or the final LN)
-    if (c.mlp_fused && mlp_fused_ok(R, dt)) {  // one launch for fc1 -> fc2 (its span is recorded as the fc1 probe), then reduce_ln
-      MlpCall mc;
-      mc.A = c.dhb;
-      mc.lda = dt;
-      mc.W1 = L.wfc1;
-      mc.b1 = L.bfc1;
-      mc.W2 = L.wfc2;
-      mc.h = c.df1;
-      mc.part = c.part;
-      mc.cnt = c.mlp_cnt;
-      mc.M = R;
-      mc.d = dt;
-      mc.tprobe = pbuf(kProbeFc1);
-      mc.pslot = c.slot;
-      launch_mlp_fused(c.dt, mc, c.st);
-      launch_reduce_ln(c.dt, c.part, kMlpSlices, L.bfc2, c.dx, last ? m.lng : m.dec[l + 1].ln1g,
-                       last ? m.lnb : m.dec[l + 1].ln1b, c.dhb, R, dt, c.st,
-                       probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr, c.slot);
-      continue;
-    }
     probe(kProbeFc1);
-    if (!(ab & 8))
-      gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), nullptr,
-             w8_of(m, L.q8fc1, L.s8fc1));
+    gemm_p(c, c.dhb, dt, L.wfc1, R, 4 * dt, dt, epi(EPI_GELU16, L.bfc1, c.df1, 4 * dt), nullptr,
+           w8_of(m, L.q8fc1, L.s8fc1));
     probe(kProbeFc2);
     gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
                  last ? m.lnb : m.dec[l + 1].ln1b,
                  probed ? pbuf(kProbeRedFc2) : prev ? c.probe_buf + kProbePrev * probe_stride : nullptr,
-                 w8_of(m, L.q8fc2, L.s8fc2), (ab & 8) ? (ab | 16) : (ab & ~16));
+                 w8_of(m, L.q8fc2, L.s8fc2));
     c.cur_probe = nullptr;
   }
 }
 
-// Decode step with every LayerNorm folded into the projection that consumes it (wmx_common.h row_ln_from_stats):
-// the residual producers (embedding, out-projection, cross out-projection, fc2) run unsplit and leave x, its 16-bit
-// copy and per-16-column statistics; the consumers (QKV -> self attention, cross-q -> cross attention, fc1) apply
-// LN through W diag(g), c1, c2.  8 launches per layer instead of 11 (no reduce_ln), plus one final LayerNorm.
-// Leaves LN_final(x) of every row in c.dhb.
+// The mixed step's residual producers: x += acc + bias, its 16-bit copy and per-16-column row statistics
 static Epi epi_resid_stats(Ctx& c, const float* bias, int R) {
   Epi e = epi(EPI_RESID_STATS, bias, c.dx, c.m->d.n_text_state);
   e.out16 = c.dhb;
@@ -1488,104 +1392,6 @@ static void debug_sync(Ctx& c, const char* what, int l) {
   if (e != hipSuccess) throw std::runtime_error(std::string("debug sync after ") + what + " (layer " + std::to_string(l) + "): " + hipGetErrorString(e));
 }
 
-static void dec_step_fold(Ctx& c, const FwdArgs& f) {
-  Model& m = *c.m;
-  const int dt = m.d.n_text_state, H = m.d.n_text_head, Lt = m.d.n_text_layer;
-  const int R = f.rows;
-  const size_t cache_layer = (size_t)c.Tctx * c.R * dt;
-  launch_embed_ln(c.dt, m.tok_emb, m.dec_pos, f.tok, f.tok_ld, R, f.pad_seq, c.slot, nullptr, nullptr, dt, c.dx, c.dhb,
-                  c.st, m.d.n_vocab, c.rstat, R);
-  debug_sync(c, "embed", -1);
-  const size_t probe_stride = (size_t)c.Tctx * kProbeWG * 2;
-  for (int l = 0; l < Lt; ++l) {
-    DecLayer& L = m.dec[l];
-    const bool probed = c.probe_kernel >= 0 && l == c.probe_layer;
-    const bool prev = c.probe_kernel >= 0 && l + 1 == c.probe_layer;  // its last launch precedes the probed qkv
-    auto probe = [&](int id) { c.cur_probe = probed ? c.probe_buf + id * probe_stride : nullptr; };
-    // self attention: x16 . (LN1-folded QKV)^T partials -> (LN1 + reduce, cache write, attention)
-    probe(kProbeQKV);
-    int S = gemm_p_part(c, c.dhb, dt, L.fqkv, R, 3 * dt, dt);
-    c.cur_probe = nullptr;
-    debug_sync(c, "qkv", l);
-    DecAttnArgs a{};
-    a.o = c.dao;
-    a.R = R;
-    a.Tn = 1;
-    a.H = H;
-    a.d = dt;
-    a.kc = c.kc + l * cache_layer;
-    a.vc = c.vc + l * cache_layer;
-    a.kv_R = c.R;
-    a.anc = f.anc;
-    a.anc_ld = c.Tctx;
-    a.pad = f.pad_seq;
-    a.slot0 = c.slot;
-    a.qpart = c.part;
-    a.qS = S;
-    a.qpart_stride = (long)R * 3 * dt;
-    a.qpart_ld = 3 * dt;
-    a.ln_c1 = L.c1qkv;
-    a.ln_c2 = L.c2qkv;
-    a.ln_stats = c.rstat;
-    a.ln_ld = R;
-    if (probed) a.tprobe = c.probe_buf + kProbeSelf * probe_stride;
-    launch_self_attn(c.dt, a, c.st);
-    debug_sync(c, "self_attn", l);
-    // out-projection, unsplit: x += o Wo^T + bo, x16, statistics
-    probe(kProbeOut);
-    gemm_p_resid(c, c.dao, dt, L.wo, R, dt, dt, epi_resid_stats(c, L.bo, R));
-    debug_sync(c, "out_resid", l);
-    // cross attention: x16 . (LN2-folded cross-q)^T partials -> (LN2 + reduce, attention)
-    probe(kProbeCrossQ);
-    S = gemm_p_part(c, c.dhb, dt, L.fcq, R, dt, dt);
-    c.cur_probe = nullptr;
-    debug_sync(c, "cross_q", l);
-    DecAttnArgs x{};
-    x.o = c.dao;
-    x.R = R;
-    x.Tn = 1;
-    x.H = H;
-    x.d = dt;
-    x.ck = cross_k(c, l);
-    x.cv = cross_v(c, l);
-    x.x_wstride = (long)kXS * dt;
-    x.x_hstride = (long)kXS * 64;
-    x.Tk = 1500;
-    x.rows_per_win = c.K;
-    x.qpart = c.part;
-    x.qS = S;
-    x.qpart_stride = (long)R * dt;
-    x.qpart_ld = dt;
-    x.ln_c1 = L.c1cq;
-    x.ln_c2 = L.c2cq;
-    x.ln_stats = c.rstat;
-    x.ln_ld = R;
-    x.xcnt = c.xa_cnt;
-    x.slot0 = c.slot;
-    if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
-    launch_cross_attn(c.dt, x, c.xa_ws, c.st);
-    debug_sync(c, "cross_attn", l);
-    probe(kProbeCrossOut);
-    gemm_p_resid(c, c.dao, dt, L.wco, R, dt, dt, epi_resid_stats(c, L.bco, R));
-    debug_sync(c, "cross_out_resid", l);
-    // MLP: GELU(LN3-folded fc1) -> fc2 unsplit (x += ..., x16, statistics)
-    probe(kProbeFc1);
-    Epi e1 = epi(EPI_LNFOLD_GELU16, nullptr, c.df1, 4 * dt);
-    e1.c1 = L.c1fc1;
-    e1.c2 = L.c2fc1;
-    e1.stats = c.rstat;
-    e1.stats_ld = R;
-    gemm_p(c, c.dhb, dt, L.ffc1, R, 4 * dt, dt, e1);
-    debug_sync(c, "fc1_fold", l);
-    probe(kProbeFc2);
-    if (prev) c.cur_probe = c.probe_buf + kProbePrev * probe_stride;
-    gemm_p_resid(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, epi_resid_stats(c, L.bfc2, R));
-    c.cur_probe = nullptr;
-    debug_sync(c, "fc2_resid", l);
-  }
-  launch_layernorm_rows(c.dt, c.dx, nullptr, m.lng, m.lnb, c.dhb, R, dt, c.st);
-  debug_sync(c, "final_ln", -1);
-}
 
 // The mixed decode step: dec_step_fast with the two d x d residual producers of every layer (out-projection,
 // cross out-projection) unsplit -- x += acc + bias, its 16-bit copy and per-16-column row statistics in the GEMM
@@ -1678,9 +1484,7 @@ static void dec_step_mixed(Ctx& c, const FwdArgs& f) {
 }
 
 static void dec_step(Ctx& c, const FwdArgs& f) {
-  if (c.m->fold)
-    dec_step_fold(c, f);
-  else if (c.m->mixed && c.xq_fused)
+  if (c.m->mixed && c.xq_fused)
     dec_step_mixed(c, f);
   else
     dec_step_fast(c, f);
@@ -1994,7 +1798,6 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   // per-call device words: the non-finite guard, and the fused MLP's slice counters + timeout word (zeroed every
   // call, so the monotonic counters never approach 2^32 and a timeout fails only the call it happened in)
   WMX_HIP(hipMemsetAsync(c.nf_err, 0, 4, c.st));
-  WMX_HIP(hipMemsetAsync(c.mlp_cnt, 0, (size_t)kMlpCounters * 4, c.st));
   rec(c, 0);
   logmel_dev(c, pcm_dev, stride, lens, seek, B, c.mel);
   rec(c, 1);
@@ -2077,16 +1880,11 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     f.pad_seq = nullptr;
     f.prefill = true;
     f.anc = nullptr;
-    if (!m.fold) {
-      // the split-K decode step, one row per window (it writes cache slot 0 of rows 0 .. B-1, which the prompt
-      // prefill rewrites or no hypothesis reads) instead of dec_forward's unsplit projections
-      f.win_rows = 1;
-      dec_step_fast(c, f);
-      dec_logits(c, nullptr, B, true);
-    } else {
-      dec_forward(c, f);
-      dec_logits(c, nullptr, B);
-    }
+    // the split-K decode step, one row per window (it writes cache slot 0 of rows 0 .. B-1, which the prompt
+    // prefill rewrites or no hypothesis reads) instead of dec_forward's unsplit projections
+    f.win_rows = 1;
+    dec_step_fast(c, f);
+    dec_logits(c, nullptr, B, true);
     launch_lang_detect(c.logits, c.ldl, sp.lang0, sp.n_langs, B, K, c.hist, T, c.lang_slot, c.lang_tok, c.lang_prob, c.st,
                        c.nf_err);
     debug_sync(c, "lang_detect", -1);
@@ -2144,14 +1942,13 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
 
   if (c.probe_kernel >= 0) {  // per-workgroup records of this call only (read after the timed region)
     WMX_HIP(hipMemsetAsync(c.probe_buf, 0, (size_t)kProbeLaunches * T * kProbeWG * 2 * 8, c.st));
-    if (c.phase_buf) WMX_HIP(hipMemsetAsync(c.phase_buf, 0, (size_t)T * kProbeWG * kPhaseStamps * 8, c.st));
   }
   {  // ALGORITHMIC bytes of one launch: weights + activations in + activations out (16-bit), cross K/V
      // (fp8 decode: weights and cross K/V images at 1 byte per element; activations stay 16-bit)
     const double d = m.d.n_text_state, w2 = 2.0, r = R, ww = m.w8 ? 1.0 : 2.0, iw = m.kv8 ? 1.0 : 2.0;
     auto proj = [&](double n, double k) { return n * k * ww + r * k * w2 + r * n * w2; };
     // (fused cross-q: the cross attention also streams the d x d query weights and reads the LN2 rows)
-    const bool xqf = c.xq_fused && !m.fold;  // (the folded step keeps its cross-q launch)
+    const bool xqf = c.xq_fused;
     const double xq = xqf ? d * d * ww + r * d * w2 : 0.0;
     const double v[kProbeLaunches] = {proj(3 * d, d), proj(d, d), xqf ? 0.0 : proj(d, d), proj(d, d),
                                       proj(4 * d, d), proj(d, 4 * d), (double)B * 1500 * 2 * d * iw + 2.0 * r * d * w2 + xq};
@@ -2162,7 +1959,6 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     sync(c);
     c.lockstep_ok = c.lockstep->arrive(std::chrono::microseconds(5000));
   }
-  if (c.start_delay_us > 0 && steps < max_new) launch_spin((unsigned long long)(c.start_delay_us * c.wall_khz / 1000.0), c.st);
   // the group's chunk barrier (default with lockstep; WMX_LOCKSTEP_CHUNKS=0 keeps only the start barrier), left on
   // every exit of the loop
   static const bool lk_every = !(getenv("WMX_LOCKSTEP_CHUNKS") && atoi(getenv("WMX_LOCKSTEP_CHUNKS")) == 0);
@@ -2231,7 +2027,6 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
     WMX_HIP(hipMemcpyAsync(fh.data(), c.bs.fin_hist, fh.size() * 4, hipMemcpyDeviceToHost, c.st));
   }
   sync(c);
-  if (nf_err != 0 && ablate_mask()) nf_err = 0;  // (timing-only ablation: the skipped launches leave stale rows)
   if (nf_err < 0)
     throw Error(WMX_ERR_NUMERIC, "non-finite decoder logits in language detection, window " + std::to_string(-nf_err - 1));
   if (nf_err != 0) {  // a NaN / inf anywhere upstream of the logits: an error, not a silently shortened transcript
@@ -2418,12 +2213,6 @@ static ResultHolder* transcribe(Ctx& c, const float* pcm_dev, long stride, const
   rec(c, 7);
   WMX_HIP(hipEventSynchronize(c.ev[7]));
   for (int i = 0; i < 7; ++i) WMX_HIP(hipEventElapsedTime(&c.stage_ms[i], c.ev[i], c.ev[i + 1]));
-  if (c.mlp_fused) {  // the fused MLP's bounded poll flags a producer that never arrived instead of hanging
-    int err = 0;
-    WMX_HIP(hipMemcpyAsync(&err, c.mlp_cnt + kMlpSlices, sizeof(int), hipMemcpyDeviceToHost, c.st));
-    WMX_HIP(hipStreamSynchronize(c.st));
-    WMX_CHECK(err == 0, "fused mlp: a slice producer never arrived (poll timeout)");
-  }
 
   for (int b = 0; b < B; ++b) {
     wmx_window_result& w = res->win[b];
@@ -2509,13 +2298,9 @@ wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_mod
       // the CTranslate2 int8 grid: the 8-bit decode path on int8 bytes + CT2 row scales, 16-bit cross K / V images
       w->m.i8 = dtype == WMX_DTYPE_I8 || dtype == WMX_DTYPE_I8_BF16;
       if (w->m.i8) w->m.w8 = true;
-      // opt-in (WMX_FOLD=1): the LayerNorm-folded decode step passes every parity test but measured slower than
-      // the split-K + reduce_ln step (356-390 vs 389-393x real time, interleaved on one box); it has
-      // no 8-bit form (the fp8 decode ignores the switch)
-      w->m.fold = getenv("WMX_FOLD") != nullptr && !w->m.w8;
-      {  // the mixed decode step (WMX_DEC_MIXED=1 while it is measured; 16-bit models)
+      {  // the mixed decode step (WMX_DEC_MIXED=1; 16-bit models)
         const char* dm = getenv("WMX_DEC_MIXED");
-        w->m.mixed = !w->m.w8 && !w->m.fold && dm && dm[0] == '1';
+        w->m.mixed = !w->m.w8 && dm && dm[0] == '1';
       }
       {
         const char* ef = getenv("WMX_ENC_FOLD");
@@ -2545,7 +2330,8 @@ wmx_status wmx_model_init_synthetic(wmx_model* w, uint64_t seed) {
   return guard([&] {
     Model& m = w->m;
     WMX_HIP(hipSetDevice(m.device));
-    m.i8_given.clear();  // (int8 model: every CT2 scale by CT2's rule from the synthetic weights)
+    for (const auto& kv : m.i8_scale_dst)  // (int8 model: every CT2 scale by CT2's rule from the synthetic weights)
+      WMX_HIP(hipMemsetAsync(kv.second.first, 0, (size_t)kv.second.second * 4, m.st));
     for (const TensorEntry& e : m.entries) {
       InitSpec s{};
       s.tid = e.tid;
@@ -2593,7 +2379,11 @@ wmx_status wmx_model_set_tensor(wmx_model* w, const char* name, const float* dat
     }
     const TensorEntry& e = find_entry(m, name, n);
     m.dirty = true;
-    m.i8_given.erase(name);  // (int8 model: a new weight takes CT2's rule for its scales unless they are set after it)
+    {  // (int8 model: a new weight takes CT2's rule for its scales unless they are set after it)
+      const auto it = m.i8_scale_dst.find(name);
+      if (it != m.i8_scale_dst.end())
+        WMX_HIP(hipMemset(it->second.first, 0, (size_t)it->second.second * 4));
+    }
     if (e.store_f32) {
       WMX_HIP(hipMemcpy(e.dst, data, n * 4, hipMemcpyHostToDevice));
       return;
@@ -2668,7 +2458,6 @@ wmx_status wmx_model_set_row_scales(wmx_model* w, const char* name, const float*
       WMX_CHECK(std::isfinite(scale[i]) && scale[i] > 0.f, "set_row_scales: scales must be finite and positive");
     WMX_HIP(hipSetDevice(m.device));
     WMX_HIP(hipMemcpy(it->second.first, scale, n * 4, hipMemcpyHostToDevice));
-    m.i8_given.insert(name);
     m.dirty = true;
   });
 }
@@ -2763,6 +2552,9 @@ void wmx_opts_default(wmx_opts* o) {
 wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
   return guard([&] {
     WMX_CHECK(w && o && out, "null argument");
+    // round 5's timing-only launch ablation (results wrong by construction) was removed from the library; a stale
+    // WMX_ABLATE in the environment fails loudly rather than suggesting that a product run measured it
+    WMX_CHECK(getenv("WMX_ABLATE") == nullptr, "WMX_ABLATE is set: the timing-only decode ablation was removed (unset it)");
     WMX_CHECK(o->max_batch >= 1 && o->beam_size >= 1 && o->beam_size <= 8, "opts: batch / beam");
     WMX_CHECK(o->temperature >= 0.f && std::isfinite(o->temperature), "opts: temperature");
     WMX_CHECK(o->temperature == 0.f || (o->best_of >= 1 && o->best_of <= 8), "opts: best_of (1..8) when sampling");
@@ -2809,8 +2601,6 @@ wmx_status wmx_ctx_create(wmx_model* w, const wmx_opts* o, wmx_ctx** out) {
       // (the int8 model: the cross-q projection on its int8 weights, its own launch -- the fused 8-bit query
       // projection reads e4m3 weights beside fp8 images only)
       c.xq_fused = !(getenv("WMX_XQ_FUSED") && atoi(getenv("WMX_XQ_FUSED")) == 0) && !w->m.i8;
-      c.mlp_fused = getenv("WMX_MLP_FUSED") && atoi(getenv("WMX_MLP_FUSED")) == 1 && !w->m.w8;
-      c.xa_recsplit = getenv("WMX_XATTN_RECSPLIT") && atoi(getenv("WMX_XATTN_RECSPLIT")) == 1;
       gemm_init_attributes();
       alloc_ctx(c);
     } catch (...) {
@@ -2839,7 +2629,6 @@ void wmx_ctx_destroy(wmx_ctx* x) {
   if (c.pinned_i) (void)hipHostFree(c.pinned_i);
   if (c.h_align) (void)hipHostFree(c.h_align);
   if (c.h_tp) (void)hipHostFree(c.h_tp);
-  if (c.phase_buf) (void)hipFree(c.phase_buf);
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
   if (c.st) (void)hipStreamDestroy(c.st);
@@ -2982,7 +2771,6 @@ wmx_status wmx_ctx_forced_decode(wmx_ctx* x, const int32_t* prefix, const int32_
     WMX_HIP(hipMemcpyAsync(c.hist, hist.data(), hist.size() * 4, hipMemcpyHostToDevice, c.st));
     WMX_HIP(hipMemcpyAsync(c.pad_row, pad_row.data(), R * 4, hipMemcpyHostToDevice, c.st));
     WMX_HIP(hipMemcpyAsync(c.pad_win, pad_win.data(), B * 4, hipMemcpyHostToDevice, c.st));
-    WMX_HIP(hipMemsetAsync(c.mlp_cnt, 0, (size_t)kMlpCounters * 4, c.st));  // per-call fused-MLP counters
     set_slot(c, 0);
     std::vector<float> lg((size_t)R * V);
     auto collect = [&](int step, int nrows, int rep) {  // logits rows [0, nrows) -> top1 / logits of R rows
@@ -3262,13 +3050,6 @@ wmx_status wmx_dedup_features(wmx_ctx* x, const float* xh, int64_t stride, const
   });
 }
 
-wmx_status wmx_ctx_set_phase_offset(wmx_ctx* x, double us) {
-  return guard([&] {
-    WMX_CHECK(us >= 0 && us <= 1e5, "phase offset: 0 .. 100000 us");
-    x->c.start_delay_us = us;
-  });
-}
-
 wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
   return guard([&] {
     WMX_CHECK(kernel < 1, "probe: 0 enables the decode-step probes, < 0 disables them");
@@ -3276,30 +3057,6 @@ wmx_status wmx_ctx_set_probe(wmx_ctx* x, int kernel, int layer) {
     Ctx& c = x->c;
     c.probe_kernel = kernel;
     c.probe_layer = layer;
-    if (kernel >= 0 && !c.phase_buf && getenv("WMX_PHASE_PROBE") && atoi(getenv("WMX_PHASE_PROBE")) == 1) {
-      WMX_HIP(hipMalloc(&c.phase_buf, (size_t)c.Tctx * kProbeWG * kPhaseStamps * 8));
-      WMX_HIP(hipMemset(c.phase_buf, 0, (size_t)c.Tctx * kProbeWG * kPhaseStamps * 8));
-    }
-  });
-}
-
-// the cross attention's phase stamps of the last transcribe's probed layer (WMX_PHASE_PROBE=1): out = [n_steps]
-// [kProbeWG][kPhaseStamps] words (zero rows: workgroups past the grid), one slot per graph-replayed decode step
-wmx_status wmx_ctx_probe_phases(wmx_ctx* x, uint64_t* out, int cap_steps, int* n_steps, int* n_wg, int* n_words,
-                                double* wall_khz) {
-  return guard([&] {
-    Ctx& c = x->c;
-    WMX_CHECK(n_steps && n_wg && n_words && wall_khz, "probe_phases: null argument");
-    const int s0 = c.probe_slots[0], s1 = std::min(c.probe_slots[1], c.Tctx);
-    *n_steps = c.phase_buf ? std::max(0, s1 - s0) : 0;
-    *n_wg = kProbeWG;
-    *n_words = kPhaseStamps;
-    *wall_khz = c.wall_khz;
-    if (!out || *n_steps == 0) return;
-    const int n = std::min(*n_steps, cap_steps);
-    WMX_HIP(hipStreamSynchronize(c.st));
-    WMX_HIP(hipMemcpy(out, c.phase_buf + (size_t)s0 * kProbeWG * kPhaseStamps, (size_t)n * kProbeWG * kPhaseStamps * 8,
-                      hipMemcpyDeviceToHost));
   });
 }
 
@@ -3311,13 +3068,14 @@ static void probe_collect(Ctx& c, double* ms, int* n, double* e2e, int* e2e_n) {
   std::vector<unsigned long long> tk((size_t)kProbeLaunches * T * kProbeWG * 2);
   WMX_HIP(hipStreamSynchronize(c.st));
   WMX_HIP(hipMemcpy(tk.data(), c.probe_buf, tk.size() * 8, hipMemcpyDeviceToHost));
-  // the chain of one layer's launches (dec_step_fast / dec_step_fold)
+  // the chain of one layer's launches (dec_step_fast / dec_step_mixed)
   static const int chain_fast[] = {kProbePrev, kProbeQKV, kProbeSelf, kProbeOut, kProbeRedOut, kProbeCrossQ,
                                    kProbeCross, kProbeCrossOut, kProbeRedCrossOut, kProbeFc1, kProbeFc2, kProbeRedFc2};
-  static const int chain_fold[] = {kProbePrev, kProbeQKV, kProbeSelf, kProbeOut, kProbeCrossQ, kProbeCross,
-                                   kProbeCrossOut, kProbeFc1, kProbeFc2};
-  const int* chain = c.m->fold ? chain_fold : chain_fast;
-  const int nchain = c.m->fold ? 9 : 12;
+  static const int chain_mixed[] = {kProbePrev, kProbeQKV, kProbeSelf, kProbeOut, kProbeCross, kProbeCrossOut,
+                                    kProbeFc1, kProbeFc2, kProbeRedFc2};
+  const bool mixed = c.m->mixed && c.xq_fused;
+  const int* chain = mixed ? chain_mixed : chain_fast;
+  const int nchain = mixed ? 9 : 12;
   for (int k = 0; k < kProbeLaunches; ++k) {
     ms[k] = e2e[k] = 0;
     n[k] = e2e_n[k] = 0;
@@ -3483,7 +3241,7 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       const double eb = m.kv8 ? 1.0 : 2.0;  // image / weight bytes per element (fp8 decode: 1)
       by = (double)B * 1500 * 2 * dt * eb + 2.0 * R * dt * 2;
       fl = 4.0 * R * 1500 * dt;
-      if (c.xq_fused && !m.fold) {  // the decode step's form: the query projection inside (reads LN2 rows + wcq)
+      if (c.xq_fused) {  // the decode step's form: the query projection inside (reads LN2 rows + wcq)
         a.wq = m.kv8 ? reinterpret_cast<const uint16_t*>(m.dec[0].q8cq) : m.dec[0].wcq;
         a.wq_scale = m.kv8 ? m.dec[0].s8cq : nullptr;
         a.qin = c.dhb;

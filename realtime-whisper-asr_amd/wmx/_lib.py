@@ -49,18 +49,23 @@ class Result(C.Structure):
     _fields_ = [("n_windows", C.c_int32), ("windows", C.POINTER(WindowResult))]
 
 
+# include/wmx.h: the product surface
 EXPORTS = [
     "wmx_last_error", "wmx_version", "wmx_device_count", "wmx_model_create", "wmx_model_free",
     "wmx_model_init_synthetic", "wmx_model_set_tensor", "wmx_model_get_tensor", "wmx_model_n_params",
-    "wmx_model_arena", "wmx_model_arena_loaded", "wmx_model_set_row_scales", "wmx_model_get_int8", "wmx_opts_default", "wmx_ctx_create", "wmx_ctx_destroy",
-    "wmx_ctx_stream", "wmx_logmel", "wmx_logmel_device", "wmx_encode", "wmx_encode_device",
-    "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device", "wmx_result_free",
-    "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_set_probe", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_probe_ticks", "wmx_ctx_probe_phases", "wmx_ctx_set_lockstep", "wmx_ctx_lockstep_timeouts", "wmx_debug_lockstep_arrive", "wmx_ctx_set_phase_offset",
-    "wmx_filtfilt", "wmx_filtfilt_device", "wmx_dedup_features", "wmx_ctx_forced_decode",
-    "wmx_ctx_record", "wmx_ctx_recorded", "wmx_debug_packed_launch", "wmx_debug_dtw",
-    "wmx_ctx_alignment_matrix", "wmx_ctx_set_sample_seed",
+    "wmx_model_arena", "wmx_model_arena_loaded", "wmx_model_set_row_scales", "wmx_model_get_int8",
+    "wmx_opts_default", "wmx_ctx_create", "wmx_ctx_destroy", "wmx_ctx_stream", "wmx_logmel", "wmx_logmel_device",
+    "wmx_encode", "wmx_encode_device", "wmx_decoder_logits", "wmx_transcribe", "wmx_transcribe_device",
+    "wmx_result_free", "wmx_ctx_set_lockstep", "wmx_ctx_lockstep_timeouts", "wmx_filtfilt", "wmx_filtfilt_device",
+    "wmx_dedup_features", "wmx_ctx_set_sample_seed",
     "wmx_vad_create", "wmx_vad_free", "wmx_vad_set_tensor", "wmx_vad_reset", "wmx_vad_process",
     "wmx_vad_process_device", "wmx_vad_stream",
+]
+# include/wmx_diag.h: test, parity and measurement hooks
+DIAG_EXPORTS = [
+    "wmx_ctx_forced_decode", "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_record",
+    "wmx_ctx_recorded", "wmx_ctx_alignment_matrix", "wmx_debug_packed_launch", "wmx_debug_dtw", "wmx_ctx_set_probe",
+    "wmx_debug_lockstep_arrive", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_probe_ticks",
 ]
 
 
@@ -107,7 +112,6 @@ def _load():
         "wmx_ctx_stage_ms": (C.c_int, [VP, P(F)]),
         "wmx_ctx_last_steps": (C.c_int, [VP]),
         "wmx_ctx_set_probe": (C.c_int, [VP, C.c_int, C.c_int]),
-        "wmx_ctx_set_phase_offset": (C.c_int, [VP, C.c_double]),
         "wmx_filtfilt": (C.c_int, [VP, P(F), I64, P(I64), C.c_int, P(C.c_double), P(C.c_double), P(C.c_double),
                                    C.c_int, P(F)]),
         "wmx_filtfilt_device": (C.c_int, [VP, VP, I64, P(I64), C.c_int, P(C.c_double), P(C.c_double),
@@ -116,8 +120,6 @@ def _load():
         "wmx_ctx_probe_stats": (C.c_int, [VP, P(F), P(C.c_int), P(C.c_double)]),
         "wmx_ctx_probe_launches": (C.c_int, [VP, P(F), P(C.c_double), P(C.c_int), P(F), P(C.c_int)]),
         "wmx_ctx_probe_ticks": (C.c_int, [VP, P(C.c_uint64), P(C.c_int), P(C.c_double)]),
-        "wmx_ctx_probe_phases": (C.c_int, [VP, P(C.c_uint64), C.c_int, P(C.c_int), P(C.c_int), P(C.c_int),
-                                           P(C.c_double)]),
         "wmx_ctx_set_lockstep": (C.c_int, [VP, C.c_int, C.c_int]),
         "wmx_ctx_lockstep_timeouts": (C.c_int, [VP, C.POINTER(C.c_int64)]),
         "wmx_debug_lockstep_arrive": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_int)]),

@@ -371,10 +371,6 @@ class Context:
         step of every following transcribe records each workgroup's first and last device-clock tick."""
         check(lib.wmx_ctx_set_probe(self._h, 0 if on else -1, layer))
 
-    def set_phase_offset(self, us: float):
-        """Idle `us` microseconds before this context's decode loop (wmx_ctx_set_phase_offset)."""
-        check(lib.wmx_ctx_set_phase_offset(self._h, float(us)))
-
     def probe_launches(self, e2e: bool = True) -> dict:
         """{launch: (average in-situ duration ms, samples, algorithmic bytes of one launch)} of the last transcribe:
         e2e = end of the launch minus end of its predecessor in the layer's chain (dispatch + execution, what
@@ -411,17 +407,6 @@ class Context:
         t = np.zeros((max(n.value, 1), len(self.PROBE_LAUNCHES), 2), np.uint64)
         if n.value:
             check(lib.wmx_ctx_probe_ticks(self._h, t.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(n), C.byref(khz)))
-        return t[:n.value], float(khz.value)
-
-    def probe_phases(self):
-        """(stamps [steps][workgroups][10] uint64, wall-clock kHz): the probed layer's cross-attention phase stamps
-        of the last transcribe (wmx_ctx_probe_phases; diagnostics, WMX_PHASE_PROBE=1 at set_probe)."""
-        n, nwg, nw, khz = C.c_int(), C.c_int(), C.c_int(), C.c_double()
-        check(lib.wmx_ctx_probe_phases(self._h, None, 0, C.byref(n), C.byref(nwg), C.byref(nw), C.byref(khz)))
-        t = np.zeros((max(n.value, 1), nwg.value, nw.value), np.uint64)
-        if n.value:
-            check(lib.wmx_ctx_probe_phases(self._h, t.ctypes.data_as(C.POINTER(C.c_uint64)), n.value, C.byref(n),
-                                           C.byref(nwg), C.byref(nw), C.byref(khz)))
         return t[:n.value], float(khz.value)
 
     def bench_kernel(self, kernel: str, batch: int, iters: int = 50):

@@ -89,17 +89,21 @@ def gather(result, world: int):
 def summarize(parts, skip_first_call: bool = True):
     """p50 / p90 of the per-stream process_iter latency over every stream of every rank, and per-call shapes.  The
     first batched call of each rank captures the decode graphs and is left out when it is not the only one."""
-    lat, calls, recs = [], [], []
+    lat, calls, recs, per_rank = [], [], [], []
     for p in parts:
         c = p["calls"]
         first_tick = None
         if skip_first_call and len(c) > 2 and p["lat"]:
             first_tick = min(k for _, k, _ in p["lat"])
             c = c[1:]
-        lat.extend(dt for _, k, dt in p["lat"] if k != first_tick)
+        mine = [dt for _, k, dt in p["lat"] if k != first_tick]
+        lat.extend(mine)
+        # the same first-call exclusion per rank (ADVICE r05: the per-rank medians were on a different basis)
+        per_rank.append(round(1000 * float(np.median(mine)), 2) if mine else None)
         calls.extend(c)
         recs.extend(p["records"])
     return {
+        "per_rank_p50_ms": per_rank,
         "streams": sum(len(p["streams"]) for p in parts), "ranks": len(parts),
         "stream_iters": len(lat), "batched_calls": len(calls),
         "p50_ms": round(1000 * float(np.median(lat)), 2) if lat else None,

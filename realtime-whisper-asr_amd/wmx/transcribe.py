@@ -477,11 +477,10 @@ class WhisperModel:
                 for c, p in zip(ctxs, parts)]
         from concurrent.futures import wait
         wait(futs)  # every group finishes before any error propagates (a context serves one call at a time)
-        res = []
-        for c, p, f in zip(ctxs, parts, futs):
-            res.extend(f.result())
+        res = [f.result() for f in futs]  # (raises before any group is counted: the fallback re-runs the batch)
+        for c, p in zip(ctxs, parts):
             self._count(c, len(p))
-        return res
+        return [r for part in res for r in part]
 
     def _transcribe_isolating(self, ctx, idx, chunk, pr, out):
         """ctx.transcribe of a batch; a WMX_ERR_NUMERIC naming one window (one stream's non-finite decode, e.g. NaN

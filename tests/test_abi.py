@@ -1,5 +1,6 @@
-"""C-ABI boundary checks that need no GPU: libwmx.so loads, exports every entry point include/wmx.h declares,
-and the ctypes struct layouts match the header's field lists."""
+"""C-ABI boundary checks that need no GPU: libwmx.so loads, exports every entry point include/wmx.h (the product
+surface) and include/wmx_diag.h (test / measurement hooks) declare, and the ctypes struct layouts match the header's
+field lists."""
 import os
 import re
 import subprocess
@@ -8,11 +9,13 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "wmx.h")
+DIAG = os.path.join(ROOT, "include", "wmx_diag.h")
 LIB = os.path.join(ROOT, "realtime-whisper-asr_amd", "wmx", "libwmx.so")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(path=None):
+    paths = [path] if path else [HEADER, DIAG]
+    src = "".join(open(p).read() for p in paths)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(wmx_[a-z0-9_]+)\s*\(", src)))
 
@@ -35,7 +38,10 @@ def test_library_exports_every_declared_symbol():
 def test_ctypes_binding_loads_and_matches():
     from wmx import _lib
     assert _lib.lib.wmx_version().decode().startswith("wmx")
-    assert sorted(_lib.EXPORTS) == declared_functions()
+    assert sorted(_lib.EXPORTS) == declared_functions(HEADER)
+    assert sorted(_lib.DIAG_EXPORTS) == declared_functions(DIAG)
+    # the product header declares no probe / debug / phase entry point
+    assert not [f for f in declared_functions(HEADER) if "probe" in f or "debug" in f or "phase" in f]
     src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
 
     def fields(struct):

@@ -59,10 +59,11 @@ def _same(a, b, tag):
     np.testing.assert_array_equal(a.text_token_probs, b.text_token_probs, err_msg=tag)
 
 
-@pytest.mark.parametrize("ct", ["bfloat16", "float8"])
+@pytest.mark.parametrize("ct", ["bfloat16", "float8", "int8_float16", "int8_bfloat16"])
 def test_two_groups_concurrent_equal_sequential_and_replay(ct):
-    """bfloat16 (the default bench line) and float8 (config 5's line: MX-fp8 encoder, 8-bit decoder weights and fp8
-    cross-K/V images)."""
+    """bfloat16 (the default bench line), float8 (config 5's line: MX-fp8 encoder, 8-bit decoder weights and fp8
+    cross-K/V images) and the reference's CTranslate2 int8 modes (int8 decoder / logits weights with CT2 row scales,
+    the separate cross-q launch, 16-bit cross-K/V images; f16 and bf16 activations: ADVICE r05)."""
     from wmx import engine as E
     m = E.Model(_edims(WIDE2), 0, ct).init_synthetic(5)
     sp = O.special_tokens(WIDE2.n_vocab)

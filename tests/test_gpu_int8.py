@@ -71,6 +71,31 @@ def test_int8_checkpoint_keeps_its_exact_grid(ct2_int8):
     print("int8 weights on the checkpoint's grid:", n)
 
 
+def test_int8_arena_copy_keeps_the_checkpoint_scales(ct2_int8):
+    """The weight broadcast of a CT2 int8 checkpoint: a second model that receives the first one's
+    parameter region (what share_weights broadcasts over RCCL; here one device-to-device copy) and derives its copies
+    (wmx_model_arena_loaded) keeps the checkpoint's row scales and int8 bytes bit for bit -- the given / derived state
+    of every scale row travels with the region, so no rank re-derives a scale the checkpoint gave."""
+    import ctypes as C
+    from wmx import engine as E
+    m, deq, file_scales, _ = ct2_int8
+    m2 = E.Model(_dims(E, WIDE2), 0, "int8_float16")
+    (src, n1), (dst, n2) = m.arena(), m2.arena()
+    assert n1 == n2
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipMemcpy(dst, src, n1, 3) == 0  # hipMemcpyDeviceToDevice
+    assert hip.hipDeviceSynchronize() == 0
+    m2.mark_loaded()
+    for name, shape in _kept(WIDE2).items():
+        q1, s1 = m.get_int8(name, shape)
+        q2, s2 = m2.get_int8(name, shape)
+        np.testing.assert_array_equal(s2, file_scales[name], err_msg=name)
+        np.testing.assert_array_equal(s2, s1, err_msg=name)
+        np.testing.assert_array_equal(q2, q1, err_msg=name)
+    m2.close()
+
+
 @pytest.mark.parametrize("B,K", [(4, 5), (20, 1)])
 def test_int8_forced_decode_matches_oracle(ct2_int8, B, K):
     from wmx import engine as E

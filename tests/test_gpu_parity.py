@@ -255,19 +255,3 @@ def test_word_alignment_matrix_micro(micro):
     assert e <= REL["f16"], e
     assert within >= 0.95, (r.jump_times, jt)
     np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)
-
-
-def test_fused_reduce_ln_tail_parity():
-    """The opt-in RedTail path (packed GEMM + in-launch split-K reduce + LayerNorm, WMX_REDLN_FUSED) against the
-    oracle: the token/beam/logit parity tests of this file and the large-v3-width decoder logits, rerun in a child
-    process with the switch set (the library reads it once per process)."""
-    import os
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, WMX_REDLN_FUSED="1")
-    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
-           "-k", "not fused_reduce_ln", "tests/test_gpu_parity.py", "tests/test_gpu_wide.py"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

@@ -126,37 +126,6 @@ def test_forced_steps_wide_beam5_4windows(wide20):
     _check_forced("wide beam5 B=4", dt, top1, lg, 1, ref_top1, ref_margin, ref_lg, 16)
 
 
-def test_cross_records_merged_by_the_out_projection_bit_identical(wide20):
-    """WMX_XATTN_RECSPLIT=1 (read at context creation): the decode cross attention's two key-chunk records are merged
-    in the cross out-projection's A loads instead of by the last-arriving chunk (no ticket, no in-launch merge).  The
-    consumer repeats the attention's merge operation for operation, so the teacher-forced logits of every step and
-    row are bit-identical to the default form's, at the bench's per-group shape (4 windows x beam 5, prompted)."""
-    import os
-    from wmx import engine as E
-    dt, m, W, mels, encs = wide20
-    sp = O.special_tokens(WIDE2.n_vocab)
-    n = 12
-    tok, par = _forced_stream(np.random.default_rng(23), n, 20, 5)
-    prefix = [[sp.sot_prev] + list(range(1000, 1000 + L)) + [sp.sot, sp.lang0, sp.transcribe] for L in (0, 5, 11, 2)]
-    prefix[0] = [sp.sot, sp.lang0, sp.transcribe]
-    out = []
-    for flag in ("0", "1"):
-        old = os.environ.get("WMX_XATTN_RECSPLIT")
-        os.environ["WMX_XATTN_RECSPLIT"] = flag
-        try:
-            ctx = E.Context(m, max_batch=4, beam_size=5, max_new_tokens=64, word_timestamps=False)
-        finally:
-            if old is None:
-                del os.environ["WMX_XATTN_RECSPLIT"]
-            else:
-                os.environ["WMX_XATTN_RECSPLIT"] = old
-        ctx.encode(mels[:4], want_output=False)
-        out.append(ctx.forced_decode(prefix, tok, par, logits_every=1))
-        ctx.close()
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-
-
 def test_forced_steps_micro_beam5_224():
     """224 steps with beams reordered every step: self attention over up to 227 ancestry-gathered slots."""
     from wmx import engine as E
@@ -481,23 +450,6 @@ def test_control_tokens_suppressed_with_boosted_logits():
         assert any(set(r.tokens) & set(ctrl) for r in bare.transcribe(audios))
 
 
-def test_folded_layernorm_step_parity():
-    """The opt-in LayerNorm-folded decode step (WMX_FOLD=1: unsplit residual producers with per-16-column row
-    statistics, LN applied through W diag(g), c1, c2 by the consumers; wmx_runtime.hip dec_step_fold) against the
-    oracle: this file's step and search tests rerun in a child process with the switch set (read at model creation)."""
-    import os
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, WMX_FOLD="1")
-    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
-           "-k", "not folded_layernorm and not full_depth and not mixed_step and not fused_mlp and not separate_cross_q",
-           "tests/test_gpu_step.py"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-
-
 def test_separate_cross_q_step_parity():
     """The decode step with the cross-q projection as its own split-K launch (WMX_XQ_FUSED=0) instead of inside the
     cross attention (the default, wmx_attn.hip dec_cross_attn_kernel<..., XQ = true>): the teacher-forced step tests
@@ -527,28 +479,8 @@ def test_mixed_step_parity():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, WMX_DEC_MIXED="1")
     cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
-           "-k", "not folded_layernorm and not mixed_step and not fused_mlp and not separate_cross_q",
+           "-k", "not mixed_step and not separate_cross_q",
            "tests/test_gpu_step.py"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=880)
-    print(r.stdout[-1500:])
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-
-
-def test_fused_mlp_step_parity():
-    """The decode MLP as one launch (WMX_MLP_FUSED=1, wmx_gemm.hip mlp_fused_kernel: fc1 + GELU -> fc2 partials with
-    the fc1 -> fc2 edge handed off inside the launch, write-through stores + slice counters): this file's teacher-forced
-    step tests, search replays and full-depth tests (d 1280 at 20 rows, d 384 at 3 rows; rows <= 32 take the fused
-    form) and the two-group concurrency test rerun in a child process with the switch set (read at context
-    creation)."""
-    import os
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, WMX_MLP_FUSED="1")
-    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
-           "-k", "forced_steps or search_replay or full_depth or concurrent", "tests/test_gpu_step.py",
-           "tests/test_gpu_concurrent.py"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=880)
     print(r.stdout[-1500:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

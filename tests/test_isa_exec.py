@@ -6,8 +6,8 @@ EXEC = 0 as a no-op; MFMA instructions ignore EXEC and accumulate whatever their
 per-step guarded loads those registers were stale (NaN bit patterns): the guarded variant produced NaN logits at the
 first step with every load address in bounds (profiles/r03a_guarded_variant.log; its bounds-checked build reported
 no out-of-range load).  tools/isa_exec_check.py disassembles the library's gfx950 code objects and flags every such
-MFMA; it must find none in the shipped libwmx.so, and it must find the guarded variant's (the check has teeth) when
-that diagnostic build is present."""
+MFMA; it must find none in the shipped libwmx.so (round 3 checked that it flags the guarded variant's; that
+diagnostic build was removed in round 6)."""
 import os
 import subprocess
 import sys
@@ -16,7 +16,6 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "realtime-whisper-asr_amd", "wmx", "libwmx.so")
-GUARDED = os.path.join(ROOT, "realtime-whisper-asr_amd", "wmx", "libwmx_guarded.so")
 CHECK = os.path.join(ROOT, "tools", "isa_exec_check.py")
 
 
@@ -31,13 +30,6 @@ def test_no_mfma_under_possibly_empty_exec():
     assert "0 MFMA(s)" in r.stdout
 
 
-@pytest.mark.skipif(not os.path.exists(GUARDED), reason="diagnostic build (tools/build_variant.sh guarded "
-                                                         "-DWMX_PACKED_GUARDED) not present")
-def test_check_flags_the_guarded_variant():
-    r = _run(GUARDED)
-    assert r.returncode == 1 and "gemm_packed_kernel" in r.stdout, r.stdout
-
-
 # Kernels allowed a private segment (tools/scratch_check.py), each for a stated reason; any other kernel that grows
 # one fails here, so a register-pressure regression on the decode / encoder path is caught at build time (round 4:
 # a prefetch struct demoted to scratch in every S == 1 packed-GEMM instantiation cost the mixed step's fc1 5 us).
@@ -48,7 +40,6 @@ SCRATCH_ALLOWED = [
     (r"gemm_mx8_256_kernelILNS_2DTE\dELi7E",
      "MX-fp8 GELU->MX8 on the 128-deep ring: 6 dwords saved at entry, reloaded outside the steady-state K loop"),
     (r"enc_attn_kernelILNS_2DTE\dELi8ELi4E", "one VGPR stored before and reloaded after the key loop"),
-    (r"gemm_packed_kernelILNS_2DTE\dELi\dELi\dELi16ELi3E", "RedTail (opt-in WMX_REDLN_FUSED)"),
     (r"dec_cross_attn_kernelILNS_2DTE\dELi[12]ELi\dELb\dELb0E",
      "16-bit images at <= 2 key blocks per wave under the 128-VGPR cap (not the default 1024-key decode chunk)"),
 ]
