@@ -67,6 +67,10 @@ wmx_status wmx_ctx_alignment_matrix(wmx_ctx* c, int b, float* out, int* n, int* 
  * (end offset), A elements touched (end offset), partial elements written (end offset), k-steps loaded outside the
  * wave's slice}, computed by walking the launch through the kernel's own index helpers (wmx_kernels.h). */
 wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int split, int64_t lda, int64_t* out9);
+/* Debug: with WMX_GUARD=1 in the environment when the model / context was created, every arena buffer is followed by a
+ * 64 KiB guard gap holding a byte pattern; *model_buf / *ctx_buf = the index (allocation order) of the first buffer
+ * whose gap was overwritten, -1 when every gap is intact (either handle may be NULL). */
+wmx_status wmx_debug_guard_check(wmx_model* m, wmx_ctx* c, int* model_buf, int* ctx_buf);
 /* Host-only (no GPU call): the word-alignment DTW of wmx_transcribe on a caller alignment matrix x[N][ld] (first M
  * columns; the DTW cost is -x, as openai timing calls dtw(-matrix)), returning the backtraced path (ti[k], tj[k]),
  * k < *len <= N + M, in path order from (0, 0).

@@ -229,11 +229,12 @@ void gemm_init_attributes();
 // log-mel
 // sparse slaney filterbank limits of the FFT log-mel form (its table is staged in LDS)
 constexpr int kMaxMels = 128, kMelWCap = 640;
-size_t logmel_smem_bytes();
-double logmel_flops_per_frame();  // algorithmic flops of the active log-mel form per STFT frame
+double logmel_flops_per_frame();  // algorithmic flops of the FFT log-mel per STFT frame
+// 32-frame blocks of a window of max_frames STFT frames; the statistics buffer holds B x blocks x (1 + n_mels) floats
+int logmel_blocks(int max_frames);
 void launch_logmel(const float* pcm, long stride, const long* lens_dev, const int* seek_dev, int B, int max_frames,
-                   const float* basis, const int* mfirst, const int* mcount, const int* moff, const float* mw,
-                   int n_mels, float* raw, int fcap, int* wmax, float* out, hipStream_t st);
+                   const int* mfirst, const int* mcount, const int* moff, const float* mw, int n_mels, float* stats,
+                   long stats_cap, float* out, hipStream_t st);
 
 // elementwise / norm / layout
 void launch_layernorm(DT dt, const float* x, const float* g, const float* b, uint16_t* out, int rows, int d,

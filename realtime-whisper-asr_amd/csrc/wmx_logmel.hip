@@ -5,28 +5,24 @@
 //   (F = N//160 + 1 frames); per-window max-8 clamp; (x+4)/4; encoder window = frames [seek, seek+3000)
 //   of the first min(3000, F-1-seek) content frames, zero padded (pad_or_trim).
 //
-// Kernel 1, GEMM form (logmel_raw, opt-in WMX_LOGMEL_GEMM=1; the FFT form below is the default): one workgroup = 64 consecutive frames of one window, 4 waves x 16 frames.
-//   The windowed real DFT is a [frames x 400] x [400 x 416] f32 GEMM on v_mfma_f32_16x16x4_f32 (exact
-//   fp32 FMA chains; bf16 would miss the 1e-4 gate).  Audio for the 64 frames (10480 samples, reflect
-//   applied) is staged once in LDS; the Hann-folded cos/sin basis streams through LDS in 16-sample
-//   K-chunks.  Re/Im tiles of one bin block share a lane layout, so |X|^2 is formed in registers,
-//   written to LDS, reduced through the sparse slaney filterbank, log10'd, stored, and the block max
-//   is folded into a per-window atomicMax.
-// Kernel 2 (logmel_finalize): clamp, scale, slice [seek, seek+3000) and zero-pad.  HBM-bound.
+// Two launches, no memset, 13.8 MB of algorithmic HBM traffic per 4 windows moved about once (round 6):
+//   logmel_fft_kernel   one workgroup = 32 consecutive frames of one window, aligned so that its frames are one
+//                       32-frame block of the OUTPUT window (f0 = seek mod 32 + 32 k); writes (v + 4) / 4 of its
+//                       in-window frames straight into the encoder input [B][n_mels][3000] and two statistics: the
+//                       block's max of v over every frame (the per-window max runs over the whole audio) and, per mel,
+//                       the min of its in-window values.  Plain stores of per-block partials: no atomics, no memset.
+//   logmel_clamp_kernel one workgroup = one 32-frame output block, one thread per mel: the window max from the block
+//                       maxima, then only the (mel, block) row pieces whose min lies below max - 8 are read and
+//                       clamped (about 6 % of them on speech-like audio), and the pad frames are zeroed.
+// Rounding: max((v + 4) / 4, (fl(gmax - 8) + 4) / 4) equals (max(v, fl(gmax - 8)) + 4) / 4 bit for bit (x -> fl(x + 4)
+// is monotone, the / 4 exact), the form the previous raw + finalize pair computed.
 #include "wmx_common.h"
 #include "wmx_kernels.h"
 
 namespace wmx {
 
-constexpr int kFFT = 400, kHop = 160, kBins = 201, kBinTiles = 13, kCols = 2 * kBinTiles * 16;  // 416
-constexpr int kFramesPerWG = 64, kKChunk = 16;
-constexpr int kSeg = kHop * (kFramesPerWG - 1) + kFFT;  // 10480 samples
-
-__device__ inline int enc_max(float f) {
-  int i = __float_as_int(f);
-  return i >= 0 ? i : i ^ 0x7FFFFFFF;
-}
-__device__ inline float dec_max(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+constexpr int kFFT = 400, kHop = 160, kOutFrames = 3000;
+constexpr int kBinsPad = 208;  // power image row stride (201 bins, padded)
 
 // mel filter table: per mel m: first bin, count, offset into weights
 struct MelTable {
@@ -36,112 +32,22 @@ struct MelTable {
   const float* w;
 };
 
-__global__ __launch_bounds__(256) void logmel_raw_kernel(const float* __restrict__ pcm, long stride,
-                                                         const long* __restrict__ lens, const float* __restrict__ basis,
-                                                         MelTable mt, int n_mels, float* __restrict__ raw,
-                                                         int fcap, int* __restrict__ wmax) {
-  const int b = blockIdx.y;
-  const long N = lens[b];
-  const int F = (int)(N / kHop) + 1;
-  const int f0 = blockIdx.x * kFramesPerWG;
-  if (f0 >= F) return;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* aud = smem;                        // [kSeg]
-  float* bas = smem + kSeg;                 // [2][kKChunk][kCols]   (reused as power [64][208] after the loop)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* x = pcm + (long)b * stride;
-  const long Lp = N + kHop;                 // padded length
-  const long period = 2 * (Lp - 1);
-  const long j0 = (long)f0 * kHop - kFFT / 2;
-  for (int i = tid; i < kSeg; i += 256) {
-    long j = j0 + i;
-    long m = j % period;
-    if (m < 0) m += period;
-    if (m >= Lp) m = period - m;
-    aud[i] = (m < N) ? x[m] : 0.0f;
-  }
-  auto stage = [&](int chunk, int buf) {
-    const float4* src = reinterpret_cast<const float4*>(basis + (long)chunk * kKChunk * kCols);
-    float4* dst = reinterpret_cast<float4*>(bas + buf * kKChunk * kCols);
-    for (int i = tid; i < kKChunk * kCols / 4; i += 256) dst[i] = src[i];
-  };
-  stage(0, 0);
-  __syncthreads();
-
-  f32x4 re[kBinTiles], im[kBinTiles];
-#pragma unroll
-  for (int t = 0; t < kBinTiles; ++t) {
-    re[t] = f32x4{0, 0, 0, 0};
-    im[t] = f32x4{0, 0, 0, 0};
-  }
-  const int arow = (wave * 16 + (lane & 15)) * kHop;  // this lane's frame start in aud[]
-  const int kq = lane >> 4;
-  constexpr int nchunks = kFFT / kKChunk;  // 25
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nchunks) stage(c + 1, buf ^ 1);
-    const float* bc = bas + buf * kKChunk * kCols;
-#pragma unroll
-    for (int ks = 0; ks < kKChunk / 4; ++ks) {
-      const int k = ks * 4 + kq;
-      const float a = aud[arow + c * kKChunk + k];
-      const float* brow = bc + k * kCols + (lane & 15);
-#pragma unroll
-      for (int t = 0; t < kBinTiles; ++t) {
-        re[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, brow[t * 16], re[t], 0, 0, 0);
-        im[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, brow[(kBinTiles + t) * 16], im[t], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-  // power -> LDS [64 frames][208 bins]
-  float* pw = bas;
-  constexpr int kPB = kBinTiles * 16;
-#pragma unroll
-  for (int t = 0; t < kBinTiles; ++t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int fr = wave * 16 + (lane >> 4) * 4 + r;
-      pw[fr * kPB + t * 16 + (lane & 15)] = re[t][r] * re[t][r] + im[t][r] * im[t][r];
-    }
-  }
-  __syncthreads();
-  // sparse filterbank + log10; thread -> (frame = tid & 63, mel stride 4)
-  float bmax = -INFINITY;
-  const int fr = tid & 63;
-  const int f = f0 + fr;
-  const bool valid = f < F;
-  for (int m = tid >> 6; m < n_mels; m += 4) {
-    const int s = mt.first[m], cnt = mt.count[m], off = mt.offset[m];
-    float acc = 0.f;
-    for (int i = 0; i < cnt; ++i) acc += mt.w[off + i] * pw[fr * kPB + s + i];
-    const float v = log10f(fmaxf(acc, 1e-10f));
-    if (valid) {
-      raw[((long)b * n_mels + m) * fcap + f] = v;
-      bmax = fmaxf(bmax, v);
-    }
-  }
-  bmax = wave_max(bmax);
-  __shared__ float red[4];
-  if (lane == 0) red[wave] = bmax;
-  __syncthreads();
-  if (tid == 0) atomicMax(&wmax[b], enc_max(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
-}
-
 // ------------------------------------------------------------------------------------------------
-// Kernel 1, FFT form (default): one workgroup = 32 consecutive frames of one window.  The 400-point real DFT of a
-// frame is a two-pass Cooley-Tukey transform with N = 20 x 20 (n = 20 n1 + n2, k = k1 + 20 k2):
+// FFT kernel: the 400-point real DFT of a frame is a two-pass Cooley-Tukey transform with N = 20 x 20
+// (n = 20 n1 + n2, k = k1 + 20 k2):
 //   pass 1, thread per (frame, n2):  Y[n2][k1] = sum_n1 xw[20 n1 + n2] W20^(n1 k1), k1 = 0..10 (real input: the
 //           other half is the conjugate), the 20 samples in registers, W20 as compile-time constants;
 //   pass 2, thread per (frame, k1):  t[n2] = Y[n2][k1] W400^(n2 k1) (table in LDS), then
 //           X[k1 + 20 k2] = sum_n2 t[n2] W20^(n2 k2) for the bins <= 200, and |X|^2 straight to the power image.
-// ~54 kFLOP per frame on the vector ALUs instead of the 333 kFLOP of the DFT-as-GEMM (no 666 KB basis stream per
-// workgroup); audio, Y (the 11 stored k1 columns, float2) and the power image all stay in LDS.
-// The filterbank / log10 / per-window max tail is the GEMM form's.
+// ~54 kFLOP per frame on the vector ALUs; audio, Y (the 11 stored k1 columns, float2) and the power image stay in
+// LDS.  The prologue issues every global load of the workgroup (audio as 16-byte loads on the interior path, the
+// filterbank tables) before the first LDS store, so it costs one round trip.
 // ------------------------------------------------------------------------------------------------
 constexpr int kFftFrames = 32;
 constexpr int kFftThreads = kFftFrames * 20;  // 10 waves: one (frame, n2) item per thread in pass 1, (frame, k1) in pass 2
 constexpr int kFftSeg = kHop * (kFftFrames - 1) + kFFT;  // 5360 samples
+constexpr int kSegVec = kFftSeg / 4;                      // 1340 16-byte pieces
+static_assert(2 * kFftThreads < kSegVec && kSegVec <= 3 * kFftThreads, "interior audio: three 16-byte loads per thread");
 
 // cos / sin(2 pi m / 20), m = 0..19 (folded into the unrolled loops as literals)
 __device__ constexpr float kC20[20] = {1.0f, 0.95105651629515357f, 0.80901699437494742f, 0.58778525229247313f,
@@ -159,57 +65,122 @@ __device__ constexpr float kS20[20] = {0.0f, 0.30901699437494742f, 0.58778525229
 
 // audio + Y (the power image reuses Y's space after pass 2) + the W400 table: 80 KB, two workgroups per CU
 constexpr int kYS = 21;  // Y row stride (float2): odd, so pass 2's per-thread row reads fall in different banks
-size_t logmel_fft_smem_bytes() { return (size_t)kFftSeg * 4 + (size_t)kFftFrames * 11 * kYS * 8 + 2 * kFFT * 4; }
+constexpr size_t kFftLdsUsed = (size_t)kFftSeg * 4 + (size_t)kFftFrames * 11 * kYS * 8 + 2 * kFFT * 4;  // 81.8 KiB
+// The launch requests the CU's whole LDS (160 KiB less the static tables), so no other workgroup shares the CU while
+// a block runs.  Measured (tools/conc_probe4.py / conc_probe6.py, round 6): with the 81.8 KiB it uses, a workgroup that
+// shared its CU with a co-running 128 x 128 LDS-DMA GEMM of another context (gemm_kernel, e.g. that context's
+// encoder at <= 2 windows) returned wrong spectra for a few frames of the block in 9-17 of 15-20 calls (whole frames,
+// up to 1.2 in normalised log-mel), although both kernels address only their own LDS; with the CU to itself, 0 of
+// 15.  The round-5 kernel (145 VGPRs) never shared a CU with such a GEMM; this one (88 VGPRs) could.  One workgroup
+// per CU is what either form runs anyway (81.8 KiB x 2 exceeds the CU's LDS).
+constexpr size_t kFftLdsStatic = 8192;  // (bound on the kernel's static __shared__ tables: 4.1 KiB)
+size_t logmel_fft_smem_bytes() { return 160 * 1024 - kFftLdsStatic; }
+static_assert(kFftLdsUsed <= 160 * 1024 - kFftLdsStatic, "log-mel: LDS image");
 
+// min over each aligned half-wave (32 lanes)
+__device__ inline float half_min32(float v) {
+  v = fminf(v, dpp_mov<kDppXor1>(v));
+  v = fminf(v, dpp_mov<kDppXor2>(v));
+  v = fminf(v, dpp_mov<kDppHalfMirror>(v));
+  v = fminf(v, dpp_mov<kDppMirror>(v));
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// the window's geometry: F STFT frames (the last one dropped from the output), content size of the output window,
+// its first frame; output block k of window b is frames f0(k) = (seek & 31 ? (seek & 31) - 32 : 0) + 32 k
+struct MelWin {
+  int F, sk, size, fbase;
+};
+__device__ inline MelWin mel_win(const long* lens, const int* seek, int b) {
+  MelWin w;
+  w.F = (int)(lens[b] / kHop) + 1;
+  w.sk = seek ? seek[b] : 0;
+  w.size = max(0, min(kOutFrames, w.F - 1 - w.sk));
+  const int fb = w.sk & 31;
+  w.fbase = fb ? fb - 32 : 0;
+  return w;
+}
+
+// stats: [B][nblk] block maxima of v, then [B][nblk][n_mels] per-mel minima of the in-window (v + 4) / 4
 __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __restrict__ pcm, long stride,
-                                                         const long* __restrict__ lens, MelTable mt, int n_mels,
-                                                         float* __restrict__ raw, int fcap, int* __restrict__ wmax) {
-  const int b = blockIdx.y;
+                                                                 const long* __restrict__ lens,
+                                                                 const int* __restrict__ seek, MelTable mt, int n_mels,
+                                                                 float* __restrict__ out, float* __restrict__ stats,
+                                                                 int nblk) {
+  const int b = blockIdx.y, blk = blockIdx.x, B = gridDim.y;
+  const MelWin win = mel_win(lens, seek, b);
   const long N = lens[b];
-  const int F = (int)(N / kHop) + 1;
-  const int f0 = blockIdx.x * kFftFrames;
-  if (f0 >= F) return;
+  const int F = win.F;
+  const int f0 = win.fbase + 32 * blk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* smax = stats + (long)b * nblk + blk;
+  float* smin = stats + (long)B * nblk + ((long)b * nblk + blk) * n_mels;
+  if (f0 >= F) {  // past the audio: neutral statistics (the clamp kernel reads every block of the window)
+    if (tid == 0) *smax = -INFINITY;
+    for (int m = tid; m < n_mels; m += kFftThreads) smin[m] = INFINITY;
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* aud = smem;                                            // [kFftSeg], Hann applied per frame in pass 1
   float2* Y = reinterpret_cast<float2*>(smem + kFftSeg);        // [frame][k1 0..10][n2 0..19, row stride kYS]
   float* pw = smem + kFftSeg;                                   // [frame][208], over Y once pass 2 has read it
   float* tc = smem + kFftSeg + kFftFrames * 11 * kYS * 2;       // cos(2 pi j / 400)
   float* ts = tc + kFFT;                                        // sin(2 pi j / 400)
-  // the sparse filterbank in LDS, loaded beside the audio: the tail's per-mel reads are then LDS, not a chain of
-  // dependent global loads per mel
+  // the sparse filterbank in LDS: the tail's per-mel reads are then LDS, not a chain of dependent global loads
   __shared__ int mfirst[kMaxMels], mcount[kMaxMels], moff[kMaxMels];
   __shared__ float mw[kMelWCap];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < n_mels; i += kFftThreads) {
-    mfirst[i] = mt.first[i];
-    mcount[i] = mt.count[i];
-    moff[i] = mt.offset[i];
-  }
-  for (int i = tid; i < kMelWCap; i += kFftThreads) mw[i] = mt.w[i];  // (the table allocation holds n_mels x 201)
+  // ---- prologue: every global load first (one round trip), then the LDS stores ----
   const float* x = pcm + (long)b * stride;
-  const long Lp = N + kHop;  // padded length
-  const long period = 2 * (Lp - 1);
-  const long j0 = (long)f0 * kHop - kFFT / 2;
-  for (int i = tid; i < kFftSeg; i += kFftThreads) {
-    const long j = j0 + i;
-    long m = j;
-    if (j < 0 || j >= Lp) {  // reflect (only the frames at the buffer edges take the 64-bit modulo)
-      m = j % period;
-      if (m < 0) m += period;
-      if (m >= Lp) m = period - m;
+  const long j0 = (long)f0 * kHop - kFFT / 2;  // a multiple of 4 (f0 160 - 200)
+  const bool interior = j0 >= 0 && j0 + kFftSeg <= N && (((uintptr_t)(x + j0)) & 15) == 0;
+  // the filterbank tables first (both paths), then the audio: every global load of the workgroup in flight together
+  int tf = 0, tcn = 0, to = 0;
+  if (tid < n_mels) {
+    tf = mt.first[tid];
+    tcn = mt.count[tid];
+    to = mt.offset[tid];
+  }
+  const float tw = mt.w[min(tid, kMelWCap - 1)];  // (the table allocation holds n_mels x 201 >= kMelWCap floats)
+  if (interior) {
+    const float4* xv = reinterpret_cast<const float4*>(x + j0);
+    const float4 a0 = xv[tid], a1 = xv[tid + kFftThreads], a2 = xv[min(tid + 2 * kFftThreads, kSegVec - 1)];
+    float4* av = reinterpret_cast<float4*>(aud);
+    av[tid] = a0;
+    av[tid + kFftThreads] = a1;
+    if (tid + 2 * kFftThreads < kSegVec) av[tid + 2 * kFftThreads] = a2;
+  } else {  // the window's edge blocks (and unaligned rows): reflect / zero padding, sample by sample
+    const long Lp = N + kHop;  // padded length
+    const long period = 2 * (Lp - 1);
+    for (int i = tid; i < kFftSeg; i += kFftThreads) {
+      const long j = j0 + i;
+      long m = j;
+      if (j < 0 || j >= Lp) {  // reflect (only the frames at the buffer edges take the 64-bit modulo)
+        m = j % period;
+        if (m < 0) m += period;
+        if (m >= Lp) m = period - m;
+      }
+      aud[i] = (m < N) ? x[m] : 0.0f;
     }
-    aud[i] = (m < N) ? x[m] : 0.0f;
   }
-  for (int j = tid; j < kFFT; j += kFftThreads) {
+  {  // the W400 table
     float sv, cv;
-    sincospif(2.0f * (float)j / (float)kFFT, &sv, &cv);
-    tc[j] = cv;
-    ts[j] = sv;
+    sincospif(2.0f * (float)min(tid, kFFT - 1) / (float)kFFT, &sv, &cv);
+    if (tid < kFFT) {
+      tc[tid] = cv;
+      ts[tid] = sv;
+    }
   }
+  if (tid < n_mels) {
+    mfirst[tid] = tf;
+    mcount[tid] = tcn;
+    moff[tid] = to;
+  }
+  if (tid < kMelWCap) mw[tid] = tw;
   __syncthreads();
   // pass 1: (frame, n2) -> Y[frame][k1][n2], k1 = 0..10; periodic Hann w[n] = 0.5 - 0.5 cos(2 pi n / 400)
-  for (int it = tid; it < kFftFrames * 20; it += kFftThreads) {
-    const int fr = it / 20, n2 = it - fr * 20;
+  {
+    const int fr = tid / 20, n2 = tid - fr * 20;
     float a[20];
 #pragma unroll
     for (int n1 = 0; n1 < 20; ++n1) {
@@ -231,28 +202,24 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
   // pass 2: (frame, k1) -> |X[k1 + 20 k2]|^2 for the bins <= 200 (one item per thread: kFftThreads = frames x 20)
   static_assert(kFftThreads == kFftFrames * 20, "pass 2 keeps its item's powers in registers across the barrier");
   float pv[11];
-  int pfr = 0, pk1 = 0;
+  const int pfr = tid / 20, pk1 = tid - pfr * 20;
   {
-    const int it = tid;
-    const int fr = it / 20, k1 = it - fr * 20;
-    pfr = fr;
-    pk1 = k1;
-    const bool conj = k1 > 10;
-    const int kk = conj ? 20 - k1 : k1;
+    const bool conj = pk1 > 10;
+    const int kk = conj ? 20 - pk1 : pk1;
     float tr[20], ti[20];
 #pragma unroll
     for (int n2 = 0; n2 < 20; ++n2) {
-      const float2 y = Y[(fr * 11 + kk) * kYS + n2];
+      const float2 y = Y[(pfr * 11 + kk) * kYS + n2];
       const float yr = y.x, yi = conj ? -y.y : y.y;
-      const int j = (n2 * k1) % kFFT;  // W400^(n2 k1) = cos - i sin
+      const int j = (n2 * pk1) % kFFT;  // W400^(n2 k1) = cos - i sin
       const float c = tc[j], sn = ts[j];
       tr[n2] = yr * c + yi * sn;
       ti[n2] = yi * c - yr * sn;
     }
 #pragma unroll
     for (int k2 = 0; k2 <= 10; ++k2) {
-      const int k = k1 + 20 * k2;
-      if (k > 200) break;
+      // (k2 = 10 holds bin 200 for k1 = 0 only; the others compute a discarded value: no branch, so pv stays in
+      // registers)
       float xr = 0.f, xi = 0.f;
 #pragma unroll
       for (int n2 = 0; n2 < 20; ++n2) {
@@ -266,23 +233,33 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
   __syncthreads();  // every thread has read Y: its space becomes the power image
 #pragma unroll
   for (int k2 = 0; k2 <= 10; ++k2)
-    if (pk1 + 20 * k2 <= 200) pw[pfr * (kBinTiles * 16) + pk1 + 20 * k2] = pv[k2];
+    if (pk1 + 20 * k2 <= 200) pw[pfr * kBinsPad + pk1 + 20 * k2] = pv[k2];
   __syncthreads();
-  // sparse filterbank + log10; thread -> (frame = tid & 31, mel stride 8)
+  // sparse filterbank + log10; thread -> (frame = tid & 31, mel = tid / 32 + 20 it); a mel's 32 frames are one
+  // aligned half-wave, so its in-window min is a 32-lane reduction (every lane of the wave takes part)
   float bmax = -INFINITY;
   const int fr = tid & (kFftFrames - 1);
   const int f = f0 + fr;
-  const bool valid = f < F;
-  constexpr int kPB = kBinTiles * 16;
-  for (int m = tid / kFftFrames; m < n_mels; m += kFftThreads / kFftFrames) {
-    const int s0 = mfirst[m], cnt = mcount[m], off = moff[m];
-    float acc = 0.f;
-    for (int i = 0; i < cnt; ++i) acc += mw[off + i] * pw[fr * kPB + s0 + i];
-    const float v = log10f(fmaxf(acc, 1e-10f));
-    if (valid) {
-      raw[((long)b * n_mels + m) * fcap + f] = v;
-      bmax = fmaxf(bmax, v);
+  const int t = f - win.sk;
+  const bool valid = f >= 0 && f < F;
+  const bool inwin = valid && t >= 0 && t < win.size;
+  const int iters = (n_mels + kFftThreads / kFftFrames - 1) / (kFftThreads / kFftFrames);
+  for (int it = 0; it < iters; ++it) {
+    const int m = tid / kFftFrames + it * (kFftThreads / kFftFrames);
+    float vn = INFINITY;
+    if (m < n_mels) {
+      const int s0 = mfirst[m], cnt = mcount[m], off = moff[m];
+      float acc = 0.f;
+      for (int i = 0; i < cnt; ++i) acc += mw[off + i] * pw[fr * kBinsPad + s0 + i];
+      const float v = log10f(fmaxf(acc, 1e-10f));
+      if (valid) bmax = fmaxf(bmax, v);
+      if (inwin) {
+        vn = (v + 4.0f) * 0.25f;
+        out[((long)b * n_mels + m) * kOutFrames + t] = vn;
+      }
     }
+    const float mn = half_min32(vn);
+    if (m < n_mels && fr == 0) smin[m] = mn;
   }
   bmax = wave_max(bmax);
   __shared__ float red[kFftThreads / 64];
@@ -291,67 +268,58 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
   if (tid == 0) {
     float mx = red[0];
     for (int w2 = 1; w2 < kFftThreads / 64; ++w2) mx = fmaxf(mx, red[w2]);
-    atomicMax(&wmax[b], enc_max(mx));
+    *smax = mx;
   }
 }
 
-static bool logmel_use_gemm() {  // WMX_LOGMEL_GEMM=1: the DFT-as-GEMM form (A/B and parity reference runs)
-  static const bool v = getenv("WMX_LOGMEL_GEMM") != nullptr;
-  return v;
-}
+double logmel_flops_per_frame() { return 53600.0; }
 
-double logmel_flops_per_frame() { return logmel_use_gemm() ? 400.0 * 416 * 2 : 53600.0; }
-
-// out[b][m][t] = (max(raw, max_b - 8) + 4) / 4 for t < segment_size, else 0
-__global__ __launch_bounds__(256) void logmel_finalize_kernel(const float* __restrict__ raw, const long* __restrict__ lens,
-                                                              const int* __restrict__ seek, const int* __restrict__ wmax,
-                                                              int n_mels, int fcap, float* __restrict__ out, int B) {
-  const long total = (long)B * n_mels * 3000;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int t = (int)(i % 3000);
-    const long bm = i / 3000;
-    const int b = (int)(bm / n_mels);
-    const int F = (int)(lens[b] / kHop) + 1;
-    const int sk = seek ? seek[b] : 0;
-    const int size = min(3000, F - 1 - sk);
-    float v = 0.f;
-    if (t < size) {
-      const float mx = dec_max(wmax[b]);
-      v = (fmaxf(raw[bm * fcap + sk + t], mx - 8.0f) + 4.0f) * 0.25f;
+// one workgroup per (32-frame output block, window), one thread per mel
+__global__ __launch_bounds__(128) void logmel_clamp_kernel(const long* __restrict__ lens, const int* __restrict__ seek,
+                                                           int n_mels, const float* __restrict__ stats, int nblk,
+                                                           float* __restrict__ out) {
+  const int b = blockIdx.y, j = blockIdx.x, B = gridDim.y;
+  const MelWin win = mel_win(lens, seek, b);
+  const int tid = threadIdx.x;
+  // the window max over every block of the window
+  float mx = -INFINITY;
+  for (int i = tid; i < nblk; i += 128) mx = fmaxf(mx, stats[(long)b * nblk + i]);
+  mx = wave_max(mx);
+  __shared__ float red[2];
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  const float gmax = fmaxf(red[0], red[1]);
+  const float thr = (gmax - 8.0f + 4.0f) * 0.25f;  // (fl(gmax - 8) + 4) / 4
+  const int t0 = 32 * j, t1 = min(t0 + 32, kOutFrames);
+  // output block j is the fft kernel's block k = j + the blocks before the window's first frame
+  const int k = j + ((win.sk - win.fbase) >> 5);
+  for (int m = tid; m < n_mels; m += 128) {
+    float* row = out + ((long)b * n_mels + m) * kOutFrames;
+    for (int t = max(t0, win.size); t < t1; ++t) row[t] = 0.f;  // pad_or_trim
+    if (t0 < win.size && k < nblk && stats[(long)B * nblk + ((long)b * nblk + k) * n_mels + m] < thr) {
+      for (int t = t0; t < min(t1, win.size); ++t) row[t] = fmaxf(row[t], thr);
     }
-    out[i] = v;
   }
 }
 
-size_t logmel_smem_bytes() { return (size_t)(kSeg + 2 * kKChunk * kCols) * sizeof(float); }
+int logmel_blocks(int max_frames) { return (max_frames + 31) / 32 + 1; }
 
 void launch_logmel(const float* pcm, long stride, const long* lens_dev, const int* seek_dev, int B, int max_frames,
-                   const float* basis, const int* mfirst, const int* mcount, const int* moff, const float* mw,
-                   int n_mels, float* raw, int fcap, int* wmax, float* out, hipStream_t st) {
+                   const int* mfirst, const int* mcount, const int* moff, const float* mw, int n_mels, float* stats,
+                   long stats_cap, float* out, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    WMX_HIP(hipFuncSetAttribute((const void*)logmel_raw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)logmel_smem_bytes()));
     WMX_HIP(hipFuncSetAttribute((const void*)logmel_fft_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)logmel_fft_smem_bytes()));
     attr = true;
   }
-  WMX_HIP(hipMemsetD32Async((hipDeviceptr_t)wmax, (int)0x80000000, B, st));
-  MelTable mt{mfirst, mcount, moff, mw};
   WMX_CHECK(n_mels <= kMaxMels, "logmel: n_mels");
-  if (logmel_use_gemm()) {
-    dim3 g1(cdiv(max_frames, kFramesPerWG), B);
-    hipLaunchKernelGGL(logmel_raw_kernel, g1, dim3(256), logmel_smem_bytes(), st, pcm, stride, lens_dev, basis, mt,
-                       n_mels, raw, fcap, wmax);
-  } else {
-    dim3 g1(cdiv(max_frames, kFftFrames), B);
-    hipLaunchKernelGGL(logmel_fft_kernel, g1, dim3(kFftThreads), logmel_fft_smem_bytes(), st, pcm, stride, lens_dev, mt,
-                       n_mels, raw, fcap, wmax);
-  }
-  long total = (long)B * n_mels * 3000;
-  int g2 = (int)std::min<long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(logmel_finalize_kernel, dim3(g2), dim3(256), 0, st, raw, lens_dev, seek_dev, wmax, n_mels, fcap,
-                     out, B);
+  const int nblk = logmel_blocks(max_frames);
+  WMX_CHECK((long)B * nblk * (1 + n_mels) <= stats_cap, "logmel: statistics buffer too small");
+  hipLaunchKernelGGL(logmel_fft_kernel, dim3(nblk, B), dim3(kFftThreads), logmel_fft_smem_bytes(), st, pcm, stride,
+                     lens_dev, seek_dev, MelTable{mfirst, mcount, moff, mw}, n_mels, out, stats, nblk);
+  hipLaunchKernelGGL(logmel_clamp_kernel, dim3(cdiv(kOutFrames, 32), B), dim3(128), 0, st, lens_dev, seek_dev, n_mels,
+                     stats, nblk, out);
   WMX_HIP(hipGetLastError());
 }
 

@@ -166,6 +166,7 @@ struct Model {
   float* i8stok = nullptr;  // CT2 scales of the token embedding (the logits projection)
   std::map<std::string, std::pair<float*, long>> i8_scale_dst;  // weight name -> (its scale rows, row count)
   size_t param_bytes = 0;  // the arena's parameter region [0, param_bytes): what a weight broadcast must carry
+  std::vector<std::pair<size_t, size_t>> guards;  // debug guard gaps (WMX_GUARD), Planner::guards
   char* arena = nullptr;
   size_t arena_bytes = 0;
   int K1p = 0;
@@ -177,7 +178,6 @@ struct Model {
   std::vector<TensorEntry> entries;
   std::map<std::string, int> by_name;
   // log-mel constants
-  float* mel_basis = nullptr;
   int *mel_first = nullptr, *mel_count = nullptr, *mel_off = nullptr;
   float* mel_w = nullptr;
   bool initialized = false;
@@ -196,10 +196,18 @@ struct Model {
 struct Planner {
   size_t off = 0;
   std::vector<std::pair<void**, size_t>> items;
+  // debug (WMX_GUARD=1 at model / context creation): a guard gap after every buffer, filled with a byte pattern and
+  // checked by wmx_debug_guard_check -- an out-of-bounds write names the buffer it ran past
+  size_t guard = 0;
+  std::vector<std::pair<size_t, size_t>> guards;  // (offset, bytes) of each buffer's trailing gap, in add order
   template <class T>
   void add(T** p, size_t elems) {
     items.push_back({(void**)p, off});
     off += (elems * sizeof(T) + 255) / 256 * 256;
+    if (guard) {
+      guards.push_back({off, guard});
+      off += guard;
+    }
   }
   void bind(char* base) {
     for (auto& it : items) *it.first = base + it.second;
@@ -217,6 +225,7 @@ static void build_model(Model& m) {
   // then everything derived from it on each rank (positions, MX-fp8 / folded / row-major / 8-bit copies, log-mel
   // constants), so a broadcast of [0, param_bytes) is all a rank needs before wmx_model_arena_loaded
   Planner P;
+  P.guard = getenv("WMX_GUARD") ? 65536 : 0;
   P.add(&m.conv1w, (size_t)da * m.K1p);
   P.add(&m.conv1b, da);
   P.add(&m.conv2w, (size_t)da * 3 * da);
@@ -342,7 +351,6 @@ static void build_model(Model& m) {
     P.add(&m.tok8s, (size_t)Vp);
   }
   // log-mel constants
-  P.add(&m.mel_basis, (size_t)400 * 416);
   P.add(&m.mel_first, M);
   P.add(&m.mel_count, M);
   P.add(&m.mel_off, M);
@@ -350,6 +358,8 @@ static void build_model(Model& m) {
   m.arena_bytes = P.off;
   WMX_HIP(hipMalloc(&m.arena, m.arena_bytes));
   WMX_HIP(hipMemsetAsync(m.arena, 0, m.arena_bytes, m.st));
+  for (const auto& g : P.guards) WMX_HIP(hipMemsetAsync(m.arena + g.first, 0xA5, g.second, m.st));
+  m.guards = P.guards;
   P.bind(m.arena);
 
   // tensor registry, in oracle/whisper_np.py tensor_specs order (tid = index)
@@ -436,19 +446,9 @@ static void build_model(Model& m) {
     }
   }
 
-  // constants: sinusoids, DFT basis (Hann folded, re | im blocks of 208), sparse mel filterbank
+  // constants: sinusoids, sparse mel filterbank
   auto pos = sinusoids(1500, da);
   WMX_HIP(hipMemcpyAsync(m.enc_pos, pos.data(), pos.size() * 4, hipMemcpyHostToDevice, m.st));
-  std::vector<float> basis((size_t)400 * 416, 0.f);
-  for (int n = 0; n < 400; ++n) {
-    const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * n / 400.0);
-    for (int k = 0; k < 201; ++k) {
-      const double ang = 2.0 * M_PI * (double)((long)n * k % 400) / 400.0;
-      basis[(size_t)n * 416 + k] = (float)(w * std::cos(ang));
-      basis[(size_t)n * 416 + 208 + k] = (float)(-w * std::sin(ang));
-    }
-  }
-  WMX_HIP(hipMemcpyAsync(m.mel_basis, basis.data(), basis.size() * 4, hipMemcpyHostToDevice, m.st));
   auto fw = mel_filters(M);
   std::vector<int> first(M), count(M), off(M);
   std::vector<float> wts;
@@ -670,8 +670,9 @@ struct Ctx {
   float* pcm = nullptr;
   long* lens = nullptr;
   int* seek = nullptr;
-  float *mel_raw = nullptr, *mel = nullptr;
-  int* wmax = nullptr;
+  float *mel_stats = nullptr, *mel = nullptr;  // log-mel block statistics [B][nblk][1 + M], the encoder input
+  std::vector<std::pair<size_t, size_t>> guards;  // debug guard gaps (WMX_GUARD), Planner::guards
+  long mel_stats_cap = 0;
   uint16_t *im1 = nullptr, *h1 = nullptr, *im2 = nullptr, *ehb = nullptr, *eqkv = nullptr, *eao = nullptr, *ef1 = nullptr,
            *enc_out = nullptr, *ckv = nullptr;
   // fp8 decode: the cross K / V^T images in e4m3 (launch_crosskv_quant of ckv) + one scale per image [L*2][maxB][H]
@@ -779,11 +780,12 @@ static void alloc_ctx(Ctx& c) {
   // split-K workspace: up to 8 splits of the widest decoder GEMM (4*dt) over R rows
   c.ws_elems = (long)8 * std::max(R, 64) * 4 * dt;
   Planner P;
+  P.guard = getenv("WMX_GUARD") ? 65536 : 0;
   P.add(&c.pcm, (size_t)B * c.max_samples);
   P.add(&c.lens, B);
   P.add(&c.seek, B);
-  P.add(&c.mel_raw, (size_t)B * M * c.fcap);
-  P.add(&c.wmax, B);
+  c.mel_stats_cap = (long)B * logmel_blocks(c.fcap) * (1 + M);
+  P.add(&c.mel_stats, (size_t)c.mel_stats_cap);
   P.add(&c.mel, (size_t)B * M * 3000);
   P.add(&c.im1, (size_t)B * 3000 * c.m->K1p);
   P.add(&c.h1, (size_t)B * 3000 * da);
@@ -874,6 +876,8 @@ static void alloc_ctx(Ctx& c) {
   P.add(&c.a_heads, c.a_heads_cap + 8);
   WMX_HIP(hipMalloc(&c.buf, P.off));
   WMX_HIP(hipMemsetAsync(c.buf, 0, P.off, c.st));
+  for (const auto& g : P.guards) WMX_HIP(hipMemsetAsync(c.buf + g.first, 0xA5, g.second, c.st));
+  c.guards = P.guards;
   P.bind(c.buf);
   WMX_HIP(hipHostMalloc(&c.pinned_i, 64));
   // (the pinned alignment images, maxB * 448 * 1500 * 4 bytes, are allocated on the first word-alignment pass: a
@@ -1684,8 +1688,8 @@ static void logmel_dev(Ctx& c, const float* pcm_dev, long stride, const long* le
   WMX_HIP(hipMemcpyAsync(c.lens, lens_host, B * sizeof(long), hipMemcpyHostToDevice, c.st));
   WMX_HIP(hipMemcpyAsync(c.seek, sk.data(), B * 4, hipMemcpyHostToDevice, c.st));
   debug_device("before logmel");
-  launch_logmel(pcm_dev, stride, c.lens, c.seek, B, (int)(maxlen / 160) + 1, m.mel_basis, m.mel_first, m.mel_count,
-                m.mel_off, m.mel_w, m.d.n_mels, c.mel_raw, c.fcap, c.wmax, out_dev, c.st);
+  launch_logmel(pcm_dev, stride, c.lens, c.seek, B, (int)(maxlen / 160) + 1, m.mel_first, m.mel_count, m.mel_off,
+                m.mel_w, m.d.n_mels, c.mel_stats, c.mel_stats_cap, out_dev, c.st);
   debug_device("logmel");
   sync(c);  // sk / lens host vectors
 }
@@ -2853,6 +2857,27 @@ wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int sp
   });
 }
 
+// debug (WMX_GUARD=1 at creation): the first guard gap of the model / context arena whose pattern was overwritten:
+// *model_buf / *ctx_buf = the index (in planner add order) of the buffer it follows, -1 when intact
+static int guard_scan(const char* base, const std::vector<std::pair<size_t, size_t>>& g, hipStream_t st) {
+  std::vector<unsigned char> h;
+  WMX_HIP(hipStreamSynchronize(st));
+  for (size_t i = 0; i < g.size(); ++i) {
+    h.resize(g[i].second);
+    WMX_HIP(hipMemcpy(h.data(), base + g[i].first, g[i].second, hipMemcpyDeviceToHost));
+    for (unsigned char v : h)
+      if (v != 0xA5) return (int)i;
+  }
+  return -1;
+}
+wmx_status wmx_debug_guard_check(wmx_model* w, wmx_ctx* x, int* model_buf, int* ctx_buf) {
+  return guard([&] {
+    WMX_CHECK(model_buf && ctx_buf, "guard_check: null argument");
+    *model_buf = w ? guard_scan(w->m.arena, w->m.guards, w->m.st) : -1;
+    *ctx_buf = x ? guard_scan(x->c.buf, x->c.guards, x->c.st) : -1;
+  });
+}
+
 wmx_status wmx_debug_dtw(const float* x, int N, int M, int ld, int32_t* ti, int32_t* tj, int* len) {
   return guard([&] {
     WMX_CHECK(x && ti && tj && len && N >= 1 && M >= 1 && ld >= M, "debug_dtw: arguments");
@@ -3283,8 +3308,8 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       by = (double)B * (480000.0 * 4 + m.d.n_mels * 3000.0 * 4);
       fl = (double)B * 3001 * logmel_flops_per_frame();
       fn = [&c, &m, B] {
-        launch_logmel(c.pcm, std::min<long>(480000, c.max_samples), c.lens, c.seek, B, 3001, m.mel_basis, m.mel_first,
-                      m.mel_count, m.mel_off, m.mel_w, m.d.n_mels, c.mel_raw, c.fcap, c.wmax, c.mel, c.st);
+        launch_logmel(c.pcm, std::min<long>(480000, c.max_samples), c.lens, c.seek, B, 3001, m.mel_first, m.mel_count,
+                      m.mel_off, m.mel_w, m.d.n_mels, c.mel_stats, c.mel_stats_cap, c.mel, c.st);
       };
     } else if (kernel == 4) {
       by = 4.0 * dt * dt * (m.w8 ? 1 : 2) + (double)R * dt * 2 + (double)R * 4 * dt * 2;

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("WMX_LIB", os.path.join(_HERE, "libwmx.so"))
+_DEFAULT_LIB = os.path.join(_HERE, "libwmx.so")
+LIB_PATH = os.environ.get("WMX_LIB", _DEFAULT_LIB)
 
 WMX_DTYPE_BF16, WMX_DTYPE_F16, WMX_DTYPE_MX8, WMX_DTYPE_I8, WMX_DTYPE_I8_BF16 = 0, 1, 2, 3, 4
 WMX_TASK_TRANSCRIBE, WMX_TASK_TRANSLATE = 0, 1
@@ -66,6 +67,7 @@ DIAG_EXPORTS = [
     "wmx_ctx_forced_decode", "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_record",
     "wmx_ctx_recorded", "wmx_ctx_alignment_matrix", "wmx_debug_packed_launch", "wmx_debug_dtw", "wmx_ctx_set_probe",
     "wmx_debug_lockstep_arrive", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_probe_ticks",
+    "wmx_debug_guard_check",
 ]
 
 
@@ -102,6 +104,7 @@ def _load():
                                             C.c_int]),
         "wmx_ctx_record": (C.c_int, [VP, C.c_int]),
         "wmx_debug_packed_launch": (C.c_int, [C.c_int, C.c_int, C.c_int, I64, C.c_int, I64, P(I64)]),
+        "wmx_debug_guard_check": (C.c_int, [VP, VP, P(C.c_int), P(C.c_int)]),
         "wmx_debug_dtw": (C.c_int, [P(C.c_float), C.c_int, C.c_int, C.c_int, P(C.c_int32), P(C.c_int32), P(C.c_int)]),
         "wmx_ctx_recorded": (C.c_int, [VP, P(F), P(I32), P(C.c_int), P(C.c_int)]),
         "wmx_ctx_alignment_matrix": (C.c_int, [VP, C.c_int, P(F), P(C.c_int), P(C.c_int)]),
@@ -133,6 +136,8 @@ def _load():
         "wmx_vad_stream": (VP, [VP]),
     }
     for name, (res, args) in sig.items():
+        if name in DIAG_EXPORTS and not hasattr(lib, name) and LIB_PATH != _DEFAULT_LIB:
+            continue  # (an older A/B build named by WMX_LIB may predate a diagnostic hook)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -93,14 +93,18 @@ def test_logmel_batched_matches_oracle(n_mels):
 def test_logmel_seek_window():
     E = _engine()
     m = E.Model("tiny", 0, "bfloat16")
-    ctx = E.Context(m, max_batch=2, beam_size=1, word_timestamps=False, max_audio_samples=640000)
+    ctx = E.Context(m, max_batch=3, beam_size=1, word_timestamps=False, max_audio_samples=640000)
     a = synth.speech_like(5, 560000)  # 35 s: second window starts at frame 3000
-    got = ctx.logmel([a, a], seek=[0, 3000])
+    # (seek 3000 and 1234 are not multiples of the kernel's 32-frame blocks: the block grid follows the seek)
+    got = ctx.logmel([a, a, a], seek=[0, 3000, 1234])
     feats = O.logmel(a, 80)
     np.testing.assert_allclose(got[0], feats[:, :3000], atol=1e-4)
     ref1 = np.zeros((80, 3000), np.float32)
     ref1[:, :500] = feats[:, 3000:3500]
     np.testing.assert_allclose(got[1], ref1, atol=1e-4)
+    ref2 = np.zeros((80, 3000), np.float32)
+    ref2[:, :2266] = feats[:, 1234:3500]
+    np.testing.assert_allclose(got[2], ref2, atol=1e-4)
 
 
 @pytest.fixture(scope="module")
