@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 METRIC = "real-time factor + p50 chunk latency, Whisper large-v3 30s@16kHz, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0
 MFMA_BF16_PEAK_TFLOPS = 2500.0
+MAX_CLOCK_MHZ = 2400.0  # MI355X_MICROARCH.md: the clock the dense peaks are quoted at
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak, spec
 
 
@@ -114,6 +115,26 @@ def check_env():
             f"is not the product path (documented knobs: {sorted(BENCH_ENV_KNOBS)})")
         sys.exit(2)
     return env
+
+
+def held_clock(run, device=0, ms=120.0, n=8):
+    """The shader clock the chip holds while `run()` executes (the clock in the encoder field):
+    n single-wave workgroups of libwmx's clock probe (wmx_debug_clock_start / _result, include/wmx_diag.h) sleep on
+    a stream of their own for `ms` of the 100 MHz constant clock, started just before `run`, each reporting
+    d(s_memtime) / d(s_memrealtime) x 100 MHz on its XCD.  Returns (run's result, {median / min / max MHz, ...})."""
+    import ctypes as C
+    from wmx._lib import lib, check
+    check(lib.wmx_debug_clock_start(device, ms, n))
+    try:
+        res = run()
+    finally:
+        buf = (C.c_float * n)()
+        check(lib.wmx_debug_clock_result(buf, n))
+    v = sorted(float(x) for x in buf)
+    return res, {"median_mhz": round(v[n // 2], 1), "min_mhz": round(v[0], 1), "max_mhz": round(v[-1], 1),
+                 "window_ms": ms, "probes": n,
+                 "how": "in-kernel d(s_memtime)/d(s_memrealtime) x 100 MHz of n sleeping waves (one per XCD) over "
+                        "the first window_ms of the passes (MI355X_MICROARCH.md 'DVFS give-back' item 6)"}
 
 
 def _cpu_sample(W, d, args, steps_done, n_text):
@@ -626,10 +647,10 @@ def main():
     if G > 1:
         scratch = engine.Context(model, max_batch=B, beam_size=1, max_new_tokens=8, word_timestamps=False,
                                  use_graph=False)
-        (e_ms_b, _, e_fl_b), e_runs_b = med3(scratch, B)
+        ((e_ms_b, _, e_fl_b), e_runs_b), sclk = held_clock(lambda: med3(scratch, B), device=local)
         scratch.close()
     else:
-        e_runs_b = e_runs
+        ((e_ms_b, _, e_fl_b), e_runs_b), sclk = held_clock(lambda: med3(ctx, B), device=local)
     e_tf_b = e_fl_b / (e_ms_b * 1e-3) / 1e12
     encoder = {"windows": Bg, "gflop_per_window": round(e_fl / Bg / 1e9, 1), "isolated_ms": round(e_ms, 2),
                "isolated_tflops": round(e_tf, 1), "isolated_mfma_util": round(e_tf / MFMA_BF16_PEAK_TFLOPS, 4),
@@ -638,7 +659,10 @@ def main():
                                       "mfma_util": round(e_tf_b / MFMA_BF16_PEAK_TFLOPS, 4),
                                       "passes_ms": e_runs_b,
                                       "best_mfma_util": round(e_fl_b / (min(e_runs_b) * 1e-3) / 1e12 /
-                                                              MFMA_BF16_PEAK_TFLOPS, 4)},
+                                                              MFMA_BF16_PEAK_TFLOPS, 4),
+                                      "held_clock": sclk,
+                                      "mfma_util_at_held_clock": round(e_tf_b / (MFMA_BF16_PEAK_TFLOPS *
+                                                                       sclk["median_mhz"] / MAX_CLOCK_MHZ), 4)},
                "insitu_stage_ms": round(stages[1], 2),
                "insitu_tflops": round(insitu_tf, 1) if insitu_tf else None,
                "insitu_mfma_util": round(insitu_tf / MFMA_BF16_PEAK_TFLOPS, 4) if insitu_tf else None,

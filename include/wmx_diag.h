@@ -71,6 +71,12 @@ wmx_status wmx_debug_packed_launch(int M, int N, int K, int64_t part_cap, int sp
  * 64 KiB guard gap holding a byte pattern; *model_buf / *ctx_buf = the index (allocation order) of the first buffer
  * whose gap was overwritten, -1 when every gap is intact (either handle may be NULL). */
 wmx_status wmx_debug_guard_check(wmx_model* m, wmx_ctx* c, int* model_buf, int* ctx_buf);
+/* Shader clock beside a workload (bench.py's encoder field): start launches n single-wave workgroups on a stream of
+ * their own (workgroup i on XCD i mod 8) that sleep for ms milliseconds of the 100 MHz constant clock and returns at
+ * once; result waits for them and writes each one's shader clock, d(s_memtime) / d(s_memrealtime) x 100 MHz, to
+ * mhz[n].  One probe pending at a time. */
+wmx_status wmx_debug_clock_start(int device, double ms, int n);
+wmx_status wmx_debug_clock_result(float* mhz, int n);
 /* Host-only (no GPU call): the word-alignment DTW of wmx_transcribe on a caller alignment matrix x[N][ld] (first M
  * columns; the DTW cost is -x, as openai timing calls dtw(-matrix)), returning the backtraced path (ti[k], tj[k]),
  * k < *len <= N + M, in path order from (0, 0).

@@ -157,6 +157,8 @@ __host__ __device__ inline long packed8_index(long n, long k, long K) {
 // (N padded entries 0), and optionally rm = the dequantized row-major [N][K] 16-bit copy (many-row passes)
 // the CTranslate2 int8 grid (model dtype I8): per-row CT2 scales (derived: 127 / max|row|, or given), int8 bytes in the
 // packed8_index layout, the GEMM's row multipliers 1 / scale, and the row-major dequantized copy (rm, optional)
+// shader-clock probe (bench diagnostic): n workgroups each write the MHz they ran at for `ms` of wall time
+void launch_clock_probe(float* out, int n, double ms, hipStream_t st);
 void launch_i8_quantize(DT dt, const uint16_t* src, int N, int K, float* ct2s, uint8_t* q8, float* mult, uint16_t* rm,
                         hipStream_t st);
 void launch_w8_quantize(DT dt, const uint16_t* src, int N, int K, uint8_t* q8, float* scale, uint16_t* rm,

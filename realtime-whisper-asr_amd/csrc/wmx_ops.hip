@@ -903,4 +903,26 @@ void launch_init_tensor(DT dt, uint64_t seed, const InitSpec& s, hipStream_t st)
   WMX_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------------------------------------------------------
+// Shader-clock probe (bench.py's encoder field, diagnostic): one wave per workgroup sleeps until `rt_ticks` of the
+// 100 MHz constant clock have passed and reports the shader clock it ran at, d(s_memtime) / d(s_memrealtime) x
+// 100 MHz (MI355X_MICROARCH.md 'DVFS give-back' item 6).  Launched beside a workload on a stream of its own; a
+// deadline on the constant clock bounds every wave.  Workgroup i lands on XCD i mod 8.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void clock_probe_kernel(float* __restrict__ out, long long rt_ticks) {
+  const long long r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
+  long long r = r0;
+  while (r - r0 < rt_ticks) {
+    __builtin_amdgcn_s_sleep(127);
+    r = __builtin_amdgcn_s_memrealtime();
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)((double)(t1 - t0) / (double)(r - r0) * 100.0);
+}
+
+void launch_clock_probe(float* out, int n, double ms, hipStream_t st) {
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(n), dim3(64), 0, st, out, (long long)(ms * 1e5));
+  WMX_HIP(hipGetLastError());
+}
+
 }  // namespace wmx

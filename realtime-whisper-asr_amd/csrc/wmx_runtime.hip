@@ -2878,6 +2878,42 @@ wmx_status wmx_debug_guard_check(wmx_model* w, wmx_ctx* x, int* model_buf, int* 
   });
 }
 
+// the shader-clock probe beside a workload: start launches it on a stream of its own and returns; result waits
+// for it and copies the n per-workgroup clocks (MHz)
+static struct {
+  hipStream_t st = nullptr;
+  float* buf = nullptr;
+  int n = 0, device = -1;
+} g_clock;
+
+wmx_status wmx_debug_clock_start(int device, double ms, int n) {
+  return guard([&] {
+    WMX_CHECK(ms > 0 && ms <= 10000 && n >= 1 && n <= 256 && g_clock.n == 0, "clock_start: arguments / pending probe");
+    WMX_HIP(hipSetDevice(device));
+    if (g_clock.device != device) {
+      if (g_clock.st) (void)hipStreamDestroy(g_clock.st);
+      if (g_clock.buf) (void)hipFree(g_clock.buf);
+      g_clock.st = nullptr;
+      g_clock.buf = nullptr;
+      WMX_HIP(hipStreamCreateWithFlags(&g_clock.st, hipStreamNonBlocking));
+      WMX_HIP(hipMalloc((void**)&g_clock.buf, 256 * sizeof(float)));
+      g_clock.device = device;
+    }
+    launch_clock_probe(g_clock.buf, n, ms, g_clock.st);
+    g_clock.n = n;
+  });
+}
+
+wmx_status wmx_debug_clock_result(float* mhz, int n) {
+  return guard([&] {
+    WMX_CHECK(mhz && g_clock.n > 0 && n == g_clock.n, "clock_result: no probe pending / count");
+    WMX_HIP(hipSetDevice(g_clock.device));
+    g_clock.n = 0;
+    WMX_HIP(hipStreamSynchronize(g_clock.st));
+    WMX_HIP(hipMemcpy(mhz, g_clock.buf, n * sizeof(float), hipMemcpyDeviceToHost));
+  });
+}
+
 wmx_status wmx_debug_dtw(const float* x, int N, int M, int ld, int32_t* ti, int32_t* tj, int* len) {
   return guard([&] {
     WMX_CHECK(x && ti && tj && len && N >= 1 && M >= 1 && ld >= M, "debug_dtw: arguments");

@@ -67,7 +67,7 @@ DIAG_EXPORTS = [
     "wmx_ctx_forced_decode", "wmx_ctx_stage_ms", "wmx_ctx_last_steps", "wmx_ctx_bench_kernel", "wmx_ctx_record",
     "wmx_ctx_recorded", "wmx_ctx_alignment_matrix", "wmx_debug_packed_launch", "wmx_debug_dtw", "wmx_ctx_set_probe",
     "wmx_debug_lockstep_arrive", "wmx_ctx_probe_stats", "wmx_ctx_probe_launches", "wmx_ctx_probe_ticks",
-    "wmx_debug_guard_check",
+    "wmx_debug_guard_check", "wmx_debug_clock_start", "wmx_debug_clock_result",
 ]
 
 
@@ -105,6 +105,8 @@ def _load():
         "wmx_ctx_record": (C.c_int, [VP, C.c_int]),
         "wmx_debug_packed_launch": (C.c_int, [C.c_int, C.c_int, C.c_int, I64, C.c_int, I64, P(I64)]),
         "wmx_debug_guard_check": (C.c_int, [VP, VP, P(C.c_int), P(C.c_int)]),
+        "wmx_debug_clock_start": (C.c_int, [C.c_int, C.c_double, C.c_int]),
+        "wmx_debug_clock_result": (C.c_int, [P(F), C.c_int]),
         "wmx_debug_dtw": (C.c_int, [P(C.c_float), C.c_int, C.c_int, C.c_int, P(C.c_int32), P(C.c_int32), P(C.c_int)]),
         "wmx_ctx_recorded": (C.c_int, [VP, P(F), P(I32), P(C.c_int), P(C.c_int)]),
         "wmx_ctx_alignment_matrix": (C.c_int, [VP, C.c_int, P(F), P(C.c_int), P(C.c_int)]),
