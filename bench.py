@@ -698,7 +698,10 @@ def main():
                                f"word_timestamps, language auto-detect, max_new_tokens {args.max_new_tokens}",
                    "model": f"whisper-{args.model}", "global_batch": B * world, "seq_len": 480000,
                    "parallelism": f"dp{world} (independent streams)", "decode_steps": steps_done,
-                   "use_graph": not args.no_graph, "context_groups": G},
+                   "use_graph": not args.no_graph, "context_groups": G,
+                   **({"int8_rule": "int8 weights (CTranslate2's grid and row scales) x 16-bit activations; "
+                                    "CTranslate2's dynamic int8 activation quantisation is not applied "
+                                    "(INTEGRATION.md)"} if args.dtype == "int8" else {})},
         "stage_ms": [round(s, 2) for s in stages],
         "env": wmx_env,
         "decode_mode": decode_mode,

@@ -98,6 +98,9 @@ def test_int8_arena_copy_keeps_the_checkpoint_scales(ct2_int8):
 
 @pytest.mark.parametrize("B,K", [(4, 5), (20, 1)])
 def test_int8_forced_decode_matches_oracle(ct2_int8, B, K):
+    """The int8 rule the product runs (INTEGRATION.md 'The int8 arithmetic rule'): CTranslate2's int8 weight grid and
+    row scales against 16-bit activation rows: the oracle's int8_decoder_weights dequantizes the weights and keeps
+    the activations in the model's 16-bit type (CTranslate2's dynamic int8 activation rows are not restated)."""
     from wmx import engine as E
     import test_gpu_step as S
     m, deq, file_scales, W0 = ct2_int8
