@@ -43,10 +43,14 @@ struct MelTable {
 // LDS.  The prologue issues every global load of the workgroup (audio as 16-byte loads on the interior path, the
 // filterbank tables) before the first LDS store, so it costs one round trip.
 // ------------------------------------------------------------------------------------------------
-constexpr int kFftFrames = 32;
-constexpr int kFftThreads = kFftFrames * 20;  // 10 waves: one (frame, n2) item per thread in pass 1, (frame, k1) in pass 2
-constexpr int kFftSeg = kHop * (kFftFrames - 1) + kFFT;  // 5360 samples
-constexpr int kSegVec = kFftSeg / 4;                      // 1340 16-byte pieces
+#ifndef WMX_LOGMEL_FRAMES
+#define WMX_LOGMEL_FRAMES 32
+#endif
+constexpr int kFftFrames = WMX_LOGMEL_FRAMES;  // frames per workgroup = one output block (a power of two, 16 or 32)
+static_assert(kFftFrames == 16 || kFftFrames == 32, "log-mel: block size");
+constexpr int kFftThreads = kFftFrames * 20;  // one (frame, n2) item per thread in pass 1, (frame, k1) in pass 2
+constexpr int kFftSeg = kHop * (kFftFrames - 1) + kFFT;  // 5360 / 2800 samples
+constexpr int kSegVec = kFftSeg / 4;                      // 16-byte pieces
 static_assert(2 * kFftThreads < kSegVec && kSegVec <= 3 * kFftThreads, "interior audio: three 16-byte loads per thread");
 
 // cos / sin(2 pi m / 20), m = 0..19 (folded into the unrolled loops as literals)
@@ -65,30 +69,36 @@ __device__ constexpr float kS20[20] = {0.0f, 0.30901699437494742f, 0.58778525229
 
 // audio + Y (the power image reuses Y's space after pass 2) + the W400 table: 80 KB, two workgroups per CU
 constexpr int kYS = 21;  // Y row stride (float2): odd, so pass 2's per-thread row reads fall in different banks
-constexpr size_t kFftLdsUsed = (size_t)kFftSeg * 4 + (size_t)kFftFrames * 11 * kYS * 8 + 2 * kFFT * 4;  // 81.8 KiB
+constexpr size_t kFftLdsUsed = (size_t)kFftSeg * 4 + (size_t)kFftFrames * 11 * kYS * 8 + 2 * kFFT * 4;  // 81.8 KiB at 32
 // The launch requests the CU's whole LDS (160 KiB less the static tables), so no other workgroup shares the CU while
 // a block runs.  Measured (tools/conc_probe4.py / conc_probe6.py, round 6): with the 81.8 KiB it uses, a workgroup that
 // shared its CU with a co-running 128 x 128 LDS-DMA GEMM of another context (gemm_kernel, e.g. that context's
 // encoder at <= 2 windows) returned wrong spectra for a few frames of the block in 9-17 of 15-20 calls (whole frames,
 // up to 1.2 in normalised log-mel), although both kernels address only their own LDS; with the CU to itself, 0 of
 // 15.  The round-5 kernel (145 VGPRs) never shared a CU with such a GEMM; this one (88 VGPRs) could.  One workgroup
-// per CU is what either form runs anyway (81.8 KiB x 2 exceeds the CU's LDS).
+// per CU is what either form runs anyway (81.8 KiB x 2 exceeds the CU's LDS).  16-frame blocks (WMX_LOGMEL_FRAMES=16,
+// 47 KiB, three workgroups per CU) ran 23.2 us per 4 windows sharing CUs but showed the same fault (5 of 15 calls,
+// gpurun_out/r06g), and 35.8 us alone on the CU: the 32-frame exclusive form is the default.
 constexpr size_t kFftLdsStatic = 8192;  // (bound on the kernel's static __shared__ tables: 4.1 KiB)
 size_t logmel_fft_smem_bytes() { return 160 * 1024 - kFftLdsStatic; }
 static_assert(kFftLdsUsed <= 160 * 1024 - kFftLdsStatic, "log-mel: LDS image");
 
-// min over each aligned half-wave (32 lanes)
-__device__ inline float half_min32(float v) {
+// min over each aligned group of kFftFrames lanes (16: one DPP row; 32: two rows joined by permlane16_swap)
+__device__ inline float block_min(float v) {
   v = fminf(v, dpp_mov<kDppXor1>(v));
   v = fminf(v, dpp_mov<kDppXor2>(v));
   v = fminf(v, dpp_mov<kDppHalfMirror>(v));
   v = fminf(v, dpp_mov<kDppMirror>(v));
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  if constexpr (kFftFrames == 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  }
+  return v;
 }
 
 // the window's geometry: F STFT frames (the last one dropped from the output), content size of the output window,
-// its first frame; output block k of window b is frames f0(k) = (seek & 31 ? (seek & 31) - 32 : 0) + 32 k
+// its first frame; output block k of window b is frames f0(k) = fbase + kFftFrames k, fbase = (seek mod kFftFrames) -
+// kFftFrames (0 when seek is a multiple), so that the blocks align with the output window's frames
 struct MelWin {
   int F, sk, size, fbase;
 };
@@ -97,8 +107,8 @@ __device__ inline MelWin mel_win(const long* lens, const int* seek, int b) {
   w.F = (int)(lens[b] / kHop) + 1;
   w.sk = seek ? seek[b] : 0;
   w.size = max(0, min(kOutFrames, w.F - 1 - w.sk));
-  const int fb = w.sk & 31;
-  w.fbase = fb ? fb - 32 : 0;
+  const int fb = w.sk & (kFftFrames - 1);
+  w.fbase = fb ? fb - kFftFrames : 0;
   return w;
 }
 
@@ -112,7 +122,7 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
   const MelWin win = mel_win(lens, seek, b);
   const long N = lens[b];
   const int F = win.F;
-  const int f0 = win.fbase + 32 * blk;
+  const int f0 = win.fbase + kFftFrames * blk;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* smax = stats + (long)b * nblk + blk;
   float* smin = stats + (long)B * nblk + ((long)b * nblk + blk) * n_mels;
@@ -141,7 +151,10 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
     tcn = mt.count[tid];
     to = mt.offset[tid];
   }
-  const float tw = mt.w[min(tid, kMelWCap - 1)];  // (the table allocation holds n_mels x 201 >= kMelWCap floats)
+  static_assert(kMaxMels <= kFftThreads && kMelWCap <= 2 * kFftThreads, "log-mel: table loads per thread");
+  // (the table allocation holds n_mels x 201 >= kMelWCap floats)
+  const float tw = mt.w[min(tid, kMelWCap - 1)];
+  const float tw2 = mt.w[min(tid + kFftThreads, kMelWCap - 1)];
   if (interior) {
     const float4* xv = reinterpret_cast<const float4*>(x + j0);
     const float4 a0 = xv[tid], a1 = xv[tid + kFftThreads], a2 = xv[min(tid + 2 * kFftThreads, kSegVec - 1)];
@@ -163,13 +176,11 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
       aud[i] = (m < N) ? x[m] : 0.0f;
     }
   }
-  {  // the W400 table
+  for (int j = tid; j < kFFT; j += kFftThreads) {  // the W400 table
     float sv, cv;
-    sincospif(2.0f * (float)min(tid, kFFT - 1) / (float)kFFT, &sv, &cv);
-    if (tid < kFFT) {
-      tc[tid] = cv;
-      ts[tid] = sv;
-    }
+    sincospif(2.0f * (float)j / (float)kFFT, &sv, &cv);
+    tc[j] = cv;
+    ts[j] = sv;
   }
   if (tid < n_mels) {
     mfirst[tid] = tf;
@@ -177,6 +188,7 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
     moff[tid] = to;
   }
   if (tid < kMelWCap) mw[tid] = tw;
+  if (tid + kFftThreads < kMelWCap) mw[tid + kFftThreads] = tw2;
   __syncthreads();
   // pass 1: (frame, n2) -> Y[frame][k1][n2], k1 = 0..10; periodic Hann w[n] = 0.5 - 0.5 cos(2 pi n / 400)
   {
@@ -235,8 +247,8 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
   for (int k2 = 0; k2 <= 10; ++k2)
     if (pk1 + 20 * k2 <= 200) pw[pfr * kBinsPad + pk1 + 20 * k2] = pv[k2];
   __syncthreads();
-  // sparse filterbank + log10; thread -> (frame = tid & 31, mel = tid / 32 + 20 it); a mel's 32 frames are one
-  // aligned half-wave, so its in-window min is a 32-lane reduction (every lane of the wave takes part)
+  // sparse filterbank + log10; thread -> (frame = tid mod kFftFrames, mel = tid / kFftFrames + 20 it); a mel's frames
+  // are one aligned lane group, so its in-window min is a lane reduction (every lane of the wave takes part)
   float bmax = -INFINITY;
   const int fr = tid & (kFftFrames - 1);
   const int f = f0 + fr;
@@ -258,7 +270,7 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
         out[((long)b * n_mels + m) * kOutFrames + t] = vn;
       }
     }
-    const float mn = half_min32(vn);
+    const float mn = block_min(vn);
     if (m < n_mels && fr == 0) smin[m] = mn;
   }
   bmax = wave_max(bmax);
@@ -274,7 +286,7 @@ __global__ __launch_bounds__(kFftThreads) void logmel_fft_kernel(const float* __
 
 double logmel_flops_per_frame() { return 53600.0; }
 
-// one workgroup per (32-frame output block, window), one thread per mel
+// one workgroup per (kFftFrames-frame output block, window), one thread per mel
 __global__ __launch_bounds__(128) void logmel_clamp_kernel(const long* __restrict__ lens, const int* __restrict__ seek,
                                                            int n_mels, const float* __restrict__ stats, int nblk,
                                                            float* __restrict__ out) {
@@ -290,9 +302,9 @@ __global__ __launch_bounds__(128) void logmel_clamp_kernel(const long* __restric
   __syncthreads();
   const float gmax = fmaxf(red[0], red[1]);
   const float thr = (gmax - 8.0f + 4.0f) * 0.25f;  // (fl(gmax - 8) + 4) / 4
-  const int t0 = 32 * j, t1 = min(t0 + 32, kOutFrames);
+  const int t0 = kFftFrames * j, t1 = min(t0 + kFftFrames, kOutFrames);
   // output block j is the fft kernel's block k = j + the blocks before the window's first frame
-  const int k = j + ((win.sk - win.fbase) >> 5);
+  const int k = j + (win.sk - win.fbase) / kFftFrames;
   for (int m = tid; m < n_mels; m += 128) {
     float* row = out + ((long)b * n_mels + m) * kOutFrames;
     for (int t = max(t0, win.size); t < t1; ++t) row[t] = 0.f;  // pad_or_trim
@@ -302,7 +314,7 @@ __global__ __launch_bounds__(128) void logmel_clamp_kernel(const long* __restric
   }
 }
 
-int logmel_blocks(int max_frames) { return (max_frames + 31) / 32 + 1; }
+int logmel_blocks(int max_frames) { return (max_frames + kFftFrames - 1) / kFftFrames + 1; }
 
 void launch_logmel(const float* pcm, long stride, const long* lens_dev, const int* seek_dev, int B, int max_frames,
                    const int* mfirst, const int* mcount, const int* moff, const float* mw, int n_mels, float* stats,
@@ -318,7 +330,7 @@ void launch_logmel(const float* pcm, long stride, const long* lens_dev, const in
   WMX_CHECK((long)B * nblk * (1 + n_mels) <= stats_cap, "logmel: statistics buffer too small");
   hipLaunchKernelGGL(logmel_fft_kernel, dim3(nblk, B), dim3(kFftThreads), logmel_fft_smem_bytes(), st, pcm, stride,
                      lens_dev, seek_dev, MelTable{mfirst, mcount, moff, mw}, n_mels, out, stats, nblk);
-  hipLaunchKernelGGL(logmel_clamp_kernel, dim3(cdiv(kOutFrames, 32), B), dim3(128), 0, st, lens_dev, seek_dev, n_mels,
+  hipLaunchKernelGGL(logmel_clamp_kernel, dim3(cdiv(kOutFrames, kFftFrames), B), dim3(128), 0, st, lens_dev, seek_dev, n_mels,
                      stats, nblk, out);
   WMX_HIP(hipGetLastError());
 }
