@@ -6,12 +6,12 @@
 //   of the first min(3000, F-1-seek) content frames, zero padded (pad_or_trim).
 //
 // Two launches, no memset, 13.8 MB of algorithmic HBM traffic per 4 windows moved about once (round 6):
-//   logmel_fft_kernel   one workgroup = 32 consecutive frames of one window, aligned so that its frames are one
-//                       32-frame block of the OUTPUT window (f0 = seek mod 32 + 32 k); writes (v + 4) / 4 of its
+//   logmel_fft_kernel   one workgroup = 16 consecutive frames of one window, aligned so that its frames are one
+//                       16-frame block of the OUTPUT window (f0 = seek mod 16 + 16 k); writes (v + 4) / 4 of its
 //                       in-window frames straight into the encoder input [B][n_mels][3000] and two statistics: the
 //                       block's max of v over every frame (the per-window max runs over the whole audio) and, per mel,
 //                       the min of its in-window values.  Plain stores of per-block partials: no atomics, no memset.
-//   logmel_clamp_kernel one workgroup = one 32-frame output block, one thread per mel: the window max from the block
+//   logmel_clamp_kernel one workgroup = one 16-frame output block, one thread per mel: the window max from the block
 //                       maxima, then only the (mel, block) row pieces whose min lies below max - 8 are read and
 //                       clamped (about 6 % of them on speech-like audio), and the pad frames are zeroed.
 // Rounding: max((v + 4) / 4, (fl(gmax - 8) + 4) / 4) equals (max(v, fl(gmax - 8)) + 4) / 4 bit for bit (x -> fl(x + 4)
@@ -43,10 +43,9 @@ struct MelTable {
 // LDS.  The prologue issues every global load of the workgroup (audio as 16-byte loads on the interior path, the
 // filterbank tables) before the first LDS store, so it costs one round trip.
 // ------------------------------------------------------------------------------------------------
-#ifndef WMX_LOGMEL_FRAMES
-#define WMX_LOGMEL_FRAMES 32
-#endif
-constexpr int kFftFrames = WMX_LOGMEL_FRAMES;  // frames per workgroup = one output block (a power of two, 16 or 32)
+// frames per workgroup = one output block: 16 (320 threads, 47 KiB of LDS, three workgroups per CU) ran 21.2 us per 4
+// windows against 30.9 for 32 (640 threads, 86 KiB, one per CU) (gpurun_out/r06p)
+constexpr int kFftFrames = 16;
 static_assert(kFftFrames == 16 || kFftFrames == 32, "log-mel: block size");
 constexpr int kFftThreads = kFftFrames * 20;  // one (frame, n2) item per thread in pass 1, (frame, k1) in pass 2
 constexpr int kFftSeg = kHop * (kFftFrames - 1) + kFFT;  // 5360 / 2800 samples
@@ -67,21 +66,16 @@ __device__ constexpr float kS20[20] = {0.0f, 0.30901699437494742f, 0.58778525229
                                        -0.95105651629515357f, -0.80901699437494742f, -0.58778525229247313f,
                                        -0.30901699437494742f};
 
-// audio + Y (the power image reuses Y's space after pass 2) + the W400 table: 80 KB, two workgroups per CU
+// audio + Y (the power image reuses Y's space after pass 2) + the W400 table: 42.9 KiB at 16 frames, three per CU
 constexpr int kYS = 21;  // Y row stride (float2): odd, so pass 2's per-thread row reads fall in different banks
-constexpr size_t kFftLdsUsed = (size_t)kFftSeg * 4 + (size_t)kFftFrames * 11 * kYS * 8 + 2 * kFFT * 4;  // 81.8 KiB at 32
-// The launch requests the CU's whole LDS (160 KiB less the static tables), so no other workgroup shares the CU while
-// a block runs.  Measured (tools/conc_probe4.py / conc_probe6.py, round 6): with the 81.8 KiB it uses, a workgroup that
-// shared its CU with a co-running 128 x 128 LDS-DMA GEMM of another context (gemm_kernel, e.g. that context's
-// encoder at <= 2 windows) returned wrong spectra for a few frames of the block in 9-17 of 15-20 calls (whole frames,
-// up to 1.2 in normalised log-mel), although both kernels address only their own LDS; with the CU to itself, 0 of
-// 15.  The round-5 kernel (145 VGPRs) never shared a CU with such a GEMM; this one (88 VGPRs) could.  One workgroup
-// per CU is what either form runs anyway (81.8 KiB x 2 exceeds the CU's LDS).  16-frame blocks (WMX_LOGMEL_FRAMES=16,
-// 47 KiB, three workgroups per CU) ran 23.2 us per 4 windows sharing CUs but showed the same fault (5 of 15 calls,
-// gpurun_out/r06g), and 35.8 us alone on the CU: the 32-frame exclusive form is the default.
-constexpr size_t kFftLdsStatic = 8192;  // (bound on the kernel's static __shared__ tables: 4.1 KiB)
-size_t logmel_fft_smem_bytes() { return 160 * 1024 - kFftLdsStatic; }
-static_assert(kFftLdsUsed <= 160 * 1024 - kFftLdsStatic, "log-mel: LDS image");
+constexpr size_t kFftLdsUsed = (size_t)kFftSeg * 4 + (size_t)kFftFrames * 11 * kYS * 8 + 2 * kFFT * 4;  // 42.9 KiB at 16
+// Co-residency (round 6, tools/conc_probe4.py / conc_probe6.py): built with the compiler's SLP vectorizer, which packs
+// this kernel's f32 arithmetic into v_pk_fma/add/mul_f32, a workgroup sharing its CU with another context's MFMA GEMM
+// (gemm_kernel, with or without LDS-DMA staging) returned wrong spectra for a few frames in 4-17 of 15 calls -- the
+// frames whose (frame, n2) item group starts in the upper half of a wave -- although both kernels address only their
+// own LDS; alone on the CU, 0 of 15.  Built without it (the Makefile compiles this file with -fno-slp-vectorize: no
+// packed f32 VALU), 0 of 60 calls differ while sharing CUs, 16- and 32-frame blocks alike (gpurun_out/r06o, r06p).
+size_t logmel_fft_smem_bytes() { return kFftLdsUsed; }
 
 // min over each aligned group of kFftFrames lanes (16: one DPP row; 32: two rows joined by permlane16_swap)
 __device__ inline float block_min(float v) {

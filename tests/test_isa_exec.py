@@ -63,3 +63,30 @@ def test_no_unexpected_scratch():
                 r"gemm_packed_kernelILNS_2DTE1ELi2ELi2ELi8ELi0ELi2E", r"gemm_packed_kernelILNS_2DTE1ELi2ELi2ELi16ELi1ELi2E"):
         hits = [n for n in ks if re.search(pat, n)]
         assert hits and all(ks[n][0] == 0 for n in hits), pat
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libwmx.so not built")
+def test_logmel_has_no_packed_f32_valu():
+    """The log-mel front end is built without SLP-packed f32 arithmetic (Makefile: wmx_logmel.o with
+    -fno-slp-vectorize).  With v_pk_fma/add/mul_f32 in it, its FFT kernel returned wrong frames while sharing CUs with
+    another context's MFMA GEMM waves (4-17 of 15 concurrent calls, tools/conc_probe4.py); without them, 0 of 60
+    (DESIGN.md 0e).  A build that loses the flag fails here, on the CPU."""
+    import re
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from isa_exec_check import code_objects, disassemble
+
+    seen, packed = set(), []
+    for _triple, blob in code_objects(LIB):
+        func = None
+        for raw in disassemble(blob).splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.+)>:$", raw.strip())
+            if m:
+                func = m.group(1) if "logmel" in m.group(1) else None
+                if func:
+                    seen.add(func)
+                continue
+            if func and re.search(r"\bv_pk_(fma|add|mul)_f32\b", raw):
+                packed.append((func, raw.strip()))
+    assert any("logmel_fft_kernel" in f for f in seen), sorted(seen)
+    assert not packed, packed[:5]
