@@ -93,10 +93,11 @@ def test_logmel_batched_matches_oracle(n_mels):
 def test_logmel_seek_window():
     E = _engine()
     m = E.Model("tiny", 0, "bfloat16")
-    ctx = E.Context(m, max_batch=3, beam_size=1, word_timestamps=False, max_audio_samples=640000)
+    ctx = E.Context(m, max_batch=5, beam_size=1, word_timestamps=False, max_audio_samples=640000)
     a = synth.speech_like(5, 560000)  # 35 s: second window starts at frame 3000
-    # (seek 3000 and 1234 are not multiples of the kernel's 32-frame blocks: the block grid follows the seek)
-    got = ctx.logmel([a, a, a], seek=[0, 3000, 1234])
+    # (seek 3000 and 1234 are not multiples of the kernel's 16-frame blocks: the block grid follows the seek; 1600 is;
+    # 3490 leaves a 10-frame window, less than one block)
+    got = ctx.logmel([a, a, a, a, a], seek=[0, 3000, 1234, 1600, 3490])
     feats = O.logmel(a, 80)
     np.testing.assert_allclose(got[0], feats[:, :3000], atol=1e-4)
     ref1 = np.zeros((80, 3000), np.float32)
@@ -105,6 +106,12 @@ def test_logmel_seek_window():
     ref2 = np.zeros((80, 3000), np.float32)
     ref2[:, :2266] = feats[:, 1234:3500]
     np.testing.assert_allclose(got[2], ref2, atol=1e-4)
+    ref3 = np.zeros((80, 3000), np.float32)
+    ref3[:, :1900] = feats[:, 1600:3500]
+    np.testing.assert_allclose(got[3], ref3, atol=1e-4)
+    ref4 = np.zeros((80, 3000), np.float32)
+    ref4[:, :10] = feats[:, 3490:3500]
+    np.testing.assert_allclose(got[4], ref4, atol=1e-4)
 
 
 @pytest.fixture(scope="module")
