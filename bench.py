@@ -97,7 +97,7 @@ BENCH_ENV_KNOBS = {
     "WMX_LOCKSTEP": "0: the context groups' decode loops start independently",
     "WMX_LOCKSTEP_CHUNKS": "0: lockstep barrier at the decode start only",
     "WMX_STREAM_GROUPS": "contexts per batched stream call (stream_load line)",
-    "WMX_DEC_MIXED": "1: the mixed decode step (out / cross-out projections unsplit, LN2 / LN3 folded)",
+    "WMX_DEC_MIXED": "0: the fast decode step (three reduce_ln launches per layer) instead of the default mixed step",
     "WMX_DEC_FP8": "0: keep the fp8 model's decode on 16-bit weights",
     "WMX_ENC_FOLD": "0: encoder LayerNorms as their own launches",
     "WMX_XQ_FUSED": "0: the cross-q projection as its own split-K launch",

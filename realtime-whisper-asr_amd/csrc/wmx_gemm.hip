@@ -1616,12 +1616,12 @@ struct FoldPre {
   // through a selected pointer, which demoted the whole struct to scratch in every generic instantiation
   float4 q0, q1;
 };
-template <DT T, int MT, int NCT, int NW>
+template <DT T, int MT, int NCT, int NW, bool LNF>
 __device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const Epi& e, int M, int N, int K, int m0,
                                                      int t0) {
   constexpr int C4 = 4 * NCT;
   const int tid = threadIdx.x, wave = tid >> 6;
-  if (e.kind == EPI_LNFOLD_GELU16) {
+  if constexpr (LNF) {
 #pragma unroll
     for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j)
       row_ln_stats_load(e.stats + min(m0 + min(wave + NW * j, MT * 16 - 1), M - 1), e.stats_ld, K >> 4, P.sa[j], P.sb[j]);
@@ -1635,14 +1635,14 @@ __device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const E
     P.q1 = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
-template <DT T, int MT, int NCT, int NW>
+template <DT T, int MT, int NCT, int NW, bool LNF>
 __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT * 16][16 * NCT + 1], const Epi& e,
                                                      int M, int N, int K, int m0, int t0, const FoldPre<MT, NW>& P) {
   constexpr int NT = 64 * NW, C4 = 4 * NCT;
   const int tid = threadIdx.x, wave = tid >> 6;
   __shared__ float2 rln[MT * 16];
-  const bool fold = e.kind == EPI_LNFOLD_GELU16;
-  if (fold) {
+  constexpr bool fold = LNF;
+  if constexpr (fold) {
 #pragma unroll
     for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j) {
       const int r = wave + NW * j;
@@ -1665,7 +1665,7 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
       for (int w = 1; w < NW; ++w) v += red[w][row][c + q];
       v4[q] = v;
     }
-    if (!fold) {
+    if constexpr (!fold) {
       float* xp = reinterpret_cast<float*>(e.out) + (long)m * e.ldc + n;
       const float4 x0 = idx == tid ? P.q0 : ok ? *reinterpret_cast<const float4*>(xp) : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 b = ok && e.bias ? *reinterpret_cast<const float4*>(e.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1680,7 +1680,8 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
         *reinterpret_cast<u16x4*>(e.out16 + (long)m * e.ldc + n) = h;
         if ((n & 15) == 0) e.stats[(long)(n >> 4) * e.stats_ld + m] = make_float2(mean, m2);
       }
-    } else if (ok) {
+    } else {
+      if (!ok) continue;
       const float2 ln = rln[row];
       const float4 a = P.q0, b = P.q1;  // (prefetched: a thread's column quad is the same in every row, NT % C4 == 0)
       const u16x4 h = {from_f32<T>(gelu_erf(ln.y * (v4[0] - ln.x * a.x) + b.x)),
@@ -1695,8 +1696,10 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
 // Epilogue class, a template parameter so each launch carries only the code it runs (these launches are a few
 // microseconds long and start on a cold instruction cache: a generic epilogue switch in a split-K launch measured
 // +0.6 us per launch): kPackedPart split-K raw partials (S > 1); kPackedGelu S == 1 bias + GELU -> 16-bit
-// (decode fc1; bias loaded beside the first k-steps); kPackedGeneric every other S == 1 epilogue
-enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2 };
+// (decode fc1; bias loaded beside the first k-steps); kPackedResidStats / kPackedLnfGelu the mixed step's folded
+// LayerNorm producer / consumer (round 6: their own instantiations, no longer branches of the generic one);
+// kPackedGeneric every other S == 1 epilogue
+enum { kPackedPart = 0, kPackedGelu = 1, kPackedGeneric = 2, kPackedResidStats = 3, kPackedLnfGelu = 4 };
 
 // W8: the weights are e4m3 bytes in the packed8_index layout with per-row scales wsc (a k-step is 64 deep: the
 // same 16-byte lane load as a bf16 k-step, widened in registers into the B fragments of two MFMAs; the row scale
@@ -1732,11 +1735,9 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   float4 wsc4 = make_float4(1.f, 1.f, 1.f, 1.f);
   if constexpr (W8) wsc4 = *reinterpret_cast<const float4*>(wsc + min(t0 * 16 + (tid % (4 * NCT)) * 4, ntiles * 16 - 4));
   // the folded-LayerNorm epilogues (S == 1): their statistics / residual loads ride ahead of the main loop
+  constexpr bool fold_epi = (EPK == kPackedResidStats || EPK == kPackedLnfGelu) && !W8;  // (S == 1: host-checked)
   FoldPre<MT, NW> fpre;
-  const bool fold_epi = EPK == kPackedGeneric && !W8 && S == 1 &&
-                        (e.kind == EPI_RESID_STATS || e.kind == EPI_LNFOLD_GELU16);
-  if constexpr (EPK == kPackedGeneric && !W8)
-    if (fold_epi) packed_fold_prefetch<T, MT, NCT, NW>(fpre, e, M, N, K, m0, t0);
+  if constexpr (fold_epi) packed_fold_prefetch<T, MT, NCT, NW, EPK == kPackedLnfGelu>(fpre, e, M, N, K, m0, t0);
   f32x4 acc[MT][NCT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -1814,9 +1815,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
   __syncthreads();
   // 4 consecutive columns per thread
   constexpr int C4 = 4 * NCT;  // column quads per row
-  if constexpr (EPK == kPackedGeneric && !W8) {  // (the folded step has no 8-bit form: host-checked)
-    if (fold_epi) packed_fold_epilogue<T, MT, NCT, NW>(red, e, M, N, K, m0, t0, fpre);
-  }
+  if constexpr (fold_epi)  // (the folded step has no 8-bit form: host-checked)
+    packed_fold_epilogue<T, MT, NCT, NW, EPK == kPackedLnfGelu>(red, e, M, N, K, m0, t0, fpre);
   for (int idx = tid; !fold_epi && idx < MT * 16 * C4; idx += NT) {
     const int row = idx / C4, c = (idx - row * C4) * 4;
     const int m = m0 + row, n = t0 * 16 + c;
@@ -1918,7 +1918,9 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
   const int nw = packed_nw<MT, NCT>(g.K, g.S, (long)grid.x * grid.y * grid.z, W8 != 0);
   const int epk = g.S > 1 ? kPackedPart
                  : (g.epi.kind == EPI_GELU16 && g.epi.bias && g.N % 4 == 0 && g.epi.ldc % 4 == 0) ? kPackedGelu
-                                                                                                 : kPackedGeneric;
+                 : g.epi.kind == EPI_RESID_STATS ? kPackedResidStats
+                 : g.epi.kind == EPI_LNFOLD_GELU16 ? kPackedLnfGelu
+                                                   : kPackedGeneric;
 #define WMX_PACKED_EPK(NWV, EPKV)                                                                                  \
   hipLaunchKernelGGL((gemm_packed_kernel<T, MT, NCT, NWV, EPKV, W8>), grid, dim3(64 * NWV), 0, st, g.A, g.lda, g.W,  \
                      g.M, g.N, g.K, g.S, g.epi, g.part, g.tprobe, g.pslot, g.wscale)
@@ -1927,6 +1929,12 @@ static void launch_packed_cfg(const PackedCall& g, hipStream_t st) {
     switch (epk) {                                                                                                 \
       case kPackedPart: WMX_PACKED_EPK(NWV, kPackedPart); break;                                                   \
       case kPackedGelu: WMX_PACKED_EPK(NWV, kPackedGelu); break;                                                   \
+      case kPackedResidStats:                                                                                      \
+        if constexpr (W8 == 0) WMX_PACKED_EPK(NWV, kPackedResidStats);                                             \
+        break;                                                                                                     \
+      case kPackedLnfGelu:                                                                                         \
+        if constexpr (W8 == 0) WMX_PACKED_EPK(NWV, kPackedLnfGelu);                                                \
+        break;                                                                                                     \
       default: WMX_PACKED_EPK(NWV, kPackedGeneric); break;                                                         \
     }                                                                                                              \
   } while (0)
