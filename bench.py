@@ -587,6 +587,16 @@ def main():
     roof["replayed_us"] = {k: round(1000 * replay[k][0], 2) for k in fams[dom]}
     # every probed launch of the layer, end to end (the whole layer-step chain of one group, in launch order)
     roof["layer_e2e_us"] = {k: round(1000 * v[0], 2) for k, v in evs.items() if v[1] and k != "prev_layer_last"}
+    # the decode step form (wmx_runtime.hip): "mixed" (default for 16-bit models since round 6: the out / cross-out
+    # projections unsplit with the residual add and row statistics in their epilogue, one reduce_ln per layer) or
+    # "fast" (three reduce_ln launches per layer).  The mixed step moves the residual + LayerNorm work of two
+    # reduce_ln launches INTO two of the family's launches, so `frac` (family bytes / family time) is not comparable
+    # across the forms; frac_projection_chain divides the same bytes by the family's time plus every reduce_ln launch
+    # of the layer, which is.  (replayed_us / frac_isolated_replay / traffic are of the split-K launch forms.)
+    red_keys = [k for k in ("reduce_ln_out", "reduce_ln_cross_out", "reduce_ln_fc2") if evs.get(k, (0, 0))[1]]
+    roof["decode_step"] = "fast" if "reduce_ln_out" in red_keys else "mixed"
+    chain_ms = ms_e2e + sum(evs[k][0] for k in red_keys)
+    roof["frac_projection_chain"] = round(by / (chain_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if chain_ms > 0 else None
     roof["layer_span_us"] = {k: round(1000 * v[0], 2) for k, v in insitu.items() if v[1] and k != "prev_layer_last"}
     span = sum(insitu[k][0] for k in fams[dom])
     roof["wg_span"] = {"what": f"device-clock span first workgroup start .. last workgroup end, layer {probe_layer}, "

@@ -41,7 +41,7 @@ int wmx_ctx_last_steps(wmx_ctx* c);
  * 1 encoder fc1 GEMM, 2 encoder self-attention (one layer), 3 log-mel (raw pass), 4 decoder fc1 GEMM (step),
  * 5 decoder self-attention (one layer, at the last decoded length), 6 the whole encoder over B windows,
  * 7 / 8 / 9 decoder qkv / d x d / fc2 projection (split-K partial launch of a step), 10 reduce_ln of a d x d
- * projection's partials (residual add + LayerNorm). */
+ * projection's partials (residual add + LayerNorm), 11 decoder fc1 of the mixed step (LayerNorm folded). */
 wmx_status wmx_ctx_bench_kernel(wmx_ctx* c, int kernel, int B, int iters, float* avg_ms, double* bytes,
                                 double* flops);
 

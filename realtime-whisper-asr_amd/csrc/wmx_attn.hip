@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void dec_self_attn_kernel(DecAttnArgs a) {
     }
     if (a.ln_c1) {  // LN1 folded into the QKV weights: this row's statistics, merged by the fourth wave
       if (wave == 3) {
-        const float2 st = row_ln_from_stats(a.ln_stats + m, a.ln_ld, a.d >> 4);
+        const float2 st = row_ln_from_stats(a.ln_stats + (long)m * a.ln_ld, 1, a.d >> 4);
         if (lane == 0) lnrow = st;
       }
       __syncthreads();
@@ -801,7 +801,8 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   if (fold_q) {  // rows wave and wave + 8 of the tile (clamped: rows past nqt are never used), merged after the MFMAs
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      row_ln_stats_load(a.ln_stats + (long)w * nq + i0 + min(wave + 8 * j, nqt - 1), a.ln_ld, a.d >> 4, lnA[j], lnB[j]);
+      row_ln_stats_load(a.ln_stats + ((long)w * nq + i0 + min(wave + 8 * j, nqt - 1)) * a.ln_ld, 1, a.d >> 4, lnA[j],
+                        lnB[j]);
   }
   __builtin_amdgcn_sched_barrier(0);  // keep the K batch in flight under the projection (the scheduler sinks it)
   if (fuse_q) {
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     __syncthreads();
   } else if (a.qS > 0 && a.ln_c1) {  // LN2 folded into the cross-q weights: the tile's row statistics, one wave per row
     for (int q = wave; q < nqt; q += NWV) {
-      const float2 st = row_ln_from_stats(a.ln_stats + (long)w * nq + i0 + q, a.ln_ld, a.d >> 4);
+      const float2 st = row_ln_from_stats(a.ln_stats + ((long)w * nq + i0 + q) * a.ln_ld, 1, a.d >> 4);
       if (lane == 0) qln[q] = st;
     }
     __syncthreads();
@@ -1154,7 +1155,7 @@ void launch_cross_attn(DT dt, const DecAttnArgs& a, float* ws, hipStream_t st) {
   const bool f8 = a.ck_scale != nullptr;
   WMX_CHECK(!f8 || (a.cv_scale && (!a.wq || a.wq_scale)), "cross attn: fp8 images need their scales (and 8-bit query weights)");
   WMX_CHECK(f8 || !a.wq_scale, "cross attn: 8-bit query weights run with the fp8 images only");
-  WMX_CHECK(!(a.wq && a.ln_c1) || (!a.wq_scale && a.ln_c2 && a.ln_stats && a.d / 16 <= 128 && a.qS == 0),
+  WMX_CHECK(!(a.wq && a.ln_c1) || (!a.wq_scale && a.ln_c2 && a.ln_stats && a.d / 16 <= 128 && a.ln_ld >= a.d / 16 && a.qS == 0),
             "cross attn: the LayerNorm-folded fused query projection is 16-bit only");
   if (dt == DT::BF16) {
     if (f8) launch_cross_t<DT::BF16, true>(a, ws, st);

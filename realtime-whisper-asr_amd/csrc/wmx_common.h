@@ -220,12 +220,15 @@ __device__ inline void row_ln_stats_load(const float2* __restrict__ st, long ld,
   a = lane < G ? st[lane * ld] : make_float2(0.f, 0.f);
   b = lane + 64 < G ? st[(lane + 64) * ld] : make_float2(0.f, 0.f);
 }
+// (hardware reciprocal and reciprocal square root, not the IEEE division and sqrt expansions: with four waves per
+// SIMD each merging two rows, those expansions were ~2 us of every LayerNorm-folded decode launch, round 6)
 __device__ inline float2 row_ln_stats_merge(float2 a, float2 b, int G) {
   const int lane = threadIdx.x & 63;
-  const float mean = wave_sum(a.x + b.x) / G;
+  const float invG = __builtin_amdgcn_rcpf((float)G);
+  const float mean = wave_sum(a.x + b.x) * invG;
   const float da = lane < G ? a.x - mean : 0.f, db = lane + 64 < G ? b.x - mean : 0.f;
   const float m2 = wave_sum((a.y + b.y) + 16.f * (da * da + db * db));
-  return make_float2(mean, 1.0f / sqrtf(m2 / (16.f * G) + 1e-5f));
+  return make_float2(mean, __builtin_amdgcn_rsqf(m2 * (0.0625f * invG) + 1e-5f));
 }
 __device__ inline float2 row_ln_from_stats(const float2* __restrict__ st, long ld, int G) {
   float2 a, b;

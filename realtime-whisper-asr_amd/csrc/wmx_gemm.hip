@@ -1624,7 +1624,8 @@ __device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const E
   if constexpr (LNF) {
 #pragma unroll
     for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j)
-      row_ln_stats_load(e.stats + min(m0 + min(wave + NW * j, MT * 16 - 1), M - 1), e.stats_ld, K >> 4, P.sa[j], P.sb[j]);
+      row_ln_stats_load(e.stats + (long)min(m0 + min(wave + NW * j, MT * 16 - 1), M - 1) * e.stats_ld, 1, K >> 4, P.sa[j],
+                         P.sb[j]);
     const int n = min(t0 * 16 + (tid % C4) * 4, N - 4);
     P.q0 = *reinterpret_cast<const float4*>(e.c1 + n);
     P.q1 = *reinterpret_cast<const float4*>(e.c2 + n);
@@ -1678,7 +1679,7 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
         *reinterpret_cast<float4*>(xp) = x;
         const u16x4 h = {from_f32<T>(x.x), from_f32<T>(x.y), from_f32<T>(x.z), from_f32<T>(x.w)};
         *reinterpret_cast<u16x4*>(e.out16 + (long)m * e.ldc + n) = h;
-        if ((n & 15) == 0) e.stats[(long)(n >> 4) * e.stats_ld + m] = make_float2(mean, m2);
+        if ((n & 15) == 0) e.stats[(long)m * e.stats_ld + (n >> 4)] = make_float2(mean, m2);  // [R][d / 16]
       }
     } else {
       if (!ok) continue;
@@ -2039,8 +2040,9 @@ void launch_gemm_packed(DT dt, const PackedCall& g, hipStream_t st) {
   WMX_CHECK(g.nct == 0 || g.nct == 1 || g.nct == 2 || g.nct == 4, "packed gemm: column tiles per workgroup");
   WMX_CHECK((g.epi.kind != EPI_RESID_STATS && g.epi.kind != EPI_LNFOLD_GELU16) ||
                 (g.S == 1 && g.N % 16 == 0 && g.epi.stats && g.epi.ldc % 4 == 0 &&
-                 (g.epi.kind == EPI_LNFOLD_GELU16 ? (g.epi.c1 && g.epi.c2 && g.K % 16 == 0 && g.K <= 2048)
-                                                  : (g.epi.out16 != nullptr && g.N <= 2048))),
+                 (g.epi.kind == EPI_LNFOLD_GELU16
+                      ? (g.epi.c1 && g.epi.c2 && g.K % 16 == 0 && g.K <= 2048 && g.epi.stats_ld >= g.K / 16)
+                      : (g.epi.out16 != nullptr && g.N <= 2048 && g.epi.stats_ld >= g.N / 16))),
             "packed gemm: folded-LayerNorm epilogue arguments");
   const bool w8 = g.wscale != nullptr;
   WMX_CHECK(!w8 || (g.K % 64 == 0 && g.epi.kind != EPI_RESID_STATS && g.epi.kind != EPI_LNFOLD_GELU16),

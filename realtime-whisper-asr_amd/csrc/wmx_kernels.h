@@ -42,7 +42,8 @@ struct Epi {
   // EPI_GELU_MX8: the block scales (one byte per 32 columns, ldc2 bytes per row)
   uint8_t* out2 = nullptr;
   long ldc2 = 0;
-  // EPI_RESID_STATS / EPI_LNFOLD_GELU16: row statistics [d / 16][stats_ld]; the 16-bit copy of x; folded constants
+  // EPI_RESID_STATS / EPI_LNFOLD_GELU16: row statistics [rows][stats_ld >= d / 16] (a row's 16-column groups contiguous,
+  // so a consumer wave reads a row's statistics in a few lines); the 16-bit copy of x; folded constants
   float2* stats = nullptr;
   long stats_ld = 0;
   uint16_t* out16 = nullptr;
@@ -324,7 +325,7 @@ struct DecAttnArgs {
   // rstd_row (sum_s qpart - mean_row ln_c1[col]) + ln_c2[col] instead of qbias + sum_s qpart
   const float* ln_c1 = nullptr;
   const float* ln_c2 = nullptr;
-  const float2* ln_stats = nullptr;  // [d / 16][ln_ld]
+  const float2* ln_stats = nullptr;  // [rows][ln_ld >= d / 16]
   long ln_ld = 0;
   // cross attention with the query projection fused (decode, wq != null): the workgroup computes its window-rows'
   // queries of head h itself, q = qin[row] . wq[64 h .. 64 h + 63]^T + qbias, on MFMA with K split over its waves

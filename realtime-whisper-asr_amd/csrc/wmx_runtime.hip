@@ -692,7 +692,7 @@ struct Ctx {
   long ws_elems = 0;
   float* part = nullptr;  // split-K partials of the packed decode GEMMs [S][rows][N]
   float2* est = nullptr;    // encoder fold: per-256-column (mean, M2) of the residual rows [da / 256][maxB * 1500]
-  float2* rstat = nullptr;  // LayerNorm-folded step: per-16-column (mean, M2) of the residual rows [dt / 16][R]
+  float2* rstat = nullptr;  // LayerNorm-folded step: per-16-column (mean, M2) of the residual rows [R][dt / 16]
   long part_elems = 0;
   int *hist = nullptr, *hist_tmp = nullptr, *anc = nullptr, *anc_tmp = nullptr, *pad_row = nullptr, *pad_win = nullptr;
   int *slot = nullptr, *n_done = nullptr, *lang_slot = nullptr, *lang_tok = nullptr, *row_map = nullptr, *gather = nullptr;
@@ -1364,7 +1364,7 @@ static Epi epi_resid_stats(Ctx& c, const float* bias, int R) {
   Epi e = epi(EPI_RESID_STATS, bias, c.dx, c.m->d.n_text_state);
   e.out16 = c.dhb;
   e.stats = c.rstat;
-  e.stats_ld = R;
+  e.stats_ld = c.m->d.n_text_state / 16;  // row stride of [R][dt / 16]
   return e;
 }
 
@@ -1463,7 +1463,7 @@ static void dec_step_mixed(Ctx& c, const FwdArgs& f) {
     x.ln_c1 = L.c1cq;
     x.ln_c2 = L.c2cq;
     x.ln_stats = c.rstat;
-    x.ln_ld = R;
+    x.ln_ld = dt / 16;
     x.xcnt = c.xa_cnt;
     x.slot0 = c.slot;
     if (probed) x.tprobe = c.probe_buf + kProbeCross * probe_stride;
@@ -1477,7 +1477,7 @@ static void dec_step_mixed(Ctx& c, const FwdArgs& f) {
     e1.c1 = L.c1fc1;
     e1.c2 = L.c2fc1;
     e1.stats = c.rstat;
-    e1.stats_ld = R;
+    e1.stats_ld = dt / 16;
     gemm_p(c, c.dhb, dt, L.ffc1, R, 4 * dt, dt, e1);
     probe(kProbeFc2);
     gemm_p_redln(c, c.df1, 4 * dt, L.wfc2, R, dt, 4 * dt, L.bfc2, last ? m.lng : m.dec[l + 1].ln1g,
@@ -3376,6 +3376,19 @@ wmx_status wmx_ctx_bench_kernel(wmx_ctx* x, int kernel, int B, int iters, float*
       by = (double)R * (s + 1) * dt * 2 * 2;
       fl = 4.0 * R * (s + 1) * dt;
       fn = [&c, a] { launch_self_attn(c.dt, a, c.st); };
+    } else if (kernel == 11) {
+      // decoder fc1 of the mixed step: LN3 folded into the weights, the row statistics merged in the epilogue
+      WMX_CHECK(m.mixed, "bench_kernel: the LayerNorm-folded fc1 exists on mixed-step models only");
+      by = 4.0 * dt * dt * 2 + (double)R * dt * 2 + (double)R * 4 * dt * 2;
+      fl = 2.0 * R * 4 * dt * dt;
+      fn = [&c, &m, R, dt] {
+        Epi e1 = epi(EPI_LNFOLD_GELU16, nullptr, c.df1, 4 * dt);
+        e1.c1 = m.dec[0].c1fc1;
+        e1.c2 = m.dec[0].c2fc1;
+        e1.stats = c.rstat;
+        e1.stats_ld = dt / 16;
+        gemm_p(c, c.dhb, dt, m.dec[0].ffc1, R, 4 * dt, dt, e1);
+      };
     } else if (kernel == 6) {
       // the whole encoder (conv front end + every layer + final LN) over B windows: its MFMA work per window
       const double T = 1500, M = m.d.n_mels, Ha = m.d.n_audio_head, La = m.d.n_audio_layer;

@@ -361,7 +361,7 @@ class Context:
         return int(lib.wmx_ctx_last_steps(self._h))
 
     KERNELS = {"cross_attn": 0, "enc_fc1": 1, "enc_attn": 2, "logmel": 3, "dec_fc1": 4, "self_attn": 5, "encoder": 6,
-               "dec_qkv": 7, "dec_proj": 8, "dec_fc2": 9, "reduce_ln": 10}
+               "dec_qkv": 7, "dec_proj": 8, "dec_fc2": 9, "reduce_ln": 10, "dec_fc1_lnf": 11}
 
     PROBE_LAUNCHES = ("dec_qkv", "dec_out", "dec_cross_q", "dec_cross_out", "dec_fc1", "dec_fc2", "cross_attn",
                       "self_attn", "reduce_ln_out", "reduce_ln_cross_out", "reduce_ln_fc2", "prev_layer_last")

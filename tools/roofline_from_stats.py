@@ -28,12 +28,20 @@ def main(stats, line, n_layers=32):
             per.append((r["Name"].split(">(")[0] + ">", round(k), float(r["AverageNs"]) / 1000.0, int(r["Calls"])))
     us = sum(n * a for _, n, a, _ in per)
     ach = by / (us * 1e-6) / 1e9
+    # the projection chain (comparable across the fast and mixed decode steps: the mixed step folds two reduce_ln
+    # launches' work into two of the family's launches): the family plus the layer-step's reduce_ln4 launches
+    red = [r for r in rows if "reduce_ln4_kernel" in r["Name"]]
+    red_us = sum(round(int(r["Calls"]) / max(1, n_layers * steps * groups)) * float(r["AverageNs"]) / 1000.0
+                 for r in red if int(r["Calls"]) / max(1, n_layers * steps * groups) >= 0.5)
     out = {"kernel_stats": stats, "bench_line": line, "algorithmic_bytes_per_layer_step": by,
            "instantiations": [{"name": nm, "per_layer_step": n, "avg_us": round(a, 3), "calls": c}
                               for nm, n, a, c in per],
            "layer_step_us": round(us, 3), "achieved_gbs": round(ach, 1), "frac": round(ach / 8000.0, 4),
            "line_frac": roof["frac"], "line_basis": roof.get("frac_basis"),
-           "agreement": round(roof["frac"] / (ach / 8000.0), 4) if us > 0 else None}
+           "agreement": round(roof["frac"] / (ach / 8000.0), 4) if us > 0 else None,
+           "reduce_ln_us_per_layer_step": round(red_us, 3),
+           "frac_projection_chain": round(by / ((us + red_us) * 1e-6) / 1e9 / 8000.0, 4) if us + red_us > 0 else None,
+           "line_frac_projection_chain": roof.get("frac_projection_chain")}
     print(json.dumps(out, indent=1))
 
 
