@@ -771,7 +771,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   constexpr bool fold_q = fuse_q && FQ;  // (launcher: FQ iff a.ln_c1 with a.wq)
   const float qc1_col = fold_q ? a.ln_c1[h * 64 + (tid & 63)] : 0.f;
   const float qc2_col = fold_q ? a.ln_c2[h * 64 + (tid & 63)] : 0.f;
-  float2 lnA[2], lnB[2];
+  float2 lns[4];  // rows wave (lanes 0..31) and wave + 8 (lanes 32..63) of the tile: their statistics groups
   if (fuse_q) {
     const uint16_t* ap = a.qin + (row0 + min(fr, trows - 1)) * a.qin_ld + 8 * g;
     const uint16_t* wp = a.wq + (((long)h * 4 * qksteps) << 9) + lane * 8;  // (F8: the same 16-byte lane pieces)
@@ -798,12 +798,9 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     load_k(kw0);
   else if (kw0 < kw1)
     load_batch(kw0);
-  if (fold_q) {  // rows wave and wave + 8 of the tile (clamped: rows past nqt are never used), merged after the MFMAs
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      row_ln_stats_load(a.ln_stats + ((long)w * nq + i0 + min(wave + 8 * j, nqt - 1)) * a.ln_ld, 1, a.d >> 4, lnA[j],
-                        lnB[j]);
-  }
+  if (fold_q)  // rows wave and wave + 8 of the tile (clamped: rows past nqt are never used), merged after the MFMAs
+    row_ln_stats_load2(a.ln_stats + ((long)w * nq + i0 + min(wave, nqt - 1)) * a.ln_ld,
+                       a.ln_stats + ((long)w * nq + i0 + min(wave + 8, nqt - 1)) * a.ln_ld, a.d >> 4, lns);
   __builtin_amdgcn_sched_barrier(0);  // keep the K batch in flight under the projection (the scheduler sinks it)
   if (fuse_q) {
     f32x4 qa[4];
@@ -844,12 +841,10 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   const float kQScale = 0.125f * 1.4426950408889634f * ksc;
   __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
   __shared__ float2 qln[16];
-  if (fold_q) {  // the statistics loaded beside the K batch, merged now (wave-uniform rows)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float2 st = row_ln_stats_merge(lnA[j], lnB[j], a.d >> 4);
-      if (lane == 0 && wave + 8 * j < nqt) qln[wave + 8 * j] = st;
-    }
+  if (fold_q) {  // the statistics loaded beside the K batch, merged now (one row per half-wave)
+    const float2 st = row_ln_stats_merge2(lns, a.d >> 4);
+    const int rq = wave + 8 * (lane >> 5);
+    if ((lane & 31) == 0 && rq < nqt) qln[rq] = st;
     __syncthreads();
   } else if (a.qS > 0 && a.ln_c1) {  // LN2 folded into the cross-q weights: the tile's row statistics, one wave per row
     for (int q = wave; q < nqt; q += NWV) {

@@ -230,6 +230,35 @@ __device__ inline float2 row_ln_stats_merge(float2 a, float2 b, int G) {
   const float m2 = wave_sum((a.y + b.y) + 16.f * (da * da + db * db));
   return make_float2(mean, __builtin_amdgcn_rsqf(m2 * (0.0625f * invG) + 1e-5f));
 }
+// sum over each aligned half-wave (32 lanes)
+__device__ inline float half_sum32(float v) {
+  v = sum8_lanes(v);
+  v += dpp_mov<kDppMirror>(v);
+  return sum_xor16(v);
+}
+// two rows at once, one per half-wave (lanes 0..31 row A, 32..63 row B): the row's G <= 128 groups of a row-major
+// [row][G] statistics image, four per lane (group (lane & 31) + 32 q); then each half's (mean, rstd).  Half the
+// reduction chains of merging the rows one after the other with the whole wave.
+__device__ inline void row_ln_stats_load2(const float2* __restrict__ ra, const float2* __restrict__ rb, int G,
+                                          float2 (&s)[4]) {
+  const int lane = threadIdx.x & 63, i = lane & 31;
+  const float2* st = lane < 32 ? ra : rb;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s[q] = i + 32 * q < G ? st[i + 32 * q] : make_float2(0.f, 0.f);
+}
+__device__ inline float2 row_ln_stats_merge2(const float2 (&s)[4], int G) {
+  const int i = threadIdx.x & 31;
+  const float invG = __builtin_amdgcn_rcpf((float)G);
+  const float mean = half_sum32((s[0].x + s[1].x) + (s[2].x + s[3].x)) * invG;
+  float dev = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float d = i + 32 * q < G ? s[q].x - mean : 0.f;
+    dev += s[q].y + 16.f * d * d;
+  }
+  const float m2 = half_sum32(dev);
+  return make_float2(mean, __builtin_amdgcn_rsqf(m2 * (0.0625f * invG) + 1e-5f));
+}
 __device__ inline float2 row_ln_from_stats(const float2* __restrict__ st, long ld, int G) {
   float2 a, b;
   row_ln_stats_load(st, ld, G, a, b);

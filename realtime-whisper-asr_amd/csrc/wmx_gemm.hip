@@ -1609,7 +1609,8 @@ constexpr int packed_ku8() {
 template <int MT, int NW>
 struct FoldPre {
   static constexpr int RPW = (MT * 16 + NW - 1) / NW;  // statistics rows per wave (rows wave + NW j)
-  float2 sa[RPW], sb[RPW];
+  static constexpr int RPH = (RPW + 1) / 2;              // row pairs: rows wave + NW 2p (lanes 0..31), + NW (2p + 1)
+  float2 s[RPH][4];
   // EPI_RESID_STATS: q0 = the residual quad of this thread's first epilogue item (idx = tid); EPI_LNFOLD_GELU16:
   // q0 / q1 = the folded constants c1 / c2 of the thread's column quad (the same in every row).  One slot for both
   // kinds, each assigned whole: two members loaded on either side of a branch were merged into one load stored
@@ -1623,9 +1624,11 @@ __device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const E
   const int tid = threadIdx.x, wave = tid >> 6;
   if constexpr (LNF) {
 #pragma unroll
-    for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j)
-      row_ln_stats_load(e.stats + (long)min(m0 + min(wave + NW * j, MT * 16 - 1), M - 1) * e.stats_ld, 1, K >> 4, P.sa[j],
-                         P.sb[j]);
+    for (int p = 0; p < FoldPre<MT, NW>::RPH; ++p) {
+      const long ra = min(m0 + min(wave + NW * 2 * p, MT * 16 - 1), M - 1);
+      const long rb = min(m0 + min(wave + NW * (2 * p + 1), MT * 16 - 1), M - 1);
+      row_ln_stats_load2(e.stats + ra * e.stats_ld, e.stats + rb * e.stats_ld, K >> 4, P.s[p]);
+    }
     const int n = min(t0 * 16 + (tid % C4) * 4, N - 4);
     P.q0 = *reinterpret_cast<const float4*>(e.c1 + n);
     P.q1 = *reinterpret_cast<const float4*>(e.c2 + n);
@@ -1645,12 +1648,10 @@ __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT *
   constexpr bool fold = LNF;
   if constexpr (fold) {
 #pragma unroll
-    for (int j = 0; j < FoldPre<MT, NW>::RPW; ++j) {
-      const int r = wave + NW * j;
-      if (r < MT * 16) {  // (wave-uniform)
-        const float2 st = row_ln_stats_merge(P.sa[j], P.sb[j], K >> 4);
-        if ((tid & 63) == 0) rln[r] = st;
-      }
+    for (int p = 0; p < FoldPre<MT, NW>::RPH; ++p) {
+      const int r = wave + NW * (2 * p + ((tid & 63) >> 5));  // this half-wave's row
+      const float2 st = row_ln_stats_merge2(P.s[p], K >> 4);
+      if ((tid & 31) == 0 && r < MT * 16) rln[r] = st;
     }
     __syncthreads();
   }
