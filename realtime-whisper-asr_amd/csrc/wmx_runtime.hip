@@ -2303,7 +2303,7 @@ wmx_status wmx_model_create(const wmx_dims* dims, int device, int dtype, wmx_mod
       w->m.i8 = dtype == WMX_DTYPE_I8 || dtype == WMX_DTYPE_I8_BF16;
       if (w->m.i8) w->m.w8 = true;
       {  // the mixed decode step, the default for 16-bit models since round 6 (two reduce_ln launches per layer fewer:
-         // 419.6-420.5x against the fast step's 416.8x, gpurun_out/r06t); WMX_DEC_MIXED=0 selects the fast step
+         // 439.4-440.4x against the fast step's 416.2-416.8x); WMX_DEC_MIXED=0 selects the fast step
         const char* dm = getenv("WMX_DEC_MIXED");
         w->m.mixed = !w->m.w8 && !(dm && dm[0] == '0');
       }
