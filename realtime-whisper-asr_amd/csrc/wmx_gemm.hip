@@ -1639,22 +1639,32 @@ __device__ __forceinline__ void packed_fold_prefetch(FoldPre<MT, NW>& P, const E
     P.q1 = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
+// the LayerNorm-folded consumer's merged (mean, rstd) of its rows, in LDS
+template <int MT>
+__device__ __forceinline__ float2* fold_rln() {
+  __shared__ float2 r[MT * 16];
+  return r;
+}
+// merged while the wave's first weight batch is in flight (the statistics loads were issued before it), so the
+// epilogue needs no merge and no barrier of its own: the reduction barrier orders these LDS writes before its reads
+template <int MT, int NW>
+__device__ __forceinline__ void packed_fold_merge(const FoldPre<MT, NW>& P, int K) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  float2* rln = fold_rln<MT>();
+#pragma unroll
+  for (int p = 0; p < FoldPre<MT, NW>::RPH; ++p) {
+    const int r = wave + NW * (2 * p + ((tid & 63) >> 5));  // this half-wave's row
+    const float2 st = row_ln_stats_merge2(P.s[p], K >> 4);
+    if ((tid & 31) == 0 && r < MT * 16) rln[r] = st;
+  }
+}
 template <DT T, int MT, int NCT, int NW, bool LNF>
 __device__ __forceinline__ void packed_fold_epilogue(const float (&red)[NW][MT * 16][16 * NCT + 1], const Epi& e,
                                                      int M, int N, int K, int m0, int t0, const FoldPre<MT, NW>& P) {
   constexpr int NT = 64 * NW, C4 = 4 * NCT;
   const int tid = threadIdx.x, wave = tid >> 6;
-  __shared__ float2 rln[MT * 16];
   constexpr bool fold = LNF;
-  if constexpr (fold) {
-#pragma unroll
-    for (int p = 0; p < FoldPre<MT, NW>::RPH; ++p) {
-      const int r = wave + NW * (2 * p + ((tid & 63) >> 5));  // this half-wave's row
-      const float2 st = row_ln_stats_merge2(P.s[p], K >> 4);
-      if ((tid & 31) == 0 && r < MT * 16) rln[r] = st;
-    }
-    __syncthreads();
-  }
+  const float2* rln = fold ? fold_rln<MT>() : nullptr;  // (merged by packed_fold_merge before the reduction barrier)
   for (int idx = tid; idx < MT * 16 * C4; idx += NT) {
     const int row = idx / C4, c = (idx - row * C4) * 4;
     const int m = m0 + row, n = t0 * 16 + c;
@@ -1786,6 +1796,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
           }
     }
   }
+  bool merged = false;  // (LNF: wave-uniform)
   for (int kk = ks0; !W8 && kk < ks1; kk += KU) {
     u16x8 b[KU][NCT], av[KU][MT];
 #pragma unroll
@@ -1800,6 +1811,12 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
     // load behind an MFMA and wait for it with vmcnt(0), two round trips per batch instead of one (measured +1 us
     // per split-K launch in one instantiation)
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (EPK == kPackedLnfGelu && !W8) {
+      if (!merged) {
+        packed_fold_merge<MT, NW>(fpre, K);
+        merged = true;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < KU; ++u)
       if (kk + u < ks1)
@@ -1808,6 +1825,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_packed_kernel(const uint16_t* __
 #pragma unroll
           for (int j = 0; j < NCT; ++j) acc[i][j] = mfma16<T>(av[u][i], b[u][j], acc[i][j]);
   }
+  if constexpr (EPK == kPackedLnfGelu && !W8)
+    if (!merged) packed_fold_merge<MT, NW>(fpre, K);  // (a wave without k-steps)
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
