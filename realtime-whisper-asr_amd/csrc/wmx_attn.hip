@@ -751,6 +751,7 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   };
   // per-wave fp32 tiles: the fused query projection's K-slice partials here, the softmax combine at the end
   __shared__ float so[NWV][16][65];
+  __shared__ float2 qln[16];  // the tile's rows' LayerNorm (mean, rstd) of the folded query projection
   // ---- fused cross-q projection (a.wq): the wave's share of the K steps of the 16 x 64 tile q = qin . wq_h^T,
   //      one MFMA fragment per (k-step, 16-column block) from the packed layout (packed_w_elem / packed_a_elem);
   //      all of the wave's query-projection loads are issued BEFORE the first K / V batch, so its MFMAs wait only
@@ -794,13 +795,15 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   // (fused path: unconditional -- a wave without keys reads past the image, zeros by the descriptor's range, and
   // never uses them; a conditional batch would make the compiler's waits for the projection's loads count as if
   // the K loads had not been issued, i.e. wait for them too)
+  // (fold: the row statistics before the K batch, so the merge after the projection MFMAs waits for them and not
+  // for the K batch)
+  if (fold_q)  // rows wave and wave + 8 of the tile (clamped: rows past nqt are never used), merged after the MFMAs
+    row_ln_stats_load2(a.ln_stats + ((long)w * nq + i0 + min(wave, nqt - 1)) * a.ln_ld,
+                       a.ln_stats + ((long)w * nq + i0 + min(wave + 8, nqt - 1)) * a.ln_ld, a.d >> 4, lns);
   if (fuse_q)
     load_k(kw0);
   else if (kw0 < kw1)
     load_batch(kw0);
-  if (fold_q)  // rows wave and wave + 8 of the tile (clamped: rows past nqt are never used), merged after the MFMAs
-    row_ln_stats_load2(a.ln_stats + ((long)w * nq + i0 + min(wave, nqt - 1)) * a.ln_ld,
-                       a.ln_stats + ((long)w * nq + i0 + min(wave + 8, nqt - 1)) * a.ln_ld, a.d >> 4, lns);
   __builtin_amdgcn_sched_barrier(0);  // keep the K batch in flight under the projection (the scheduler sinks it)
   if (fuse_q) {
     f32x4 qa[4];
@@ -830,6 +833,11 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) so[wave][4 * g + r][16 * j + fr] = qa[j][r];
+    if (fold_q) {  // one row per half-wave; ordered before the q build by the barrier below
+      const float2 st = row_ln_stats_merge2(lns, a.d >> 4);
+      const int rq = wave + 8 * (lane >> 5);
+      if ((lane & 31) == 0 && rq < nqt) qln[rq] = st;
+    }
     load_v(kw0);
     __syncthreads();
   }
@@ -840,12 +848,8 @@ __global__ __launch_bounds__(64 * NWV, KPW <= 2 ? WMX_XATTN_OCC : 1) void dec_cr
   // (F8: times the K image's power-of-two scale, so S = K8 . q' = K . q exactly as with the dequantized image)
   const float kQScale = 0.125f * 1.4426950408889634f * ksc;
   __shared__ __attribute__((aligned(16))) uint16_t qsh[16][72];
-  __shared__ float2 qln[16];
-  if (fold_q) {  // the statistics loaded beside the K batch, merged now (one row per half-wave)
-    const float2 st = row_ln_stats_merge2(lns, a.d >> 4);
-    const int rq = wave + 8 * (lane >> 5);
-    if ((lane & 31) == 0 && rq < nqt) qln[rq] = st;
-    __syncthreads();
+  if (fold_q) {
+    // (merged beside the projection, above)
   } else if (a.qS > 0 && a.ln_c1) {  // LN2 folded into the cross-q weights: the tile's row statistics, one wave per row
     for (int q = wave; q < nqt; q += NWV) {
       const float2 st = row_ln_from_stats(a.ln_stats + ((long)w * nq + i0 + q) * a.ln_ld, 1, a.d >> 4);
